@@ -1,0 +1,190 @@
+"""Benchmark: 1DVBC SpMV effective GB/s (and GFLOP/s) vs the MI355X HBM roofline (BASELINE.json).
+
+A step is one mul!(y, B', x) -- the transposed 1D-VBR product the reference's paper and benchmark
+time (bin/test_table.jl:80) -- over the NS-1DVBC workload of SURVEY.md §8d: a synthetic
+10^7 x 10^7 matrix with 1e8 nonzeros in 2.5e6 width-4 stripes (costs.jl:63-83 generator), fp64,
+inputs resident in HBM.  N ranks = N GPUs, one process each (torchrun); every rank owns its own
+block-row shard of that size (weak scaling, no data-path collective: the transposed product writes
+disjoint y ranges).  rank 0 prints one JSON line.
+
+    python bench.py [--gpus N --steps K --warmup W --workload ns|ns-mixed --dtype f64|f32]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes(B, esz, ti=4):
+    """SURVEY.md §8d, transposed: Tv·|val| + Ti·q + Ti·(3L+3) + Tx·m + Ty·n."""
+    nval = int(B.ofs[-1] - 1)
+    q = int(B.pos[-1] - 1)
+    L = len(B.Phi)
+    return esz * nval + ti * q + ti * (3 * L + 3) + esz * B.m + esz * B.n
+
+
+def load_traffic(workload, dtype):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
+    p = ROOT / "profiles" / f"pmc_{workload}_{dtype}.json"
+    if p.exists():
+        try:
+            d = json.loads(p.read_text())
+            return d.get("hbm_bytes_per_launch"), str(p.relative_to(ROOT))
+        except Exception:
+            pass
+    return None, None
+
+
+def cpu_baseline(B, x, esz, budget_s=12.0, max_reps=20):
+    """Oracle (C restatement of multiply_1DVBC.jl:85-180, OpenMP dynamic-1 stripe scheduling) on the
+    host cores, full-size product repeated until ~budget_s of CPU work; returns GB/s and details."""
+    from oracle import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    y = np.zeros(B.n, dtype=B.val.dtype)
+    O.mul(R, x, y, trans=True, nthreads=threads)  # warm-up (page faults)
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < max_reps and (time.perf_counter() - t_start) < budget_s:
+        t0 = time.perf_counter()
+        O.mul(R, x, y, trans=True, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return dict(value=round(algorithmic_bytes(B, esz) / t / 1e9, 3), unit="GB/s", cores=threads,
+                kind="port", sample=f"full workload, median of {len(times)} oracle mul!(y,B',x) "
+                                    f"runs ({t * 1e3:.1f} ms each), {threads} OpenMP threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="ns", choices=["ns", "ns-mixed"])
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import sparsematrixvbcs_amd as V
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    esz = np.dtype(dtype).itemsize
+    # each rank: its own block-row shard (different stripes), the same replicated x
+    B = V.synthetic.north_star(dtype=dtype, scale=args.scale, seed=0xDEADBEEF + rank,
+                               mixed=(args.workload == "ns-mixed"))
+    rng = np.random.default_rng(0xC0FFEE)
+    x_host = rng.uniform(-1, 1, B.m).astype(dtype)
+    x = torch.from_numpy(x_host).to(device)
+    y = torch.empty(B.n, dtype=x.dtype, device=device)
+    Bt = B.T
+    B.handle(local, True)  # build the HBM layout outside the timed region
+    stream = torch.cuda.current_stream(device)
+
+    for _ in range(args.warmup):
+        V.mul_(y, Bt, x)
+    torch.cuda.synchronize(device)
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        V.mul_(y, Bt, x)
+        ends[i].record(stream)
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    bytes_rank = algorithmic_bytes(B, esz)
+    nnz = int(np.count_nonzero(B.val))
+    stats = torch.tensor([elapsed, float(bytes_rank), float(nnz), kernel_ms], dtype=torch.float64, device=device)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, kernel_ms = mx[0].item(), mx[3].item()
+        total_bytes, total_nnz = sm[1].item(), sm[2].item()
+    else:
+        total_bytes, total_nnz = float(bytes_rank), float(nnz)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_bytes * args.steps / elapsed / 1e9
+    achieved = bytes_rank / (kernel_ms * 1e-3) / 1e9
+    workload = "NS-1DVBC-10Mx10M-1e8nnz-w4" if args.workload == "ns" else "NS-1DVBC-mixed-w1..8-1e8nnz"
+    if args.scale != 1.0:
+        workload += f"-scale{args.scale}"
+    traffic, traffic_src = load_traffic(args.workload, args.dtype)
+    out = {
+        "metric": "1DVBC SpMV effective GB/s (and GFLOP/s) vs HBM roofline, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (costs.jl:63-83 VBR generator, seed 0xDEADBEEF+rank; x ~ U[-1,1), seed 0xC0FFEE)",
+        "config": {
+            "workload": workload,
+            "op": "mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)",
+            "m": B.m, "n_per_rank": B.n, "stripes_per_rank": len(B.Phi), "row_blocks_per_rank": int(B.pos[-1] - 1),
+            "nnz_per_rank": nnz, "W": B.W, "index_bytes": 4,
+            "parallelism": f"stripe-shard x{world} (disjoint y, no collective)",
+        },
+        "gflops": round(2.0 * total_nnz * args.steps / elapsed / 1e9, 2),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "vbc::spmv_bins<T, 0>",
+            "bytes_per_launch": bytes_rank,
+            "avg_launch_ms": round(kernel_ms, 5),
+            "traffic_source": traffic_src,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(B, x_host, esz)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/*
+ * vbc.h -- C ABI of libvbc, the MI355X-native variable-block SpMV library.
+ *
+ * Drop-in boundary for SparseMatrixVBCs.jl's hot path (reference @ /root/reference, v0.1.12).
+ * Every entry point is what a Julia `ccall` shim would bind underneath the reference's own operator
+ * surface (see INTEGRATION.md for the binding).  Plain pointers and sizes only: no torch types,
+ * no C++ types.  All functions return an int status (vbc_status) and never throw.
+ *
+ * Index conventions at the boundary follow the Julia struct fields verbatim: 1-based Int64
+ * (`Ti = Int64`) arrays, exactly as SparseMatrix1DVBC{W,Tv,Ti} / SparseMatrixVBC{U,W,Tv,Ti} /
+ * SplitPartition{Ti} store them (SparseMatrixVBCs.jl:36-53, :62-82).  The library validates them and
+ * converts once, at create time, into its own 0-based int32 HBM layout.
+ */
+#ifndef VBC_H
+#define VBC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes.  The Julia shim maps them onto the reference's exceptions:
+ * DimensionMismatch (multiply_1DVBC.jl:44-45,139-140), ArgumentError (SparseMatrixVBCs.jl:45-50,
+ * :72-79) and AssertionError (constructors_1DVBC.jl:46, constructors_VBC.jl:59,65). */
+typedef enum vbc_status {
+    VBC_OK = 0,
+    VBC_DIM_MISMATCH = 1,      /* -> DimensionMismatch() */
+    VBC_INVALID_ARG = 2,       /* -> ArgumentError(msg) */
+    VBC_HIP_ERROR = 3,         /* -> ErrorException(msg) */
+    VBC_RCCL_ERROR = 4,        /* -> ErrorException(msg) */
+    VBC_UNSUPPORTED_DTYPE = 5, /* -> MethodError-like: no GPU kernel for this eltype */
+    VBC_ASSERTION = 6          /* -> AssertionError (w <= W, u <= U) */
+} vbc_status;
+
+/* Element types (Tv; x and y must have the same eltype as Tv on the GPU path). */
+typedef enum vbc_dtype { VBC_F64 = 0, VBC_F32 = 1 } vbc_dtype;
+
+/* Where x / y live for vbc_mul / vbc_mul_mat. */
+typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
+
+/* create flags */
+#define VBC_CREATE_TRANSPOSED 0x1u /* build the layout for mul!(y, B', x)  (default if 0 given) */
+#define VBC_CREATE_FORWARD 0x2u    /* build the layout for mul!(y, B, x)                         */
+
+/* mul flags */
+#define VBC_MUL_REFERENCE_QUIRKS 0x1u /* reproduce the reference bit-for-bit in alpha/beta:
+                                         forward drops alpha (multiply_1DVBC.jl:48,
+                                         multiply_VBC.jl:55-57); transposed overwrites y, ignoring
+                                         alpha and beta (multiply_1DVBC.jl:114-116,
+                                         multiply_VBC.jl:117-121).  Default (0) is BLAS:
+                                         y = alpha*op(B)*x + beta*y.  Both agree at (1, 0). */
+
+typedef struct vbc_handle vbc_handle; /* opaque; immutable after create */
+
+/* ---------------------------------------------------------------------------------------------
+ * Handles (device-resident matrices)
+ * ------------------------------------------------------------------------------------------- */
+
+/* SparseMatrix1DVBC{W,Tv,Int64}(m, n, Φ, pos, idx, ofs, val)  (SparseMatrixVBCs.jl:36-53).
+ * spl[L+1] = Φ.spl, pos[L+1], idx[pos[L+1]-1], ofs[L+1]: 1-based Int64.  val has nval >=
+ * ofs[L+1]-1 elements (the reference's SIMD tail pad, constructors_1DVBC.jl:35-39, is ignored).
+ * `device` is the HIP ordinal; `flags` selects which product layouts to build (0 = transposed). */
+int vbc1d_create(vbc_handle **out, int64_t m, int64_t n, int64_t W, int64_t L, const int64_t *spl,
+                 const int64_t *pos, const int64_t *idx, const int64_t *ofs, const void *val,
+                 int64_t nval, int dtype, int device, unsigned flags);
+
+/* SparseMatrixVBC{U,W,Tv,Int64}(m, n, Π, Φ, pos, idx, ofs, val)  (SparseMatrixVBCs.jl:62-82).
+ * pspl[K+1] = Π.spl; idx holds block-row ids k (constructors_VBC.jl:123). */
+int vbc2d_create(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K,
+                 const int64_t *pspl, int64_t L, const int64_t *spl, const int64_t *pos,
+                 const int64_t *idx, const int64_t *ofs, const void *val, int64_t nval, int dtype,
+                 int device, unsigned flags);
+
+/* SparseMatrixCSC{Tv,Int64} (colptr[n+1], rowval, nzval), the operand of TrSpMV!(y, A, x)
+ * (TrSpMV.jl:1-20).  Internally a 1DVBC with unit-width stripes. */
+int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t *colptr,
+                   const int64_t *rowval, const void *nzval, int dtype, int device, unsigned flags);
+
+int vbc_destroy(vbc_handle *h);
+
+/* ---------------------------------------------------------------------------------------------
+ * Products
+ * ------------------------------------------------------------------------------------------- */
+
+/* mul!(y, B, x, α, β) (trans = 0; multiply_1DVBC.jl:9-83, multiply_VBC.jl:3-87) or
+ * mul!(y, B', x, α, β) (trans = 1; multiply_1DVBC.jl:85-180, multiply_VBC.jl:89-192, and
+ * TrSpMV!(y, A, x) for a CSC handle, TrSpMV.jl:1-20).  Adjoint and Transpose are identical (real
+ * eltypes only).  nx / ny are length(x) / length(y): a mismatch returns VBC_DIM_MISMATCH before any
+ * work.  mem = VBC_MEM_DEVICE: x, y are device pointers on the handle's device, and the product is
+ * enqueued on `stream` (a hipStream_t; NULL = null stream) without synchronising.
+ * mem = VBC_MEM_HOST: x, y are host pointers; the call stages them and returns when y is final.
+ * x and y must not alias (the reference has the same precondition). */
+int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
+            double beta, int mem, void *stream, unsigned flags);
+
+/* Multi-RHS Y = α·op(B)·X + β·Y with X, Y column-major (ldx, ldy >= rows).  The reference has no
+ * matrix mul! (Base.:* forwards to an undefined method, multiply_1DVBC.jl:184-185), so its
+ * semantics is defined column by column as vbc_mul. */
+int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t ldx, int64_t nx,
+                void *Y, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
+                unsigned flags);
+
+/* ---------------------------------------------------------------------------------------------
+ * Introspection (for the Julia shim's size(), and for roofline accounting in bench.py)
+ * ------------------------------------------------------------------------------------------- */
+typedef struct vbc_info {
+    int64_t m, n;          /* size(A) */
+    int64_t L;             /* stripes */
+    int64_t K;             /* block rows (2D), 0 for 1D */
+    int64_t nblocks;       /* stored row-blocks q (2D: stored u×w tiles) */
+    int64_t nrows;         /* stored w-wide rows after 2D expansion (== nblocks for 1D) */
+    int64_t nval;          /* |val| = ofs[L+1]-1 (includes fill zeros) */
+    int64_t nnz_hint;      /* nonzeros of val (useful flops = 2*nnz_hint) */
+    int32_t dtype;
+    int32_t device;
+    int32_t bins_t, bins_f; /* kernel bins built for each direction (0 = layout absent) */
+    int64_t device_bytes;   /* HBM held by the handle */
+    int64_t bytes_t;        /* HBM bytes one transposed product moves in this layout */
+    int64_t bytes_f;        /* same for the forward product */
+} vbc_info;
+
+int vbc_get_info(const vbc_handle *h, vbc_info *info);
+
+/* Copies the thread's last error message (NUL-terminated, truncated to n). Returns its length. */
+int vbc_last_error(char *buf, size_t n);
+
+/* Library version (major*10000 + minor*100 + patch). */
+int vbc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBC_H */

@@ -1,0 +1,29 @@
+"""sparsematrixvbcs.jl_amd -- MI355X-native variable-block SpMV behind SparseMatrixVBCs.jl's surface.
+
+Host mirror (Python stands in for the absent Julia host) of the reference's operator API:
+SparseMatrix1DVBC / SparseMatrixVBC / mul! / TrSpMV! / Base.:*, over libvbc's C ABI
+(include/vbc.h), whose hand-written gfx950 kernels do every product.  Import it as
+`sparsematrixvbcs_amd` (the repo-root loader) since the directory name is not an identifier.
+"""
+from . import _lib, synthetic
+from ._lib import ArgumentError, DimensionMismatch, HIPError, UnsupportedDtype
+from .matrices import (DEFAULT_SIMD_SIZE, Adjoint, SparseMatrix1DVBC, SparseMatrixCSC, SparseMatrixVBC,
+                       Transpose, adjoint, transpose)
+from .multiply import TrSpMV_, matmul, mul_, mulmat_
+from .partition import (AlternatePacker, AlternatingPacker, ConstrainedCost, DynamicTotalChunker,
+                        EquiChunker, OverlapChunker, SplitPartition, StrictChunker, VertexCount,
+                        model_SparseMatrix1DVBC_blocks, model_SparseMatrix1DVBC_memory, pack_plaid,
+                        pack_stripe)
+
+# Julia spellings
+globals()["mul!"] = mul_
+globals()["TrSpMV!"] = TrSpMV_
+
+__all__ = [
+    "SparseMatrix1DVBC", "SparseMatrixVBC", "SparseMatrixCSC", "Adjoint", "Transpose", "adjoint",
+    "transpose", "mul_", "mulmat_", "matmul", "TrSpMV_", "SplitPartition", "EquiChunker",
+    "StrictChunker", "OverlapChunker", "DynamicTotalChunker", "ConstrainedCost", "VertexCount",
+    "AlternatingPacker", "AlternatePacker", "pack_stripe", "pack_plaid",
+    "model_SparseMatrix1DVBC_blocks", "model_SparseMatrix1DVBC_memory", "DimensionMismatch",
+    "ArgumentError", "HIPError", "UnsupportedDtype", "DEFAULT_SIMD_SIZE",
+]

@@ -1,0 +1,126 @@
+"""ctypes binding of libvbc (include/vbc.h, include/vbc_host.h).
+
+The product path has no fallback: if libvbc.so is missing or cannot be loaded, every product call
+raises.  Status codes map onto the reference's exception types (vbc.h `vbc_status`).
+"""
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("VBC_LIBRARY", PKG_DIR / "libvbc.so"))
+
+VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR, VBC_UNSUPPORTED_DTYPE, \
+    VBC_ASSERTION = range(7)
+VBC_F64, VBC_F32 = 0, 1
+VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
+VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD = 0x1, 0x2
+VBC_MUL_REFERENCE_QUIRKS = 0x1
+
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = (
+    "vbc1d_create", "vbc2d_create", "vbc_csc_create", "vbc_destroy", "vbc_mul", "vbc_mul_mat",
+    "vbc_get_info", "vbc_last_error", "vbc_version",
+    "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
+    "vbcx_partition_dynamic", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
+    "vbcx_vbc_fill", "vbcx_transpose_pattern",
+)
+
+
+class DimensionMismatch(ValueError):
+    """Julia's DimensionMismatch (multiply_1DVBC.jl:44-45,139-140)."""
+
+
+class ArgumentError(ValueError):
+    """Julia's ArgumentError (SparseMatrixVBCs.jl:45-50,72-79)."""
+
+
+class HIPError(RuntimeError):
+    pass
+
+
+class UnsupportedDtype(TypeError):
+    pass
+
+
+class vbc_info(C.Structure):
+    _fields_ = [("m", C.c_int64), ("n", C.c_int64), ("L", C.c_int64), ("K", C.c_int64),
+                ("nblocks", C.c_int64), ("nrows", C.c_int64), ("nval", C.c_int64),
+                ("nnz_hint", C.c_int64), ("dtype", C.c_int32), ("device", C.c_int32),
+                ("bins_t", C.c_int32), ("bins_f", C.c_int32), ("device_bytes", C.c_int64),
+                ("bytes_t", C.c_int64), ("bytes_f", C.c_int64)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libvbc.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(f"libvbc.so not found at {LIB_PATH}; build it with `make -C {PKG_DIR}` "
+                              "or __graft_entry__.build()")
+        L = C.CDLL(str(LIB_PATH))
+        P, I64, INT, U, D = C.c_void_p, C.c_int64, C.c_int, C.c_uint, C.c_double
+        L.vbc1d_create.argtypes = [C.POINTER(P), I64, I64, I64, I64, P, P, P, P, P, I64, INT, INT, U]
+        L.vbc2d_create.argtypes = [C.POINTER(P), I64, I64, I64, I64, I64, P, I64, P, P, P, P, P, I64,
+                                   INT, INT, U]
+        L.vbc_csc_create.argtypes = [C.POINTER(P), I64, I64, P, P, P, INT, INT, U]
+        L.vbc_destroy.argtypes = [P]
+        L.vbc_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
+        L.vbc_mul_mat.argtypes = [P, INT, I64, P, I64, I64, P, I64, I64, D, D, INT, P, U]
+        L.vbc_get_info.argtypes = [P, C.POINTER(vbc_info)]
+        L.vbc_last_error.argtypes = [C.c_char_p, C.c_size_t]
+        L.vbcx_partition_equi.argtypes = [I64, I64, P, P]
+        L.vbcx_partition_strict.argtypes = [I64, I64, P, P, I64, P, P]
+        L.vbcx_partition_overlap.argtypes = [I64, I64, P, P, D, I64, P, P]
+        L.vbcx_partition_dynamic.argtypes = [I64, I64, P, P, I64, D, D, D, D, D, P, P]
+        L.vbcx_1dvbc_count.argtypes = [I64, I64, P, P, I64, P, P, P]
+        L.vbcx_1dvbc_fill.argtypes = [I64, I64, I64, P, P, P, INT, I64, P, P, P, P, P, I64]
+        L.vbcx_vbc_count.argtypes = [I64, I64, P, P, I64, P, I64, P, P, P]
+        L.vbcx_vbc_fill.argtypes = [I64, I64, I64, I64, P, P, P, INT, I64, P, I64, P, P, P, P, P, I64]
+        L.vbcx_transpose_pattern.argtypes = [I64, I64, P, P, P, P]
+        _lib = L
+    return _lib
+
+
+def last_error():
+    buf = C.create_string_buffer(1024)
+    lib().vbc_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def check(status, what=""):
+    if status == VBC_OK:
+        return
+    msg = f"{what}: {last_error()}" if what else last_error()
+    if status == VBC_DIM_MISMATCH:
+        raise DimensionMismatch(msg)
+    if status == VBC_INVALID_ARG:
+        raise ArgumentError(msg)
+    if status == VBC_ASSERTION:
+        raise AssertionError(msg)
+    if status == VBC_UNSUPPORTED_DTYPE:
+        raise UnsupportedDtype(msg)
+    raise HIPError(msg)
+
+
+def ptr(a):
+    """Address of a numpy array's data, a torch tensor's storage, or None."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+def dtype_code(dtype):
+    dtype = np.dtype(dtype)
+    if dtype == np.float64:
+        return VBC_F64
+    if dtype == np.float32:
+        return VBC_F32
+    raise UnsupportedDtype(f"the GPU path supports Float64 / Float32 eltypes, got {dtype}")

@@ -1,0 +1,319 @@
+// libvbc host-side layout producers: partitioners and CSC -> reference-layout builders.
+//
+// The builders produce the exact field arrays of the reference's constructors
+// (constructors_1DVBC.jl:9-92, constructors_VBC.jl:15-133) but by a different algorithm: instead of
+// the reference's w-way column merge, each stripe's distinct rows (or block rows) are collected with
+// a stamp array, sorted, given slots, and the stripe's entries are scattered into their slots.  The
+// oracle (oracle/vbc_oracle.c) restates the merge line by line; tests require both to agree
+// exactly, which pins this implementation.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "vbc_host.h"
+#include "vbc_internal.h"
+
+using vbc::fail;
+
+namespace {
+
+int check_csc(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval)
+{
+    if (m < 0 || n < 0) return fail(VBC_INVALID_ARG, "number of rows/columns must be >= 0");
+    if (!colptr) return fail(VBC_INVALID_ARG, "colptr is NULL");
+    if (colptr[0] != 1) return fail(VBC_INVALID_ARG, "colptr[1] must be 1");
+    for (int64_t j = 0; j < n; j++) {
+        if (colptr[j + 1] < colptr[j]) return fail(VBC_INVALID_ARG, "colptr must be non-decreasing");
+        for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+            const int64_t i = rowval[p];
+            if (i < 1 || i > m) return fail(VBC_INVALID_ARG, "rowval out of range 1:m");
+            if (p > colptr[j] - 1 && rowval[p - 1] >= i)
+                return fail(VBC_INVALID_ARG, "rowval must be strictly increasing within a column");
+        }
+    }
+    return VBC_OK;
+}
+
+int check_spl(int64_t n, int64_t L, const int64_t *spl, int64_t W, bool assert_w)
+{
+    if (L < 0) return fail(VBC_INVALID_ARG, "L must be >= 0");
+    if (spl[0] != 1 || spl[L] != n + 1) return fail(VBC_INVALID_ARG, "spl must run from 1 to n+1");
+    for (int64_t l = 0; l < L; l++) {
+        const int64_t w = spl[l + 1] - spl[l];
+        if (w < 1) return fail(VBC_INVALID_ARG, "spl must be strictly increasing");
+        if (assert_w && w > W) return fail(VBC_ASSERTION, "AssertionError: w <= W");
+    }
+    return VBC_OK;
+}
+
+template <typename T>
+int fill_1d(int64_t m, int64_t W, const int64_t *colptr, const int64_t *rowval, const T *nzval,
+            int64_t L, const int64_t *spl, const int64_t *pos, const int64_t *ofs, int64_t *idx,
+            T *val, int64_t pad)
+{
+    std::vector<int64_t> stamp(m, 0), slot(m, 0), rows;
+    const int64_t nv = ofs[L] - 1;
+    std::fill(val, val + nv + pad, T(0));
+    for (int64_t l = 0; l < L; l++) {
+        const int64_t j0 = spl[l] - 1, j1 = spl[l + 1] - 1, w = j1 - j0;
+        if (w > W) return fail(VBC_ASSERTION, "AssertionError: w <= W");
+        rows.clear();
+        for (int64_t j = j0; j < j1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t i = rowval[p] - 1;
+                if (stamp[i] != l + 1) { stamp[i] = l + 1; rows.push_back(i); }
+            }
+        std::sort(rows.begin(), rows.end());
+        if ((int64_t)rows.size() != pos[l + 1] - pos[l])
+            return fail(VBC_INVALID_ARG, "pos inconsistent with A and spl");
+        for (size_t s = 0; s < rows.size(); s++) {
+            slot[rows[s]] = (int64_t)s;
+            idx[pos[l] - 1 + (int64_t)s] = rows[s] + 1;
+        }
+        T *seg = val + (ofs[l] - 1);
+        for (int64_t j = j0; j < j1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++)
+                seg[slot[rowval[p] - 1] * w + (j - j0)] = nzval[p];
+    }
+    return VBC_OK;
+}
+
+template <typename T>
+int fill_2d(int64_t m, int64_t U, int64_t W, const int64_t *colptr, const int64_t *rowval,
+            const T *nzval, int64_t K, const int64_t *pspl, int64_t L, const int64_t *spl,
+            const int64_t *pos, const int64_t *ofs, int64_t *idx, T *val, int64_t pad)
+{
+    std::vector<int64_t> asg(m), stamp(K, 0), boff(K, 0), blocks;
+    for (int64_t k = 0; k < K; k++) {
+        if (pspl[k + 1] - pspl[k] > U) return fail(VBC_ASSERTION, "AssertionError: u <= U");
+        for (int64_t i = pspl[k] - 1; i < pspl[k + 1] - 1; i++) asg[i] = k;
+    }
+    const int64_t nv = ofs[L] - 1;
+    std::fill(val, val + nv + pad, T(0));
+    for (int64_t l = 0; l < L; l++) {
+        const int64_t j0 = spl[l] - 1, j1 = spl[l + 1] - 1, w = j1 - j0;
+        if (w > W) return fail(VBC_ASSERTION, "AssertionError: w <= W");
+        blocks.clear();
+        for (int64_t j = j0; j < j1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t k = asg[rowval[p] - 1];
+                if (stamp[k] != l + 1) { stamp[k] = l + 1; blocks.push_back(k); }
+            }
+        std::sort(blocks.begin(), blocks.end());
+        if ((int64_t)blocks.size() != pos[l + 1] - pos[l])
+            return fail(VBC_INVALID_ARG, "pos inconsistent with A, Π and Φ");
+        int64_t off = 0;
+        for (size_t s = 0; s < blocks.size(); s++) {
+            const int64_t k = blocks[s];
+            boff[k] = off;
+            off += (pspl[k + 1] - pspl[k]) * w;
+            idx[pos[l] - 1 + (int64_t)s] = k + 1;
+        }
+        if (off != ofs[l + 1] - ofs[l]) return fail(VBC_INVALID_ARG, "ofs inconsistent");
+        T *seg = val + (ofs[l] - 1);
+        for (int64_t j = j0; j < j1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t i = rowval[p] - 1, k = asg[i];
+                seg[boff[k] + (i - (pspl[k] - 1)) * w + (j - j0)] = nzval[p];
+            }
+    }
+    return VBC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vbcx_partition_equi(int64_t n, int64_t w, int64_t *spl, int64_t *L)
+{
+    if (n < 0 || w < 1) return fail(VBC_INVALID_ARG, "EquiChunker: need n >= 0 and w >= 1");
+    int64_t l = 0;
+    for (int64_t j = 1; j <= n; j += w) spl[l++] = j;
+    spl[l] = n + 1;
+    *L = l;
+    return VBC_OK;
+}
+
+int vbcx_partition_strict(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                          int64_t W, int64_t *spl, int64_t *L)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (W < 1) return fail(VBC_INVALID_ARG, "W must be > 0");
+    int64_t l = 0, first = 0;
+    for (int64_t j = 0; j < n; j++) {
+        bool join = false;
+        if (j > 0 && j - first < W) {
+            const int64_t a0 = colptr[first] - 1, a1 = colptr[first + 1] - 1;
+            const int64_t b0 = colptr[j] - 1, b1 = colptr[j + 1] - 1;
+            join = (a1 - a0 == b1 - b0) && std::equal(rowval + a0, rowval + a1, rowval + b0);
+        }
+        if (!join) { spl[l++] = j + 1; first = j; }
+    }
+    spl[l] = n + 1;
+    *L = l;
+    return VBC_OK;
+}
+
+int vbcx_partition_overlap(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                           double rho, int64_t W, int64_t *spl, int64_t *L)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (W < 1 || !(rho >= 0.0 && rho <= 1.0)) return fail(VBC_INVALID_ARG, "need W > 0, 0 <= rho <= 1");
+    std::vector<int64_t> stamp(m, -1);
+    int64_t l = 0, first = 0, nfirst = 0;
+    for (int64_t j = 0; j < n; j++) {
+        const int64_t b0 = colptr[j] - 1, b1 = colptr[j + 1] - 1, nb = b1 - b0;
+        bool join = false;
+        if (j > 0 && j - first < W) {
+            int64_t common = 0;
+            for (int64_t p = b0; p < b1; p++) common += (stamp[rowval[p] - 1] == first);
+            join = (double)common >= rho * (double)std::max(nb, nfirst);
+        }
+        if (!join) {
+            spl[l++] = j + 1;
+            first = j;
+            nfirst = nb;
+            for (int64_t p = b0; p < b1; p++) stamp[rowval[p] - 1] = first;
+        }
+    }
+    spl[l] = n + 1;
+    *L = l;
+    return VBC_OK;
+}
+
+int vbcx_partition_dynamic(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                           int64_t W, double c_stripe, double c_col, double c_pin, double c_row,
+                           double c_cell, int64_t *spl, int64_t *L)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (W < 1) return fail(VBC_INVALID_ARG, "W must be > 0");
+    const double inf = std::numeric_limits<double>::infinity();
+    std::vector<double> f(n + 1, inf);
+    std::vector<int64_t> back(n + 1, 0), stamp(m, -1);
+    f[0] = 0.0;
+    for (int64_t e = 1; e <= n; e++) {
+        int64_t rows = 0, pins = 0;
+        for (int64_t w = 1; w <= W && w <= e; w++) {
+            const int64_t j = e - w;  // add column j (0-based) to the stripe [j, e)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t i = rowval[p] - 1;
+                if (stamp[i] != e) { stamp[i] = e; rows++; }
+            }
+            pins += colptr[j + 1] - colptr[j];
+            const double c = c_stripe + c_col * w + c_pin * pins + c_row * rows + c_cell * w * rows;
+            if (f[j] + c < f[e]) { f[e] = f[j] + c; back[e] = j; }  // ties keep the widest stripe
+        }
+    }
+    std::vector<int64_t> cuts;
+    for (int64_t e = n; e > 0; e = back[e]) cuts.push_back(back[e]);
+    int64_t l = 0;
+    for (auto it = cuts.rbegin(); it != cuts.rend(); ++it) spl[l++] = *it + 1;
+    spl[l] = n + 1;
+    *L = l;
+    return VBC_OK;
+}
+
+int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
+                     const int64_t *spl, int64_t *pos, int64_t *ofs)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (int st = check_spl(n, L, spl, 0, false)) return st;
+    std::vector<int64_t> stamp(m, 0);
+    pos[0] = 1;
+    ofs[0] = 1;
+    for (int64_t l = 0; l < L; l++) {
+        int64_t rows = 0;
+        for (int64_t j = spl[l] - 1; j < spl[l + 1] - 1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t i = rowval[p] - 1;
+                if (stamp[i] != l + 1) { stamp[i] = l + 1; rows++; }
+            }
+        pos[l + 1] = pos[l] + rows;
+        ofs[l + 1] = ofs[l] + rows * (spl[l + 1] - spl[l]);
+    }
+    return VBC_OK;
+}
+
+int vbcx_1dvbc_fill(int64_t m, int64_t n, int64_t W, const int64_t *colptr, const int64_t *rowval,
+                    const void *nzval, int dtype, int64_t L, const int64_t *spl, const int64_t *pos,
+                    const int64_t *ofs, int64_t *idx, void *val, int64_t pad)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (W < 1) return fail(VBC_INVALID_ARG, "W must be > 0");
+    if (int st = check_spl(n, L, spl, W, true)) return st;
+    if (pad < 0) return fail(VBC_INVALID_ARG, "pad must be >= 0");
+    if (dtype == VBC_F64)
+        return fill_1d(m, W, colptr, rowval, (const double *)nzval, L, spl, pos, ofs, idx,
+                       (double *)val, pad);
+    if (dtype == VBC_F32)
+        return fill_1d(m, W, colptr, rowval, (const float *)nzval, L, spl, pos, ofs, idx,
+                       (float *)val, pad);
+    return fail(VBC_UNSUPPORTED_DTYPE, "dtype must be VBC_F64 or VBC_F32");
+}
+
+int vbcx_vbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t K,
+                   const int64_t *pspl, int64_t L, const int64_t *spl, int64_t *pos, int64_t *ofs)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (int st = check_spl(n, L, spl, 0, false)) return st;
+    if (int st = check_spl(m, K, pspl, 0, false)) return st;
+    std::vector<int64_t> asg(m), stamp(K, 0);
+    for (int64_t k = 0; k < K; k++)
+        for (int64_t i = pspl[k] - 1; i < pspl[k + 1] - 1; i++) asg[i] = k;
+    pos[0] = 1;
+    ofs[0] = 1;
+    for (int64_t l = 0; l < L; l++) {
+        const int64_t w = spl[l + 1] - spl[l];
+        int64_t nb = 0, nv = 0;
+        for (int64_t j = spl[l] - 1; j < spl[l + 1] - 1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t k = asg[rowval[p] - 1];
+                if (stamp[k] != l + 1) {
+                    stamp[k] = l + 1;
+                    nb++;
+                    nv += (pspl[k + 1] - pspl[k]) * w;
+                }
+            }
+        pos[l + 1] = pos[l] + nb;
+        ofs[l + 1] = ofs[l] + nv;
+    }
+    return VBC_OK;
+}
+
+int vbcx_vbc_fill(int64_t m, int64_t n, int64_t U, int64_t W, const int64_t *colptr,
+                  const int64_t *rowval, const void *nzval, int dtype, int64_t K,
+                  const int64_t *pspl, int64_t L, const int64_t *spl, const int64_t *pos,
+                  const int64_t *ofs, int64_t *idx, void *val, int64_t pad)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (U < 1 || W < 1) return fail(VBC_INVALID_ARG, "U and W must be > 0");
+    if (int st = check_spl(n, L, spl, W, true)) return st;
+    if (int st = check_spl(m, K, pspl, U, true)) return st;
+    if (pad < 0) return fail(VBC_INVALID_ARG, "pad must be >= 0");
+    if (dtype == VBC_F64)
+        return fill_2d(m, U, W, colptr, rowval, (const double *)nzval, K, pspl, L, spl, pos, ofs,
+                       idx, (double *)val, pad);
+    if (dtype == VBC_F32)
+        return fill_2d(m, U, W, colptr, rowval, (const float *)nzval, K, pspl, L, spl, pos, ofs,
+                       idx, (float *)val, pad);
+    return fail(VBC_UNSUPPORTED_DTYPE, "dtype must be VBC_F64 or VBC_F32");
+}
+
+int vbcx_transpose_pattern(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                           int64_t *rowptr, int64_t *colval)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    std::fill(rowptr, rowptr + m + 1, 0);
+    for (int64_t p = 0; p < colptr[n] - 1; p++) rowptr[rowval[p]]++;
+    rowptr[0] = 1;
+    for (int64_t i = 0; i < m; i++) rowptr[i + 1] += rowptr[i];
+    std::vector<int64_t> next(rowptr, rowptr + m);
+    for (int64_t j = 0; j < n; j++)
+        for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++)
+            colval[(next[rowval[p] - 1]++) - 1] = j + 1;
+    return VBC_OK;
+}
+
+}  // extern "C"

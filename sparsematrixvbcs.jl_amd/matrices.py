@@ -1,0 +1,283 @@
+"""SparseMatrix1DVBC / SparseMatrixVBC / SparseMatrixCSC mirrors of the reference types.
+
+Fields are the reference's, verbatim: 1-based int64 `spl`/`pos`/`idx`/`ofs` and a `val` vector with
+the SIMD tail pad (SparseMatrixVBCs.jl:36-53, :62-82; constructors_1DVBC.jl:35-39).  The host arrays
+are what a Julia caller owns; the GPU copy lives behind a libvbc handle created on first use per
+(device, direction) and released with the object.
+"""
+import ctypes as C
+import weakref
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _lib as _L
+from .partition import (DynamicTotalChunker, SplitPartition, model_SparseMatrix1DVBC_memory,
+                        pack_plaid, pack_stripe, AlternatingPacker, EquiChunker)
+
+DEFAULT_SIMD_SIZE = 64  # CpuId.simdbytes() on the AVX-512 hosts the reference was run on
+
+
+def _simd_pad(W, dtype, U=1):
+    dw = max(1, DEFAULT_SIMD_SIZE // np.dtype(dtype).itemsize)
+    return U * dw * (-(-W // dw))
+
+
+def _value_dtype(A):
+    """Bool / integer matrices are promoted to Float64 (exact for |v| < 2^53); fp32 stays fp32."""
+    if A.dtype == np.float32:
+        return np.float32
+    if A.dtype == np.float64 or A.dtype.kind in "biu":
+        return np.float64
+    raise _L.UnsupportedDtype(f"eltype {A.dtype} has no GPU kernel")
+
+
+def _csc_fields(A):
+    A = sp.csc_matrix(A)
+    A.sum_duplicates()
+    A.sort_indices()
+    colptr = np.ascontiguousarray(A.indptr, dtype=np.int64) + 1
+    rowval = np.ascontiguousarray(A.indices, dtype=np.int64) + 1
+    nzval = np.ascontiguousarray(A.data, dtype=_value_dtype(A))
+    return A.shape, colptr, rowval, nzval
+
+
+class _Handles:
+    """libvbc handles of one matrix, keyed by (device, create flags)."""
+
+    def __init__(self):
+        self.h = {}
+
+    def get(self, key, create):
+        if key not in self.h:
+            hp = C.c_void_p()
+            _L.check(create(C.byref(hp)), "create")
+            self.h[key] = hp
+        return self.h[key]
+
+    def release(self):
+        if _L._lib is not None:
+            for hp in self.h.values():
+                _L._lib.vbc_destroy(hp)
+        self.h.clear()
+
+
+class _DeviceMatrix:
+    """Shared handle management for the three matrix mirrors."""
+
+    def _init_handles(self):
+        self._handles = _Handles()
+        self._finalizer = weakref.finalize(self, _Handles.release, self._handles)
+
+    def handle(self, device=0, trans=True):
+        flags = _L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD
+        return self._handles.get((int(device), flags), lambda out: self._create(out, int(device), flags))
+
+    def info(self, device=0, trans=True):
+        inf = _L.vbc_info()
+        _L.check(_L.lib().vbc_get_info(self.handle(device, trans), C.byref(inf)), "info")
+        return {f: getattr(inf, f) for f, _ in _L.vbc_info._fields_}
+
+    def release(self):
+        self._handles.release()
+
+    @property
+    def shape(self):
+        return (self.m, self.n)
+
+    def size(self, dim=None):
+        return self.shape if dim is None else self.shape[dim - 1]
+
+    @property
+    def dtype(self):
+        return self.val.dtype
+
+    # adjoint / transpose views (LinearAlgebra.Adjoint / Transpose)
+    @property
+    def T(self):
+        return Transpose(self)
+
+    def adjoint(self):
+        return Adjoint(self)
+
+    def __matmul__(self, x):
+        from .multiply import matmul
+        return matmul(self, x)
+
+
+class SparseMatrix1DVBC(_DeviceMatrix):
+    """SparseMatrix1DVBC{W,Tv,Ti} (SparseMatrixVBCs.jl:36-53).
+
+    Construct like the reference:
+        SparseMatrix1DVBC[W](A)                 default partitioner (constructors_1DVBC.jl:1-7)
+        SparseMatrix1DVBC[W](A, method)         pack_stripe(A, method)
+        SparseMatrix1DVBC[W](A, Φ)              given SplitPartition (constructors_1DVBC.jl:9)
+        SparseMatrix1DVBC(W, m, n, Φ, pos, idx, ofs, val)   inner constructor (:44)
+    """
+
+    def __class_getitem__(cls, W):
+        return lambda *a, **k: cls.from_csc(W, *a, **k)
+
+    def __init__(self, W, m, n, Phi, pos, idx, ofs, val):
+        if m < 0:
+            raise _L.ArgumentError(f"number of rows (m) must be ≥ 0, got {m}")
+        if n < 0:
+            raise _L.ArgumentError(f"number of columns (n) must be ≥ 0, got {n}")
+        if not isinstance(W, (int, np.integer)):
+            raise _L.ArgumentError("W must be an Int")
+        if W <= 0:
+            raise _L.ArgumentError("W must be > 0")
+        self.W, self.m, self.n = int(W), int(m), int(n)
+        self.Phi = Phi if isinstance(Phi, SplitPartition) else SplitPartition(Phi)
+        self.pos = np.ascontiguousarray(pos, dtype=np.int64)
+        self.idx = np.ascontiguousarray(idx, dtype=np.int64)
+        self.ofs = np.ascontiguousarray(ofs, dtype=np.int64)
+        self.val = np.ascontiguousarray(val)
+        self._init_handles()
+
+    @classmethod
+    def from_csc(cls, W, A, method=None, dtype=None):
+        if method is None:
+            method = DynamicTotalChunker(model_SparseMatrix1DVBC_memory(np.float64, np.int64), W)
+        Phi = method if isinstance(method, SplitPartition) else pack_stripe(A, method)
+        (m, n), colptr, rowval, nzval = _csc_fields(A)
+        if dtype is not None:
+            nzval = nzval.astype(dtype)
+        lib = _L.lib()
+        L = len(Phi)
+        pos = np.zeros(L + 1, np.int64)
+        ofs = np.zeros(L + 1, np.int64)
+        _L.check(lib.vbcx_1dvbc_count(m, n, colptr.ctypes.data, rowval.ctypes.data, L, Phi.spl.ctypes.data,
+                                      pos.ctypes.data, ofs.ctypes.data), "SparseMatrix1DVBC")
+        pad = _simd_pad(W, nzval.dtype)
+        idx = np.zeros(pos[-1] - 1, np.int64)
+        val = np.zeros(ofs[-1] - 1 + pad, nzval.dtype)
+        _L.check(lib.vbcx_1dvbc_fill(m, n, W, colptr.ctypes.data, rowval.ctypes.data, nzval.ctypes.data,
+                                     _L.dtype_code(nzval.dtype), L, Phi.spl.ctypes.data, pos.ctypes.data,
+                                     ofs.ctypes.data, idx.ctypes.data, val.ctypes.data, pad),
+                 "SparseMatrix1DVBC")
+        return cls(W, m, n, Phi, pos, idx, ofs, val)
+
+    def _create(self, out, device, flags):
+        spl = self.Phi.spl
+        return _L.lib().vbc1d_create(out, self.m, self.n, self.W, len(self.Phi), spl.ctypes.data,
+                                     self.pos.ctypes.data, self.idx.ctypes.data, self.ofs.ctypes.data,
+                                     self.val.ctypes.data, len(self.val), _L.dtype_code(self.val.dtype),
+                                     device, flags)
+
+    def __repr__(self):
+        return (f"SparseMatrix1DVBC{{{self.W},{self.val.dtype},Int64}}({self.m}×{self.n}, "
+                f"{len(self.Phi)} stripes, {len(self.idx)} row-blocks)")
+
+
+class SparseMatrixVBC(_DeviceMatrix):
+    """SparseMatrixVBC{U,W,Tv,Ti} (SparseMatrixVBCs.jl:62-82); idx holds block-row ids.
+
+        SparseMatrixVBC[U, W](A)            default packer (constructors_VBC.jl:1-8)
+        SparseMatrixVBC[U, W](A, method)    pack_plaid(A, method)
+        SparseMatrixVBC[U, W](A, Π, Φ)      given partitions (constructors_VBC.jl:15)
+    """
+
+    def __class_getitem__(cls, UW):
+        U, W = UW
+        return lambda *a, **k: cls.from_csc(U, W, *a, **k)
+
+    def __init__(self, U, W, m, n, Pi, Phi, pos, idx, ofs, val):
+        if m < 0:
+            raise _L.ArgumentError(f"number of rows (m) must be ≥ 0, got {m}")
+        if n < 0:
+            raise _L.ArgumentError(f"number of columns (n) must be ≥ 0, got {n}")
+        for name, v in (("U", U), ("W", W)):
+            if not isinstance(v, (int, np.integer)):
+                raise _L.ArgumentError(f"{name} must be an Int")
+            if v <= 0:
+                raise _L.ArgumentError(f"{name} must be > 0")
+        self.U, self.W, self.m, self.n = int(U), int(W), int(m), int(n)
+        self.Pi = Pi if isinstance(Pi, SplitPartition) else SplitPartition(Pi)
+        self.Phi = Phi if isinstance(Phi, SplitPartition) else SplitPartition(Phi)
+        self.pos = np.ascontiguousarray(pos, dtype=np.int64)
+        self.idx = np.ascontiguousarray(idx, dtype=np.int64)
+        self.ofs = np.ascontiguousarray(ofs, dtype=np.int64)
+        self.val = np.ascontiguousarray(val)
+        self._init_handles()
+
+    @classmethod
+    def from_csc(cls, U, W, A, method=None, Phi=None, dtype=None):
+        if isinstance(method, SplitPartition):
+            Pi = method
+            if Phi is None:
+                raise _L.ArgumentError("SparseMatrixVBC(A, Π, Φ) needs both partitions")
+        else:
+            if method is None:
+                method = AlternatingPacker(EquiChunker(1), EquiChunker(1))
+            Pi, Phi = pack_plaid(A, method)
+        (m, n), colptr, rowval, nzval = _csc_fields(A)
+        if dtype is not None:
+            nzval = nzval.astype(dtype)
+        lib = _L.lib()
+        K, L = len(Pi), len(Phi)
+        pos = np.zeros(L + 1, np.int64)
+        ofs = np.zeros(L + 1, np.int64)
+        _L.check(lib.vbcx_vbc_count(m, n, colptr.ctypes.data, rowval.ctypes.data, K, Pi.spl.ctypes.data, L,
+                                    Phi.spl.ctypes.data, pos.ctypes.data, ofs.ctypes.data), "SparseMatrixVBC")
+        pad = _simd_pad(W, nzval.dtype, U)
+        idx = np.zeros(pos[-1] - 1, np.int64)
+        val = np.zeros(ofs[-1] - 1 + pad, nzval.dtype)
+        _L.check(lib.vbcx_vbc_fill(m, n, U, W, colptr.ctypes.data, rowval.ctypes.data, nzval.ctypes.data,
+                                   _L.dtype_code(nzval.dtype), K, Pi.spl.ctypes.data, L, Phi.spl.ctypes.data,
+                                   pos.ctypes.data, ofs.ctypes.data, idx.ctypes.data, val.ctypes.data, pad),
+                 "SparseMatrixVBC")
+        return cls(U, W, m, n, Pi, Phi, pos, idx, ofs, val)
+
+    def _create(self, out, device, flags):
+        return _L.lib().vbc2d_create(out, self.m, self.n, self.U, self.W, len(self.Pi), self.Pi.spl.ctypes.data,
+                                     len(self.Phi), self.Phi.spl.ctypes.data, self.pos.ctypes.data,
+                                     self.idx.ctypes.data, self.ofs.ctypes.data, self.val.ctypes.data,
+                                     len(self.val), _L.dtype_code(self.val.dtype), device, flags)
+
+    def __repr__(self):
+        return (f"SparseMatrixVBC{{{self.U},{self.W},{self.val.dtype},Int64}}({self.m}×{self.n}, "
+                f"{len(self.Pi)}×{len(self.Phi)} partition, {len(self.idx)} blocks)")
+
+
+class SparseMatrixCSC(_DeviceMatrix):
+    """SparseMatrixCSC{Tv,Int64} fields (colptr, rowval, nzval), the operand of TrSpMV!."""
+
+    def __init__(self, A):
+        (self.m, self.n), self.colptr, self.rowval, self.nzval = _csc_fields(A)
+        self.val = self.nzval
+        self._init_handles()
+
+    def _create(self, out, device, flags):
+        return _L.lib().vbc_csc_create(out, self.m, self.n, self.colptr.ctypes.data, self.rowval.ctypes.data,
+                                       self.nzval.ctypes.data, _L.dtype_code(self.nzval.dtype), device, flags)
+
+
+class Adjoint:
+    """LinearAlgebra.Adjoint wrapper (real eltypes: identical to Transpose)."""
+
+    def __init__(self, parent):
+        self.parent = parent
+
+    @property
+    def shape(self):
+        return (self.parent.n, self.parent.m)
+
+    def size(self, dim=None):
+        return self.shape if dim is None else self.shape[dim - 1]
+
+    def __matmul__(self, x):
+        from .multiply import matmul
+        return matmul(self, x)
+
+
+class Transpose(Adjoint):
+    """LinearAlgebra.Transpose wrapper."""
+
+
+def adjoint(A):
+    return Adjoint(A)
+
+
+def transpose(A):
+    return Transpose(A)

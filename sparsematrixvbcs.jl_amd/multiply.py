@@ -1,0 +1,128 @@
+"""mul! / * / TrSpMV! on the GPU through libvbc (the reference's operator surface).
+
+    mul_(y, B, x[, α, β])      LinearAlgebra.mul!(y, B, x, α, β)     multiply_1DVBC.jl:9 / multiply_VBC.jl:3
+    mul_(y, B.T, x[, α, β])    mul!(y, B', x, α, β)                   multiply_1DVBC.jl:85 / multiply_VBC.jl:89
+    TrSpMV_(y, A, x)           TrSpMV!(y, A::SparseMatrixCSC, x)      TrSpMV.jl:1-20
+    B @ x, B.T @ x             Base.:*                                multiply_1DVBC.jl:182-185
+
+x / y are torch CUDA tensors (the product is enqueued on torch's current stream of that device, no
+synchronisation) or numpy arrays (staged through HBM by libvbc; returns when y is final).  The
+eltype of x and y must equal the matrix's.  Semantics are BLAS (y = α·op(B)·x + β·y); pass
+`quirks=True` to reproduce the reference's α/β handling bit for bit (vbc.h VBC_MUL_REFERENCE_QUIRKS).
+There is no CPU fallback: without libvbc or a GPU these raise.
+"""
+import numpy as np
+
+from . import _lib as _L
+from .matrices import Adjoint, SparseMatrixCSC, _DeviceMatrix
+
+
+def _unwrap(A):
+    if isinstance(A, Adjoint):
+        return A.parent, True
+    return A, False
+
+
+def _is_torch(a):
+    return type(a).__module__.startswith("torch")
+
+
+def _mem_device_stream(x, y, stream):
+    if _is_torch(x) or _is_torch(y):
+        import torch
+        if not (_is_torch(x) and _is_torch(y)):
+            raise _L.ArgumentError("x and y must both be torch tensors or both numpy arrays")
+        if not (x.is_cuda and y.is_cuda):
+            raise _L.ArgumentError("torch tensors must live on a GPU (no CPU fallback)")
+        if x.device != y.device:
+            raise _L.ArgumentError("x and y must be on the same device")
+        dev = x.device.index
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device).cuda_stream
+        elif hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        return _L.VBC_MEM_DEVICE, dev, stream
+    return _L.VBC_MEM_HOST, 0, None
+
+
+def _check_vec(a, dtype, name):
+    if a.dtype != dtype if isinstance(a, np.ndarray) else str(a.dtype) != "torch." + np.dtype(dtype).name:
+        raise _L.UnsupportedDtype(f"{name} eltype {a.dtype} != matrix eltype {np.dtype(dtype)}")
+    contiguous = a.flags.c_contiguous if isinstance(a, np.ndarray) else a.is_contiguous()
+    if not contiguous:
+        raise _L.ArgumentError(f"{name} must be contiguous (StridedVector with stride 1)")
+
+
+def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None):
+    """LinearAlgebra.mul!(y, A, x, α, β); returns y."""
+    B, trans = _unwrap(A)
+    if not isinstance(B, _DeviceMatrix):
+        raise TypeError(f"mul_ expects SparseMatrix1DVBC / SparseMatrixVBC / SparseMatrixCSC, got {type(B)}")
+    if len(y.shape) != 1 or len(x.shape) != 1:
+        return mulmat_(y, A, x, alpha, beta, stream=stream, quirks=quirks)
+    mem, dev, stream = _mem_device_stream(x, y, stream)
+    if device is not None and mem == _L.VBC_MEM_HOST:
+        dev = device
+    _check_vec(x, B.dtype, "x")
+    _check_vec(y, B.dtype, "y")
+    # DimensionMismatch before any handle is built (multiply_1DVBC.jl:44-45, :139-140)
+    nx, ny = x.shape[0], y.shape[0]
+    if (nx, ny) != ((B.m, B.n) if trans else (B.n, B.m)):
+        raise _L.DimensionMismatch(f"size(A)={A.shape}, length(x)={nx}, length(y)={ny}")
+    h = B.handle(dev, trans)
+    flags = _L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0
+    _L.check(_L.lib().vbc_mul(h, int(trans), _L.ptr(x), nx, _L.ptr(y), ny, float(alpha), float(beta), mem,
+                              stream, flags), "mul!")
+    return y
+
+
+def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False):
+    """Multi-RHS Y = α·op(A)·X + β·Y, column by column semantics (no reference kernel exists)."""
+    B, trans = _unwrap(A)
+    mem, dev, stream = _mem_device_stream(X, Y, stream)
+    if mem == _L.VBC_MEM_HOST:
+        # column-major (Julia) layout expected
+        if not (X.flags.f_contiguous and Y.flags.f_contiguous):
+            raise _L.ArgumentError("host X / Y must be Fortran-ordered (column-major, like Julia)")
+        ldx, ldy = X.shape[0], Y.shape[0]
+    else:
+        # torch: accept a (k, rows) C-contiguous tensor viewed as column-major (rows, k) via .T
+        if not (X.stride(0) == 1 and Y.stride(0) == 1):
+            raise _L.ArgumentError("device X / Y must be column-major: pass M.T of a contiguous (k, rows) tensor")
+        ldx, ldy = X.stride(1), Y.stride(1)
+    nrhs = X.shape[1]
+    if Y.shape[1] != nrhs:
+        raise _L.DimensionMismatch("X and Y have different numbers of columns")
+    h = B.handle(dev, trans)
+    flags = _L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0
+    _L.check(_L.lib().vbc_mul_mat(h, int(trans), nrhs, _L.ptr(X), max(ldx, 1), X.shape[0], _L.ptr(Y),
+                                  max(ldy, 1), Y.shape[0], float(alpha), float(beta), mem, stream, flags),
+             "mul!")
+    return Y
+
+
+def matmul(A, x):
+    """Base.:*(A, x): allocate y = similar(x, T, size(A, 1)) and mul!(y, A, x, true, false)."""
+    m = A.shape[0]
+    if _is_torch(x):
+        import torch
+        y = torch.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if x.dim() == 2:
+            y = torch.empty((x.shape[1], m), dtype=x.dtype, device=x.device).T
+    else:
+        y = np.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, order="F")
+    return mul_(y, A, x, True, False)
+
+
+def TrSpMV_(y, A, x, *, stream=None):
+    """TrSpMV!(y, A::SparseMatrixCSC, x): y = Aᵀx (overwrite), TrSpMV.jl:1-20."""
+    if not isinstance(A, SparseMatrixCSC):
+        cached = getattr(A, "_vbc_csc", None)
+        if cached is None:
+            cached = SparseMatrixCSC(A)
+            try:
+                A._vbc_csc = cached
+            except AttributeError:
+                pass
+        A = cached
+    return mul_(y, Adjoint(A), x, 1.0, 0.0, stream=stream)

@@ -1,0 +1,60 @@
+"""Synthetic variable-block matrices for parity tests and the benchmark.
+
+Follows the reference's own VBR generator (costs.jl:63-83): draw q distinct (row i, stripe l) pairs
+uniformly and store a full w-wide dense row for each, values rand(Tv) ~ U[0, 1).  The fields are
+produced directly in the reference layout (1-based Int64 spl/pos/idx/ofs + val), exactly what
+`SparseMatrix1DVBC{W}(sparse(I, J, V, m, n), pack_stripe(A, EquiChunker(w)))` would hold for that
+matrix (constructors_1DVBC.jl:9-92), without materialising the CSC.
+"""
+import numpy as np
+
+from .matrices import SparseMatrix1DVBC, _simd_pad
+from .partition import SplitPartition
+
+
+def vbr_1dvbc(m, L, q, widths, W=8, dtype=np.float64, seed=0xDEADBEEF, pad=True):
+    """m rows, L stripes with widths `widths` (int or length-L array), ~q stored rows.
+
+    Returns a SparseMatrix1DVBC whose stripe l has the distinct sorted rows drawn for it."""
+    rng = np.random.default_rng(seed)
+    w = np.broadcast_to(np.asarray(widths, dtype=np.int64), (L,)).copy()
+    if w.max(initial=1) > W:
+        raise ValueError("stripe width exceeds W")
+    keys = np.unique(rng.integers(0, np.int64(m) * L, size=int(q), dtype=np.int64))  # sorted by (l, i)
+    stripe = keys // m
+    row = keys - stripe * m
+    counts = np.bincount(stripe, minlength=L).astype(np.int64)
+    spl = np.empty(L + 1, np.int64)
+    spl[0] = 1
+    np.cumsum(w, out=spl[1:])
+    spl[1:] += 1
+    pos = np.empty(L + 1, np.int64)
+    pos[0] = 1
+    np.cumsum(counts, out=pos[1:])
+    pos[1:] += 1
+    ofs = np.empty(L + 1, np.int64)
+    ofs[0] = 1
+    np.cumsum(counts * w, out=ofs[1:])
+    ofs[1:] += 1
+    nv = int(ofs[-1] - 1)
+    padn = _simd_pad(W, dtype) if pad else 0
+    val = np.empty(nv + padn, dtype)
+    val[:nv] = rng.random(nv, dtype=np.float64 if dtype == np.float64 else np.float32)
+    val[nv:] = 0
+    n = int(spl[-1] - 1)
+    return SparseMatrix1DVBC(W, m, n, SplitPartition(spl), pos, row + 1, ofs, val)
+
+
+def north_star(dtype=np.float64, scale=1.0, seed=0xDEADBEEF, mixed=False):
+    """NS-1DVBC: 10^7 x 10^7, W = 8, w = 4, 2.5e6 stripes, 10 row-blocks per stripe
+    on average -> q = 2.5e7 stored rows, nnz = 1.0e8, no fill.  `mixed`: w ~ U{1..8} per stripe with
+    the row count chosen so that nnz is still ~1e8.  `scale` shrinks every dimension (tests)."""
+    m = int(round(1e7 * scale))
+    if mixed:
+        rng = np.random.default_rng(seed ^ 0x5EED)
+        L = int(round(1e7 * scale / 4.5))  # E[w] = 4.5 -> n ~ 1e7
+        w = rng.integers(1, 9, L)
+        q = int(round(1e8 * scale / w.mean()))
+        return vbr_1dvbc(m, L, q, w, 8, dtype, seed)
+    L = m // 4
+    return vbr_1dvbc(m, L, int(round(2.5e7 * scale)), 4, 8, dtype, seed)

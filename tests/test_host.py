@@ -1,0 +1,119 @@
+"""Host-side product code (libvbc vbcx_*), no GPU: the reference-layout builders must reproduce the
+oracle's restatement of constructors_1DVBC.jl / constructors_VBC.jl EXACTLY for every partition, and
+the partitioners must return valid partitions with their defining property."""
+import itertools
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import sparsematrixvbcs_amd as V
+from oracle import oracle as O
+from tests.conftest import sprand_family
+
+METHODS_1D = [
+    ("strict", lambda: V.StrictChunker(4)),
+    ("overlap", lambda: V.OverlapChunker(0.9, 4)),
+    ("blocks", lambda: V.DynamicTotalChunker(V.ConstrainedCost(V.model_SparseMatrix1DVBC_blocks(), V.VertexCount(), 4))),
+    ("memory", lambda: V.DynamicTotalChunker(V.ConstrainedCost(V.model_SparseMatrix1DVBC_memory(np.float64, np.int64), V.VertexCount(), 4))),
+]
+METHODS_2D = [
+    ("strict2d", lambda: V.AlternatingPacker(V.StrictChunker(4), V.StrictChunker(4))),
+    ("overlap2d", lambda: V.AlternatingPacker(V.OverlapChunker(0.9, 4), V.OverlapChunker(0.9, 4))),
+]
+
+
+def same_layout(B, R):
+    assert np.array_equal(B.Phi.spl, R.spl)
+    for f in ("pos", "idx", "ofs", "val"):
+        a, b = getattr(B, f), getattr(R, f)
+        assert a.dtype == b.dtype and np.array_equal(a, b), f
+
+
+@pytest.mark.parametrize("name,method", METHODS_1D)
+def test_1dvbc_builder_matches_oracle(golden, name, method):
+    corpus = [(k, g["A"]) for k, g in golden.items()] + sprand_family(trials=1)
+    for key, A in corpus:
+        B = V.SparseMatrix1DVBC[4](A, method())
+        R = O.build_1dvbc(sp.csc_matrix(A, dtype=np.float64), B.Phi.spl, 4, pad=8)
+        same_layout(B, R)
+        assert np.array_equal(O.vbc_to_dense(R), A.toarray())
+
+
+@pytest.mark.parametrize("name,method", METHODS_2D)
+def test_vbc_builder_matches_oracle(golden, name, method):
+    corpus = [(k, g["A"]) for k, g in golden.items()] + sprand_family(trials=1, kinds=("f64",))
+    for key, A in corpus:
+        B = V.SparseMatrixVBC[4, 4](A, method())
+        R = O.build_vbc(sp.csc_matrix(A, dtype=np.float64), B.Pi.spl, B.Phi.spl, 4, 4, pad=32)
+        same_layout(B, R)
+        assert np.array_equal(B.Pi.spl, R.pspl)
+
+
+def test_fp32_builder_matches_oracle(golden):
+    A = golden["HB__west0132"]["A"]
+    B = V.SparseMatrix1DVBC[8](A, V.EquiChunker(5), dtype=np.float32)
+    R = O.build_1dvbc(A, B.Phi.spl, 8, pad=16, dtype=np.float32)
+    same_layout(B, R)
+
+
+def patterns(A):
+    A = A.tocsc()
+    return [tuple(A.indices[A.indptr[j]:A.indptr[j + 1]]) for j in range(A.shape[1])]
+
+
+def test_partitioners_properties(golden):
+    for key, g in golden.items():
+        A = g["A"]
+        pats = patterns(A)
+        for W in (1, 3, 8):
+            for meth in (V.StrictChunker(W), V.OverlapChunker(0.5, W), V.EquiChunker(W),
+                         V.DynamicTotalChunker(V.model_SparseMatrix1DVBC_memory(), W)):
+                P = V.pack_stripe(A, meth)
+                assert P.spl[0] == 1 and P.spl[-1] == A.shape[1] + 1
+                assert P.widths().max(initial=0) <= W
+            # strict: stripes are maximal runs of identical patterns (capped at W)
+            P = V.pack_stripe(A, V.StrictChunker(W))
+            for l in range(len(P)):
+                j0, j1 = P.spl[l] - 1, P.spl[l + 1] - 1
+                assert all(pats[j] == pats[j0] for j in range(j0, j1))
+                if j1 < A.shape[1] and j1 - j0 < W:
+                    assert pats[j1] != pats[j0]
+
+
+def brute_min_cost(A, W, cost):
+    n = A.shape[1]
+    best = {0: 0.0}
+    for e in range(1, n + 1):
+        best[e] = min(best[e - w] + cost(e - w, e) for w in range(1, min(W, e) + 1))
+    return best[n]
+
+
+def test_dynamic_chunker_is_optimal():
+    rng = np.random.default_rng(5)
+    for t in range(20):
+        m, n = rng.integers(1, 12, 2)
+        A = sp.csc_matrix((rng.random((m, n)) < 0.3).astype(float))
+        W = int(rng.integers(1, 5))
+        model = V.model_SparseMatrix1DVBC_memory(np.float64, np.int64)
+        P = V.pack_stripe(A, V.DynamicTotalChunker(model, W))
+        D = A.toarray() != 0
+
+        def cost(j0, j1):
+            rows = D[:, j0:j1].any(axis=1).sum()
+            return 24 + 8 * rows + 8 * (j1 - j0) * rows
+
+        got = sum(cost(P.spl[l] - 1, P.spl[l + 1] - 1) for l in range(len(P)))
+        assert got == pytest.approx(brute_min_cost(A, W, cost))
+
+
+def test_constructor_argument_errors():
+    with pytest.raises(V.ArgumentError):
+        V.SparseMatrix1DVBC(0, 2, 2, [1, 3], [1, 1], [], [1, 1], np.zeros(0))
+    with pytest.raises(V.ArgumentError):
+        V.SparseMatrix1DVBC(2, -1, 2, [1, 3], [1, 1], [], [1, 1], np.zeros(0))
+    A = sp.csc_matrix(np.ones((3, 4)))
+    with pytest.raises(AssertionError):  # w = 4 > W = 2 (constructors_1DVBC.jl:46)
+        V.SparseMatrix1DVBC[2](A, V.SplitPartition([1, 5]))
+    with pytest.raises(V.UnsupportedDtype):
+        V.SparseMatrix1DVBC[2](sp.csc_matrix(np.ones((2, 2), dtype=np.complex128)), V.EquiChunker(1))
