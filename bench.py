@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="ns", choices=["ns", "ns-mixed"])
+    ap.add_argument("--workload", default="ns", choices=["ns", "ns-mixed", "fe"])
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -93,8 +93,11 @@ def main():
     dtype = np.float64 if args.dtype == "f64" else np.float32
     esz = np.dtype(dtype).itemsize
     # each rank: its own block-row shard (different stripes), the same replicated x
-    B = V.synthetic.north_star(dtype=dtype, scale=args.scale, seed=0xDEADBEEF + rank,
-                               mixed=(args.workload == "ns-mixed"))
+    if args.workload == "fe":
+        B = V.synthetic.fe_grid_2d(int(round(2236 * args.scale ** 0.5)), dof=2, dtype=dtype, seed=0xDEADBEEF + rank)
+    else:
+        B = V.synthetic.north_star(dtype=dtype, scale=args.scale, seed=0xDEADBEEF + rank,
+                                   mixed=(args.workload == "ns-mixed"))
     rng = np.random.default_rng(0xC0FFEE)
     x_host = rng.uniform(-1, 1, B.m).astype(dtype)
     x = torch.from_numpy(x_host).to(device)
@@ -139,7 +142,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_bytes * args.steps / elapsed / 1e9
     achieved = bytes_rank / (kernel_ms * 1e-3) / 1e9
-    workload = "NS-1DVBC-10Mx10M-1e8nnz-w4" if args.workload == "ns" else "NS-1DVBC-mixed-w1..8-1e8nnz"
+    workload = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform", "ns-mixed": "NS-1DVBC-mixed-w1..8-1e8nnz-uniform",
+                "fe": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2"}[args.workload]
     if args.scale != 1.0:
         workload += f"-scale{args.scale}"
     traffic, traffic_src = load_traffic(args.workload, args.dtype)
@@ -171,7 +175,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "vbc::spmv_bins<T, 0>",
+            "kernel": "vbc::spmv_ranges<T, 0>",
             "bytes_per_launch": bytes_rank,
             "avg_launch_ms": round(kernel_ms, 5),
             "traffic_source": traffic_src,

@@ -1,10 +1,11 @@
-// libvbc device side: handle creation (reference layout -> binned HBM layout), product launches
+// libvbc device side: handle creation (reference layout -> tiled HBM entry streams), product launches
 // and the C ABI of include/vbc.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdarg>
 #include <cstring>
+#include <cmath>
 #include <map>
 #include <string>
 #include <vector>
@@ -50,27 +51,14 @@ struct DeviceGuard {
     }
 };
 
-constexpr int kGroupSizes[] = {4, 8, 16, 32, 64};
-
-// Smallest lane group that covers `elems` values of a segment of width w in one pass.
-static int choose_group(int esz, int w, int64_t elems)
-{
-    const int V = w <= 8 ? vec_elems(esz, w) : 1;
-    const int LPR = w / V;
-    for (int G : kGroupSizes) {
-        if (G < LPR) continue;
-        const int64_t per_pass = (int64_t)(G / LPR) * LPR * V;
-        if (per_pass >= elems) return G;
-    }
-    return 64;
-}
-
-// One fused launch: a bin table (device) plus its host copy.
+// One fused launch of spmv_ranges (+ its fix-up pass).
 struct Launch {
     std::vector<Bin> bins;
     Bin *d_bins = nullptr;
-    int total_vblocks = 0;
-    int grid = 0;
+    int total_ranges = 0;
+    int nfill = 0;
+    size_t o_fill = 0;             // arena offset of the fill list (y indices)
+    const int32_t *d_fill = nullptr;
 };
 
 // Host description of the input stripes, common to 1D, 2D (expanded) and CSC inputs.
@@ -91,10 +79,11 @@ struct vbc_handle {
     void *d_arena = nullptr;
     size_t arena_bytes = 0;
     bool has_t = false, has_f = false;
-    vbc::Launch lt;                 // transposed product
-    std::vector<vbc::Launch> lf;    // forward product: one launch per width bucket
+    vbc::Launch lt;               // transposed product: all buckets in one launch
+    std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
+    bool f_scale = false;         // forward with several buckets: scale y by beta first
     int64_t bytes_t = 0, bytes_f = 0;
-    int grid_cap = 2048;
+    int target_ranges = 4096;     // waves resident on the device (one range each)
 };
 
 namespace vbc {
@@ -105,7 +94,7 @@ struct Arena {
     size_t reserve(size_t bytes)
     {
         size_t off = (host.size() + 255) & ~size_t(255);
-        host.resize(off + bytes);
+        host.resize(off + std::max<size_t>(bytes, 1));
         return off;
     }
     template <typename U>
@@ -114,7 +103,7 @@ struct Arena {
 
 struct PendingBin {
     Bin b;
-    size_t o_rptr, o_out, o_idx, o_val;
+    size_t o_key, o_val, o_rseg, o_out, o_carry, o_cseg;
 };
 
 static int check_limits(const Stripes &s)
@@ -126,155 +115,161 @@ static int check_limits(const Stripes &s)
     return VBC_OK;
 }
 
-// Transposed layout: segments = stripes, binned by (w, G).
-static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                            std::vector<PendingBin> &out)
+// A logical entry of a bucket's stream: gather index + where its w values come from.
+struct Entry {
+    uint32_t key;   // gather index | HEAD
+    int64_t voff;   // element offset into the input val
+};
+
+// Lay out one bucket's entry stream (segment-ordered) as tiles, ranges and fix-up slots.
+static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry> &ents,
+                        const std::vector<int32_t> &out, int64_t total_entries, const char *val,
+                        Arena &ar, int &range0, PendingBin &pb)
 {
     const int esz = h->esz;
-    std::map<std::pair<int, int>, std::vector<int64_t>> bins;  // (w, G) -> stripes
-    for (int64_t l = 0; l < s.L; l++) {
-        const int64_t R = s.rbeg[l + 1] - s.rbeg[l];
-        bins[{s.w[l], choose_group(esz, s.w[l], R * s.w[l])}].push_back(l);
-    }
-    int vblock = 0;
-    for (auto &kv : bins) {
-        const int w = kv.first.first, G = kv.first.second;
-        const std::vector<int64_t> &segs = kv.second;
-        int64_t rows = 0;
-        for (int64_t l : segs) rows += s.rbeg[l + 1] - s.rbeg[l];
-        if (rows >= (int64_t(1) << 31) || (int64_t)segs.size() >= (int64_t(1) << 31))
-            return fail(VBC_INVALID_ARG, "bin too large for int32 offsets");
-        PendingBin pb{};
-        pb.b.w = w;
-        pb.b.G = G;
-        pb.b.key = make_key(0, w <= 8 ? w : 0, G);
-        pb.b.nseg = (int32_t)segs.size();
-        const int per_vb = kWavesPerBlock * (64 / G);
-        const int64_t nvb = ((int64_t)segs.size() + per_vb - 1) / per_vb;
-        if ((int64_t)vblock + nvb >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "too many blocks");
-        pb.b.vblock0 = vblock;
-        pb.b.nvblock = (int32_t)nvb;
-        vblock += (int)nvb;
-        pb.o_rptr = ar.reserve((segs.size() + 1) * 4);
-        pb.o_out = ar.reserve(segs.size() * 4);
-        pb.o_idx = ar.reserve(rows * 4);
-        pb.o_val = ar.reserve(rows * w * esz);
-        int32_t *rptr = ar.at<int32_t>(pb.o_rptr);
-        int32_t *o = ar.at<int32_t>(pb.o_out);
-        int32_t *ix = ar.at<int32_t>(pb.o_idx);
-        char *vv = ar.at<char>(pb.o_val);
-        int64_t r = 0;
-        for (size_t q = 0; q < segs.size(); q++) {
-            const int64_t l = segs[q];
-            const int64_t R = s.rbeg[l + 1] - s.rbeg[l];
-            rptr[q] = (int32_t)r;
-            o[q] = (int32_t)s.col0[l];
-            std::memcpy(ix + r, s.rows.data() + s.rbeg[l], R * 4);
-            std::memcpy(vv + r * w * esz, val + s.voff[l] * esz, R * w * esz);
-            r += R;
+    const int V = w <= 8 ? vec_elems(esz, w) : 1;
+    const int LPR = w / V;
+    const int RPI = 64 / LPR;
+    const int64_t tile_rows = (int64_t)RPI * kTileK;
+    const int64_t R = (int64_t)ents.size();
+    const int64_t ntiles = (R + tile_rows - 1) / tile_rows;
+    if (ntiles >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
+    if ((int64_t)out.size() >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "too many segments");
+    // ranges: one wave each, about target_ranges over the whole launch, >= 2 tiles per range
+    int64_t nr = (int64_t)std::llround((double)h->target_ranges * (double)R / (double)std::max<int64_t>(total_entries, 1));
+    nr = std::max<int64_t>(1, std::min<int64_t>(nr, (ntiles + 1) / 2));
+    const int64_t tpr = ntiles > 0 ? (ntiles + nr - 1) / nr : 1;
+    nr = ntiles > 0 ? (ntiles + tpr - 1) / tpr : 0;
+    pb = PendingBin{};
+    pb.b.kind = kind;
+    pb.b.wkey = w <= 8 ? w : 0;
+    pb.b.w = w;
+    pb.b.rpi = RPI;
+    pb.b.range0 = range0;
+    pb.b.nranges = (int32_t)nr;
+    pb.b.tiles_per_range = (int32_t)tpr;
+    pb.b.ntiles = (int32_t)ntiles;
+    range0 += (int)nr;
+    const int64_t Rp = ntiles * tile_rows;
+    pb.o_key = ar.reserve(Rp * 4);
+    pb.o_val = ar.reserve(Rp * w * esz);
+    pb.o_rseg = ar.reserve(std::max<int64_t>(nr, 1) * 4);
+    pb.o_out = ar.reserve(std::max<size_t>(out.size(), 1) * 4);
+    pb.o_carry = ar.reserve(std::max<int64_t>(nr, 1) * (kind == 0 ? w : 1) * esz);
+    pb.o_cseg = ar.reserve(std::max<int64_t>(nr, 1) * 4);
+    uint32_t *key = ar.at<uint32_t>(pb.o_key);
+    char *vv = ar.at<char>(pb.o_val);
+    int32_t *rseg = ar.at<int32_t>(pb.o_rseg);
+    std::memcpy(ar.at<int32_t>(pb.o_out), out.data(), out.size() * 4);
+    int64_t heads = 0;
+    for (int64_t t = 0; t < Rp; t++) {
+        const int64_t tile = t / tile_rows, within = t - tile * tile_rows;
+        const int64_t slot = within / kTileK, k = within - slot * kTileK;
+        const int64_t phys = tile * tile_rows + k * RPI + slot;
+        if (within == 0 && tile % tpr == 0) rseg[tile / tpr] = (int32_t)heads;
+        if (t < R) {
+            key[phys] = ents[t].key;
+            heads += (ents[t].key >> 31);
+            std::memcpy(vv + phys * w * esz, val + ents[t].voff * esz, (size_t)w * esz);
+        } else {
+            key[phys] = 0;  // padding extends the last segment by zeros
+            std::memset(vv + phys * w * esz, 0, (size_t)w * esz);
         }
-        rptr[segs.size()] = (int32_t)r;
-        h->bytes_t += (int64_t)(segs.size() + 1) * 4 + (int64_t)segs.size() * 4 + rows * 4 + rows * w * esz;
-        out.push_back(pb);
     }
-    h->bytes_t += (s.m + s.n) * esz;  // x read once, y written once
     return VBC_OK;
 }
 
-// Forward layout: per width bucket, segments = output rows, entries ordered by stripe.
-static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                         std::vector<std::vector<PendingBin>> &out)
+// Transposed layout: segments = non-empty stripes of each width, entries = their stored rows.
+static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
+                            std::vector<PendingBin> &pbs, Launch &L, std::vector<int32_t> &fill)
 {
-    const int esz = h->esz;
     std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
-    for (int64_t l = 0; l < s.L; l++) buckets[s.w[l]].push_back(l);
-    if (buckets.empty()) buckets[1];  // still need one launch to apply beta to y
-    bool first = true;
-    std::vector<int64_t> cnt(s.m), cur(s.m);
+    for (int64_t l = 0; l < s.L; l++) {
+        if (s.rbeg[l + 1] > s.rbeg[l]) buckets[s.w[l]].push_back(l);
+        else for (int c = 0; c < s.w[l]; c++) fill.push_back((int32_t)(s.col0[l] + c));
+    }
+    const int64_t total = (int64_t)s.rows.size();
+    int range0 = 0;
+    for (auto &kv : buckets) {
+        const int w = kv.first;
+        std::vector<Entry> ents;
+        std::vector<int32_t> out;
+        for (int64_t l : kv.second) {
+            out.push_back((int32_t)s.col0[l]);
+            for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
+                ents.push_back({(uint32_t)s.rows[r] | (r == s.rbeg[l] ? kHead : 0u),
+                                s.voff[l] + (r - s.rbeg[l]) * w});
+        }
+        PendingBin pb;
+        if (int st = build_bucket(h, 0, w, ents, out, total, val, ar, range0, pb)) return st;
+        h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)w * h->esz) + (int64_t)out.size() * 4;
+        pbs.push_back(pb);
+    }
+    L.total_ranges = range0;
+    h->bytes_t += (s.m + s.n) * h->esz;  // x read once, y written once
+    return VBC_OK;
+}
+
+// Forward layout: per width bucket, segments = output rows with entries of that width (ascending),
+// entries = (row, stripe) blocks ordered by stripe within the row.
+static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
+                         std::vector<std::vector<PendingBin>> &pbs, std::vector<Launch> &Ls,
+                         std::vector<int32_t> &fill)
+{
+    std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
+    for (int64_t l = 0; l < s.L; l++)
+        if (s.rbeg[l + 1] > s.rbeg[l]) buckets[s.w[l]].push_back(l);
+    std::vector<int64_t> cnt(s.m + 1), cur(s.m);
+    std::vector<char> any(s.m, 0);
     for (auto &kv : buckets) {
         const int w = kv.first;
         std::fill(cnt.begin(), cnt.end(), 0);
         for (int64_t l : kv.second)
-            for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) cnt[s.rows[r]]++;
-        // segments per G
-        std::map<int, std::vector<int64_t>> groups;
-        for (int64_t i = 0; i < s.m; i++)
-            if (cnt[i] > 0 || first) groups[choose_group(esz, w, cnt[i] * w)].push_back(i);
-        std::vector<PendingBin> launch;
-        int vblock = 0;
-        for (auto &gv : groups) {
-            const int G = gv.first;
-            const std::vector<int64_t> &segs = gv.second;
-            int64_t ents = 0;
-            for (int64_t i : segs) ents += cnt[i];
-            if (ents >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bin too large for int32 offsets");
-            PendingBin pb{};
-            pb.b.w = w;
-            pb.b.G = G;
-            pb.b.key = make_key(1, w <= 8 ? w : 0, G);
-            pb.b.nseg = (int32_t)segs.size();
-            const int per_vb = kWavesPerBlock * (64 / G);
-            const int64_t nvb = ((int64_t)segs.size() + per_vb - 1) / per_vb;
-            if ((int64_t)vblock + nvb >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "too many blocks");
-            pb.b.vblock0 = vblock;
-            pb.b.nvblock = (int32_t)nvb;
-            vblock += (int)nvb;
-            pb.o_rptr = ar.reserve((segs.size() + 1) * 4);
-            pb.o_out = ar.reserve(segs.size() * 4);
-            pb.o_idx = ar.reserve(ents * 4);
-            pb.o_val = ar.reserve(ents * w * esz);
-            int32_t *rptr = ar.at<int32_t>(pb.o_rptr);
-            int32_t *o = ar.at<int32_t>(pb.o_out);
-            int64_t e = 0;
-            for (size_t q = 0; q < segs.size(); q++) {
-                rptr[q] = (int32_t)e;
-                o[q] = (int32_t)segs[q];
-                cur[segs[q]] = e;  // write cursor of row segs[q] within this bin
-                e += cnt[segs[q]];
-            }
-            rptr[segs.size()] = (int32_t)e;
-            h->bytes_f += (int64_t)(segs.size() + 1) * 4 + (int64_t)segs.size() * 4 + ents * 4 + ents * w * esz;
-            h->bytes_f += (int64_t)segs.size() * esz * (first ? 1 : 2);  // y write (+ read when accumulating)
-            launch.push_back(pb);
-        }
-        // scatter entries into their row segments, stripe-ascending
-        std::vector<int> bin_of(s.m, -1);
-        for (size_t bi = 0; bi < launch.size(); bi++) {
-            const int32_t *o = ar.at<int32_t>(launch[bi].o_out);
-            for (int32_t q = 0; q < launch[bi].b.nseg; q++) bin_of[o[q]] = (int)bi;
-        }
-        for (int64_t l : kv.second) {
+            for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) cnt[s.rows[r] + 1]++;
+        for (int64_t i = 0; i < s.m; i++) cnt[i + 1] += cnt[i];
+        std::vector<Entry> ents(cnt[s.m]);
+        for (int64_t i = 0; i < s.m; i++) cur[i] = cnt[i];
+        for (int64_t l : kv.second)
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) {
                 const int64_t i = s.rows[r];
-                PendingBin &pb = launch[bin_of[i]];
                 const int64_t e = cur[i]++;
-                ar.at<int32_t>(pb.o_idx)[e] = (int32_t)s.col0[l];
-                std::memcpy(ar.at<char>(pb.o_val) + e * w * esz,
-                            val + (s.voff[l] + (r - s.rbeg[l]) * w) * esz, (size_t)w * esz);
+                ents[e] = {(uint32_t)s.col0[l] | (e == cnt[i] ? kHead : 0u), s.voff[l] + (r - s.rbeg[l]) * w};
             }
-        }
-        h->bytes_f += s.n * esz;  // x slices (read once, ideally)
-        out.push_back(std::move(launch));
-        first = false;
+        std::vector<int32_t> out;
+        for (int64_t i = 0; i < s.m; i++)
+            if (cnt[i + 1] > cnt[i]) { out.push_back((int32_t)i); any[i] = 1; }
+        PendingBin pb;
+        int range0 = 0;
+        if (int st = build_bucket(h, 1, w, ents, out, (int64_t)ents.size(), val, ar, range0, pb)) return st;
+        h->bytes_f += (int64_t)ents.size() * (4 + (int64_t)w * h->esz) + (int64_t)out.size() * (4 + h->esz);
+        pbs.push_back({pb});
+        Ls.emplace_back();
+        Ls.back().total_ranges = range0;
     }
+    h->f_scale = buckets.size() > 1;
+    if (buckets.size() <= 1)
+        for (int64_t i = 0; i < s.m; i++)
+            if (!any[i]) fill.push_back((int32_t)i);
+    if (h->f_scale) h->bytes_f += s.m * h->esz * 2 * (int64_t)buckets.size();
+    h->bytes_f += s.n * h->esz;
     return VBC_OK;
 }
 
 static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, Launch &L)
 {
     L.bins.clear();
+    char *base = static_cast<char *>(h->d_arena);
     for (const PendingBin &pb : pbs) {
         Bin b = pb.b;
-        char *base = static_cast<char *>(h->d_arena);
-        b.rptr = reinterpret_cast<const int32_t *>(base + pb.o_rptr);
-        b.out = reinterpret_cast<const int32_t *>(base + pb.o_out);
-        b.idx = reinterpret_cast<const int32_t *>(base + pb.o_idx);
+        b.key = reinterpret_cast<const uint32_t *>(base + pb.o_key);
         b.val = base + pb.o_val;
+        b.rseg = reinterpret_cast<const int32_t *>(base + pb.o_rseg);
+        b.out = reinterpret_cast<const int32_t *>(base + pb.o_out);
+        b.carry = base + pb.o_carry;
+        b.carry_seg = reinterpret_cast<int32_t *>(base + pb.o_cseg);
         L.bins.push_back(b);
     }
-    L.total_vblocks = 0;
-    for (const Bin &b : L.bins) L.total_vblocks = std::max(L.total_vblocks, b.vblock0 + b.nvblock);
-    L.grid = std::max(1, std::min(L.total_vblocks, h->grid_cap));
+    L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
     if (!L.bins.empty()) {
         VBC_HIP(hipMalloc(&L.d_bins, L.bins.size() * sizeof(Bin)));
         VBC_HIP(hipMemcpy(L.d_bins, L.bins.data(), L.bins.size() * sizeof(Bin), hipMemcpyHostToDevice));
@@ -335,22 +330,35 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipGetDeviceProperties failed"); }
     int occ = 0;
     if (dtype == VBC_F64)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_bins<double, 0>, kBlockThreads, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<double, 0>, kBlockThreads, 0);
     else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_bins<float, 0>, kBlockThreads, 0);
-    h->grid_cap = prop.multiProcessorCount * std::max(1, std::min(occ, 8));
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<float, 0>, kBlockThreads, 0);
+    h->target_ranges = prop.multiProcessorCount * std::max(1, std::min(occ, 8)) * kWavesPerBlock;
+    if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges = std::max(1, atoi(e));
 
     Arena ar;
     std::vector<PendingBin> pt;
     std::vector<std::vector<PendingBin>> pf;
+    std::vector<int32_t> fill_t, fill_f;
     int st = VBC_OK;
     if (flags & VBC_CREATE_TRANSPOSED) {
-        st = build_transposed(h, s, v, ar, pt);
+        st = build_transposed(h, s, v, ar, pt, h->lt, fill_t);
         h->has_t = st == VBC_OK;
+        if (st == VBC_OK) {
+            h->lt.nfill = (int)fill_t.size();
+            h->lt.o_fill = ar.reserve(fill_t.size() * 4);
+            std::memcpy(ar.at<int32_t>(h->lt.o_fill), fill_t.data(), fill_t.size() * 4);
+        }
     }
     if (st == VBC_OK && (flags & VBC_CREATE_FORWARD)) {
-        st = build_forward(h, s, v, ar, pf);
+        st = build_forward(h, s, v, ar, pf, h->lf, fill_f);
         h->has_f = st == VBC_OK;
+        if (st == VBC_OK) {
+            if (h->lf.empty()) h->lf.emplace_back();  // no entries: the fill list alone writes y
+            h->lf[0].nfill = (int)fill_f.size();
+            h->lf[0].o_fill = ar.reserve(fill_f.size() * 4);
+            std::memcpy(ar.at<int32_t>(h->lf[0].o_fill), fill_f.data(), fill_f.size() * 4);
+        }
     }
     if (st != VBC_OK) { release(h); return st; }
     h->arena_bytes = std::max<size_t>(ar.host.size(), 256);
@@ -364,29 +372,41 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         return fail(VBC_HIP_ERROR, "hipMemcpy of the matrix arena failed");
     }
     if (h->has_t && (st = finalize_launch(h, pt, h->lt))) { release(h); return st; }
-    for (auto &p : pf) {
-        h->lf.emplace_back();
-        if ((st = finalize_launch(h, p, h->lf.back()))) { release(h); return st; }
-    }
+    for (size_t b = 0; b < pf.size(); b++)
+        if ((st = finalize_launch(h, pf[b], h->lf[b]))) { release(h); return st; }
+    if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, h->lf[0]))) { release(h); return st; }
     *out = h;
     return VBC_OK;
 }
 
 template <typename T>
-static int launch(const vbc_handle *h, const Launch &L, int kind, const void *x, void *y, double alpha,
-                  double beta, bool rd, hipStream_t stream)
+static int launch(const Launch &L, int kind, const void *x, void *y, double alpha, double beta, bool rd,
+                  hipStream_t stream)
 {
-    if (L.bins.empty() || L.total_vblocks == 0) return VBC_OK;
-    if (kind == 0)
-        hipLaunchKernelGGL((spmv_bins<T, 0>), dim3(L.grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                           (int)L.bins.size(), L.total_vblocks, static_cast<const T *>(x),
-                           static_cast<T *>(y), (T)alpha, (T)beta, (int)rd);
-    else
-        hipLaunchKernelGGL((spmv_bins<T, 1>), dim3(L.grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                           (int)L.bins.size(), L.total_vblocks, static_cast<const T *>(x),
-                           static_cast<T *>(y), (T)alpha, (T)beta, (int)rd);
-    VBC_HIP(hipGetLastError());
-    (void)h;
+    const T *xs = static_cast<const T *>(x);
+    T *ys = static_cast<T *>(y);
+    if (L.total_ranges > 0) {
+        const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
+        if (kind == 0)
+            hipLaunchKernelGGL((spmv_ranges<T, 0>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                               (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+        else
+            hipLaunchKernelGGL((spmv_ranges<T, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                               (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+        VBC_HIP(hipGetLastError());
+    }
+    const int work = (L.total_ranges > 1 ? L.total_ranges : 0) + L.nfill;
+    if (work > 0) {
+        const int nr = L.total_ranges > 1 ? L.total_ranges : 0;
+        const int grid = (work + kBlockThreads - 1) / kBlockThreads;
+        if (kind == 0)
+            hipLaunchKernelGGL((fixup<T, 0>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                               (int)L.bins.size(), nr, L.d_fill, L.nfill, ys, (T)alpha, (T)beta, (int)rd);
+        else
+            hipLaunchKernelGGL((fixup<T, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                               (int)L.bins.size(), nr, L.d_fill, L.nfill, ys, (T)alpha, (T)beta, (int)rd);
+        VBC_HIP(hipGetLastError());
+    }
     return VBC_OK;
 }
 
@@ -396,13 +416,18 @@ static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, do
 {
     if (trans) {
         if (h->n == 0) return VBC_OK;
-        return launch<T>(h, h->lt, 0, x, y, alpha, beta, beta != 0.0, stream);
+        return launch<T>(h->lt, 0, x, y, alpha, beta, beta != 0.0, stream);
     }
     if (h->m == 0) return VBC_OK;
+    if (h->f_scale) {
+        hipLaunchKernelGGL((scale<T>), dim3(std::min<int64_t>((h->m + kBlockThreads - 1) / kBlockThreads, 4096)),
+                           dim3(kBlockThreads), 0, stream, static_cast<T *>(y), h->m, (T)beta, (int)(beta != 0.0));
+        VBC_HIP(hipGetLastError());
+    }
     for (size_t b = 0; b < h->lf.size(); b++) {
-        const bool first = b == 0;
-        if (int st = launch<T>(h, h->lf[b], 1, x, y, alpha, first ? beta : 1.0,
-                               first ? beta != 0.0 : true, stream))
+        const bool own_beta = !h->f_scale;
+        if (int st = launch<T>(h->lf[b], 1, x, y, alpha, own_beta ? beta : 1.0, own_beta ? beta != 0.0 : true,
+                               stream))
             return st;
     }
     return VBC_OK;

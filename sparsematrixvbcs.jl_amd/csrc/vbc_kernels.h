@@ -1,18 +1,23 @@
 // gfx950 variable-block SpMV kernels (device code, included by vbc_device.hip only).
 //
-// One fused launch per product.  The launch's work is cut into *bins*; a bin holds segments of one
-// width w that all use the same lane-group size G:
-//   kind 0 (mul!(y, B', x), multiply_1DVBC.jl:90-134 / multiply_VBC.jl:93-147 / TrSpMV.jl:1-20):
-//          a segment is one stripe; its stored rows are streamed by a G-lane group, lane (ro, sub)
-//          owning V consecutive columns of rows ro, ro+RPI, ...; partials are tree-reduced across
-//          the RPI row slots with wavefront shuffles and the group writes y[j : j+w-1] once.
-//   kind 1 (mul!(y, B, x), multiply_1DVBC.jl:13-83 / multiply_VBC.jl:7-87): a segment is one
-//          output row of B holding the w-wide entries of this width bucket (a setup-time transpose
-//          of the block structure, so no atomics and a deterministic order); the G lanes stream
-//          the entries and the group's full sum goes to y[i].
-// G is chosen on the host per segment as the smallest group that covers the segment in one pass,
-// so segments that share a wavefront take the same number of iterations (no divergence); G = 64
-// segments loop.  val / idx are read once: non-temporal, 16 B per lane where w allows.
+// Merge-based, flat streaming design.  Per width bucket w the stored w-wide rows of
+// the product are one stream of *entries*, ordered by output *segment*:
+//   kind 0, mul!(y, B', x)  (multiply_1DVBC.jl:90-134, multiply_VBC.jl:93-147, TrSpMV.jl:1-20):
+//       segment = stripe, entry = stored row; y[j : j+w-1] += val_row * x[row].
+//   kind 1, mul!(y, B, x)   (multiply_1DVBC.jl:13-83, multiply_VBC.jl:7-87):
+//       segment = output row i of B, entry = (i, stripe) block; y[i] += val_row · x[j : j+w-1].
+// Each entry's 32-bit key holds its gather index (kind 0: x row; kind 1: first x column) and, in
+// bit 31, a HEAD flag marking the first entry of a segment.  The stream is cut into tiles of
+// RPI x K entries: a wave's 64 lanes form RPI = 64/LPR row *slots* of LPR lanes (V consecutive
+// columns per lane, 16 B per lane where w allows); slot s owns the K consecutive entries
+// s*K .. s*K+K-1 of the tile, stored k-major so every load instruction is one contiguous, fully
+// coalesced sweep of the stream.  A slot accumulates its entries serially (HEAD restarts the sum;
+// segments that close inside the slot are written at once), a segmented scan across the slots
+// (wavefront shuffles) joins segments that cross slots, and the open segment flows into the next
+// tile in registers.  Every wave owns a contiguous range of tiles; a segment is written by the wave
+// that holds its HEAD (it applies beta); the partial of a segment continued from an earlier range is
+// written to the range's carry slot and added by the fix-up kernel in range order -- results are
+// deterministic.  val and keys are read once: non-temporal loads keep x resident in the caches.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -22,29 +27,30 @@ namespace vbc {
 
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlock = kBlockThreads / 64;
+constexpr int kTileK = 8;  // entries per slot per tile
+constexpr uint32_t kHead = 0x80000000u;
 
-// One bin of a fused launch.  Read by every workgroup through the scalar cache.
+// One width bucket of a fused launch (read through the scalar cache).
 struct Bin {
-    int32_t key;      // dispatch key: kind * 1024 + wvariant * 128 + G (wvariant 0 = runtime w)
-    int32_t w;        // values per stored row (block width)
-    int32_t G;        // lanes per segment group (4..64)
-    int32_t nseg;     // segments in the bin
-    int32_t vblock0;  // first virtual block of the bin in the launch
-    int32_t nvblock;  // virtual blocks of the bin
-    const int32_t *rptr;  // nseg+1 prefix of stored rows (kind 0) / entries (kind 1), bin-relative
-    const int32_t *out;   // nseg: kind 0 -> first y column of the stripe; kind 1 -> y row
-    const int32_t *idx;   // per stored row: kind 0 -> x row; kind 1 -> first x column of entry
-    const void *val;      // rows * w values, row-major w-wide rows, 16-B aligned
+    int32_t kind;     // 0: B'x, 1: Bx
+    int32_t wkey;     // dispatch width: 1..8, or 0 = runtime width (w > 8)
+    int32_t w;        // entry width
+    int32_t rpi;      // slots per tile (64 / lanes-per-entry)
+    int32_t range0;   // first range (wave) of this bucket in the launch
+    int32_t nranges;  // ranges of this bucket
+    int32_t tiles_per_range;
+    int32_t ntiles;   // tiles of this bucket
+    const uint32_t *key;  // entries (tile-permuted): HEAD | gather index
+    const void *val;      // entries * w values, 16-B aligned
+    const int32_t *rseg;  // per range: number of HEADs before the range (segment base)
+    const int32_t *out;   // per segment: kind 0 -> first y column; kind 1 -> y row
+    void *carry;          // per range: w (kind 0) or 1 (kind 1) partial values
+    int32_t *carry_seg;   // per range: continued segment, or -1
 };
 
 __host__ __device__ constexpr int vec_elems(int esz, int w)
 {
     return esz == 8 ? (w % 2 == 0 ? 2 : 1) : (w % 4 == 0 ? 4 : (w % 2 == 0 ? 2 : 1));
-}
-
-__host__ __device__ constexpr int make_key(int kind, int wvariant, int G)
-{
-    return kind * 1024 + wvariant * 128 + G;
 }
 
 template <typename T, int V>
@@ -60,195 +66,284 @@ __device__ __forceinline__ void ld_stream(const T *__restrict__ p, T (&r)[V])
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// kind 0: y[j + c] = alpha * sum_r val[r, c] * x[idx[r]] (+ beta * y[j + c])
-// ---------------------------------------------------------------------------------------------
-template <typename T, int W_, int G>
-__device__ __forceinline__ void seg_transposed(const Bin &b, int vb, int tid, const T *__restrict__ x,
-                                               T *__restrict__ y, T alpha, T beta, bool rd)
+// Kind 1 keeps per-lane column partials; the LPR lanes of a slot are summed when a segment is
+// written.  Called with the whole slot active (its lanes share every control decision).
+template <typename T, int V>
+__device__ __forceinline__ T slot_sum(const T (&v)[V], int lane, int sub, int LPR)
 {
-    constexpr bool kGeneric = (W_ == 0);
-    constexpr int V = kGeneric ? 1 : vec_elems(sizeof(T), W_);
-    if constexpr (!kGeneric && G < W_ / V) {
-        return;  // never generated by the host (G smaller than one row)
-    } else {
-        const int w = kGeneric ? b.w : W_;
-        const int LPR = w / V;       // lanes per stored row
-        const int RPI = G / LPR;     // rows per iteration
-        constexpr int SPW = 64 / G;  // segments per wavefront
-        const int lane = tid & 63;
-        const int g = lane / G, k = lane % G;
-        const int seg = (vb * kWavesPerBlock + (tid >> 6)) * SPW + g;
-        const bool segok = seg < b.nseg;
-        const int ro = k / LPR, sub = k - ro * LPR;
-        const bool laneok = ro < RPI;
-        int r0 = 0, r1 = 0;
-        if (segok) {
-            r0 = b.rptr[seg];
-            r1 = b.rptr[seg + 1];
-        }
-        const T *__restrict__ val = static_cast<const T *>(b.val) + sub * V;
-        const int32_t *__restrict__ idx = b.idx;
-        T acc[V];
+    T s = T(0);
 #pragma unroll
-        for (int e = 0; e < V; e++) acc[e] = T(0);
-        if (laneok) {
-            int r = r0 + ro;
-            for (; r + RPI < r1; r += 2 * RPI) {
-                const int i0 = __builtin_nontemporal_load(idx + r);
-                const int i1 = __builtin_nontemporal_load(idx + r + RPI);
-                T v0[V], v1[V];
-                ld_stream<T, V>(val + (size_t)r * w, v0);
-                ld_stream<T, V>(val + (size_t)(r + RPI) * w, v1);
-                const T x0 = x[i0], x1 = x[i1];
-#pragma unroll
-                for (int e = 0; e < V; e++) acc[e] = __builtin_fma(v0[e], x0, acc[e]);
-#pragma unroll
-                for (int e = 0; e < V; e++) acc[e] = __builtin_fma(v1[e], x1, acc[e]);
-            }
-            if (r < r1) {
-                const int i0 = __builtin_nontemporal_load(idx + r);
-                T v0[V];
-                ld_stream<T, V>(val + (size_t)r * w, v0);
-                const T x0 = x[i0];
-#pragma unroll
-                for (int e = 0; e < V; e++) acc[e] = __builtin_fma(v0[e], x0, acc[e]);
-            }
-        }
-        // Tree over the RPI row slots of the group: after the step with stride s, slot ro holds the
-        // sum of slots [ro, ro + 2s) clipped to RPI; slot 0 ends with the column sums.
-        for (int s = 1; s < RPI; s <<= 1) {
-            const int src = (lane + s * LPR) & 63;
-#pragma unroll
-            for (int e = 0; e < V; e++) {
-                const T t = __shfl(acc[e], src, 64);
-                if (ro + s < RPI) acc[e] += t;
-            }
-        }
-        if (segok && laneok && ro == 0) {
-            T *__restrict__ yo = y + b.out[seg] + sub * V;
-#pragma unroll
-            for (int e = 0; e < V; e++) {
-                T r = alpha * acc[e];
-                if (rd) r = __builtin_fma(beta, yo[e], r);
-                yo[e] = r;
-            }
-        }
+    for (int e = 0; e < V; e++) s += v[e];
+    for (int d = 1; d < LPR; d <<= 1) {
+        const T t = __shfl(s, (lane + d) & 63, 64);
+        if (sub + d < LPR) s += t;
     }
+    return s;
 }
 
-// ---------------------------------------------------------------------------------------------
-// kind 1: y[i] = alpha * sum_e sum_c val[e, c] * x[idx[e] + c] (+ beta * y[i])
-// ---------------------------------------------------------------------------------------------
-template <typename T, int W_, int G>
-__device__ __forceinline__ void seg_forward(const Bin &b, int vb, int tid, const T *__restrict__ x,
-                                            T *__restrict__ y, T alpha, T beta, bool rd)
+// Owner write of one segment: y = alpha * v (+ beta * y).
+template <typename T, int KIND, int V>
+__device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int sub, int LPR, int lane,
+                                     T *__restrict__ y, T alpha, T beta, bool rd)
 {
-    constexpr bool kGeneric = (W_ == 0);
-    constexpr int V = kGeneric ? 1 : vec_elems(sizeof(T), W_);
-    if constexpr (!kGeneric && G < W_ / V) {
-        return;
+    if constexpr (KIND == 0) {
+        T *__restrict__ yo = y + b.out[seg] + sub * V;
+#pragma unroll
+        for (int e = 0; e < V; e++) {
+            T r = alpha * v[e];
+            if (rd) r = __builtin_fma(beta, yo[e], r);
+            yo[e] = r;
+        }
     } else {
-        const int w = kGeneric ? b.w : W_;
-        const int LPR = w / V;
-        const int EPI = G / LPR;  // entries per iteration
-        const int GA = EPI * LPR;
-        constexpr int SPW = 64 / G;
-        const int lane = tid & 63;
-        const int g = lane / G, k = lane % G;
-        const int seg = (vb * kWavesPerBlock + (tid >> 6)) * SPW + g;
-        const bool segok = seg < b.nseg;
-        const int eo = k / LPR, sub = k - eo * LPR;
-        const bool laneok = eo < EPI;
-        int e0 = 0, e1 = 0;
-        if (segok) {
-            e0 = b.rptr[seg];
-            e1 = b.rptr[seg + 1];
-        }
-        const T *__restrict__ val = static_cast<const T *>(b.val) + sub * V;
-        const int32_t *__restrict__ idx = b.idx;
-        const T *__restrict__ xs = x + sub * V;
-        T acc = T(0);
-        if (laneok) {
-            int e = e0 + eo;
-            for (; e + EPI < e1; e += 2 * EPI) {
-                const int j0 = __builtin_nontemporal_load(idx + e);
-                const int j1 = __builtin_nontemporal_load(idx + e + EPI);
-                T v0[V], v1[V];
-                ld_stream<T, V>(val + (size_t)e * w, v0);
-                ld_stream<T, V>(val + (size_t)(e + EPI) * w, v1);
-#pragma unroll
-                for (int c = 0; c < V; c++) acc = __builtin_fma(v0[c], xs[j0 + c], acc);
-#pragma unroll
-                for (int c = 0; c < V; c++) acc = __builtin_fma(v1[c], xs[j1 + c], acc);
-            }
-            if (e < e1) {
-                const int j0 = __builtin_nontemporal_load(idx + e);
-                T v0[V];
-                ld_stream<T, V>(val + (size_t)e * w, v0);
-#pragma unroll
-                for (int c = 0; c < V; c++) acc = __builtin_fma(v0[c], xs[j0 + c], acc);
-            }
-        }
-        for (int s = 1; s < GA; s <<= 1) {
-            const T t = __shfl(acc, (lane + s) & 63, 64);
-            if (k + s < GA) acc += t;
-        }
-        if (segok && k == 0) {
+        const T s = slot_sum<T, V>(v, lane, sub, LPR);
+        if (sub == 0) {
             T *__restrict__ yo = y + b.out[seg];
-            T r = alpha * acc;
+            T r = alpha * s;
             if (rd) r = __builtin_fma(beta, *yo, r);
             *yo = r;
         }
     }
 }
 
-#define VBC_G_CASES(KIND, FN, W_)                                                                 \
-    case make_key(KIND, W_, 4): FN<T, W_, 4>(b, vb, tid, x, y, alpha, beta, rd); break;                \
-    case make_key(KIND, W_, 8): FN<T, W_, 8>(b, vb, tid, x, y, alpha, beta, rd); break;                \
-    case make_key(KIND, W_, 16): FN<T, W_, 16>(b, vb, tid, x, y, alpha, beta, rd); break;              \
-    case make_key(KIND, W_, 32): FN<T, W_, 32>(b, vb, tid, x, y, alpha, beta, rd); break;              \
-    case make_key(KIND, W_, 64): FN<T, W_, 64>(b, vb, tid, x, y, alpha, beta, rd); break;
-
-#define VBC_W_CASES(KIND, FN)                                                                     \
-    VBC_G_CASES(KIND, FN, 0)                                                                      \
-    VBC_G_CASES(KIND, FN, 1)                                                                      \
-    VBC_G_CASES(KIND, FN, 2)                                                                      \
-    VBC_G_CASES(KIND, FN, 3)                                                                      \
-    VBC_G_CASES(KIND, FN, 4)                                                                      \
-    VBC_G_CASES(KIND, FN, 5)                                                                      \
-    VBC_G_CASES(KIND, FN, 6)                                                                      \
-    VBC_G_CASES(KIND, FN, 7)                                                                      \
-    VBC_G_CASES(KIND, FN, 8)
-
-// Fused launch: blocks walk the virtual blocks of all bins grid-stride; each virtual block finds
-// its bin by binary search on vblock0 (scalar, uniform) and runs that bin's specialisation.
-template <typename T, int KIND>
-__global__ __launch_bounds__(kBlockThreads) void spmv_bins(const Bin *__restrict__ bins, int nbins,
-                                                           int total_vblocks,
-                                                           const T *__restrict__ x,
-                                                           T *__restrict__ y, T alpha, T beta,
-                                                           int rd_i)
+// Hand a continued segment's partial to the fix-up pass.
+template <typename T, int KIND, int V>
+__device__ __forceinline__ void hand_off(const Bin &b, int r, int seg, const T (&v)[V], int sub, int LPR,
+                                         int lane, int w)
 {
-    const bool rd = rd_i != 0;
-    for (int v = blockIdx.x; v < total_vblocks; v += gridDim.x) {
-        int lo = 0, hi = nbins - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (bins[mid].vblock0 <= v) lo = mid; else hi = mid - 1;
-        }
-        const Bin b = bins[lo];
-        const int vb = v - b.vblock0;
-        // Opaque thread id: keeps LICM from hoisting every variant's lane arithmetic out of the
-        // grid-stride loop (that alone costs ~200 VGPRs and 3/4 of the occupancy).
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        if constexpr (KIND == 0) {
-            switch (b.key) { VBC_W_CASES(0, seg_transposed) default: break; }
-        } else {
-            switch (b.key) { VBC_W_CASES(1, seg_forward) default: break; }
-        }
+    if constexpr (KIND == 0) {
+        T *c = static_cast<T *>(b.carry) + (size_t)r * w + sub * V;
+#pragma unroll
+        for (int e = 0; e < V; e++) c[e] = v[e];
+    } else {
+        const T s = slot_sum<T, V>(v, lane, sub, LPR);
+        if (sub == 0) static_cast<T *>(b.carry)[r] = s;
     }
+    if (sub == 0) b.carry_seg[r] = seg;
+}
+
+template <typename T, int KIND, int W_>
+__device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T *__restrict__ x,
+                                          T *__restrict__ y, T alpha, T beta, bool rd)
+{
+    constexpr bool kGeneric = (W_ == 0);
+    constexpr int V = kGeneric ? 1 : vec_elems(sizeof(T), W_);
+    constexpr int K = kTileK;
+    const int w = kGeneric ? b.w : W_;
+    const int LPR = w / V;
+    const int RPI = b.rpi;
+    const int slot = lane / LPR;
+    const int sub = lane - slot * LPR;
+    const bool active = slot < RPI;
+    const int t0 = r * b.tiles_per_range;
+    const int t1 = min(t0 + b.tiles_per_range, b.ntiles);
+    if (t0 >= t1) return;
+    const T *__restrict__ val = static_cast<const T *>(b.val);
+    const uint32_t *__restrict__ key = b.key;
+    const size_t tile_rows = (size_t)RPI * K;
+
+    int seg_base = b.rseg[r];  // segments whose HEAD precedes the current tile
+    // A range that does not start at a HEAD continues the segment open before it.
+    const bool starts_at_head = (key[(size_t)t0 * tile_rows] & kHead) != 0;
+    T carry[V];                // value of the segment open when entering the tile
+#pragma unroll
+    for (int e = 0; e < V; e++) carry[e] = T(0);
+    bool owned = false;        // the open segment's HEAD lies in this range
+
+    for (int t = t0; t < t1; t++) {
+        const size_t base = (size_t)t * tile_rows;
+        uint32_t kk[K];
+        T v[K][V];
+        T xv[K][V];
+        if (active) {
+#pragma unroll
+            for (int k = 0; k < K; k++) kk[k] = __builtin_nontemporal_load(key + base + (size_t)k * RPI + slot);
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                ld_stream<T, V>(val + (base + (size_t)k * RPI + slot) * w + sub * V, v[k]);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const uint32_t gi = kk[k] & ~kHead;
+                if constexpr (KIND == 0) {
+                    const T xg = x[gi];
+#pragma unroll
+                    for (int e = 0; e < V; e++) xv[k][e] = xg;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < V; e++) xv[k][e] = x[gi + sub * V + e];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                kk[k] = 0;
+#pragma unroll
+                for (int e = 0; e < V; e++) v[k][e] = xv[k][e] = T(0);
+            }
+        }
+        // HEADs per slot and their exclusive prefix over the slots
+        int nh = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) nh += (int)(kk[k] >> 31);
+        int pre = nh;
+        for (int d = 1; d < RPI; d <<= 1) {
+            const int o = __shfl(pre, (lane - d * LPR) & 63, 64);
+            if (slot >= d) pre += o;
+        }
+        const int tile_heads = __shfl(pre, (RPI - 1) * LPR, 64);
+        pre -= nh;
+
+        // lane-serial pass over the slot's K entries
+        T lead[V], cur[V];
+#pragma unroll
+        for (int e = 0; e < V; e++) lead[e] = cur[e] = T(0);
+        int seg = seg_base + pre - 1;  // segment open at the slot's start
+        bool seen = false;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (kk[k] & kHead) {
+                if (seen)  // opened and closed inside this slot: owned and complete
+                    emit<T, KIND, V>(b, seg, cur, sub, LPR, lane, y, alpha, beta, rd);
+                seg++;
+                seen = true;
+#pragma unroll
+                for (int e = 0; e < V; e++) cur[e] = T(0);
+            }
+#pragma unroll
+            for (int e = 0; e < V; e++) {
+                const T p = v[k][e] * xv[k][e];
+                if (seen) cur[e] += p;
+                else lead[e] += p;
+            }
+        }
+        // segmented inclusive scan of (seen, seen ? cur : lead) over the slots
+        bool f = seen;
+        T s[V];
+#pragma unroll
+        for (int e = 0; e < V; e++) s[e] = seen ? cur[e] : lead[e];
+        for (int d = 1; d < RPI; d <<= 1) {
+            const int src = (lane - d * LPR) & 63;
+            const bool of = __shfl((int)f, src, 64) != 0;
+            T os[V];
+#pragma unroll
+            for (int e = 0; e < V; e++) os[e] = __shfl(s[e], src, 64);
+            if (slot >= d) {
+                if (!f) {
+#pragma unroll
+                    for (int e = 0; e < V; e++) s[e] += os[e];
+                }
+                f = f || of;
+            }
+        }
+        // value entering each slot (exclusive scan)
+        const int srcx = (lane - LPR) & 63;
+        bool ef = __shfl((int)f, srcx, 64) != 0;
+        T es[V];
+#pragma unroll
+        for (int e = 0; e < V; e++) es[e] = __shfl(s[e], srcx, 64);
+        if (slot == 0) {
+            ef = false;
+#pragma unroll
+            for (int e = 0; e < V; e++) es[e] = T(0);
+        }
+        // the segment open when entering a slot closes at the slot's first HEAD
+        if (active && seen) {
+            const int cseg = seg_base + pre - 1;
+            const bool from_tile = ef || owned;  // opened inside this range
+            if (from_tile || !starts_at_head) {
+                T tot[V];
+#pragma unroll
+                for (int e = 0; e < V; e++) tot[e] = (ef ? es[e] : carry[e] + es[e]) + lead[e];
+                if (from_tile)
+                    emit<T, KIND, V>(b, cseg, tot, sub, LPR, lane, y, alpha, beta, rd);
+                else
+                    hand_off<T, KIND, V>(b, r, cseg, tot, sub, LPR, lane, w);
+            }
+        }
+        // flow into the next tile
+        const int last = (RPI - 1) * LPR + sub;
+        const bool lf = __shfl((int)f, last, 64) != 0;
+#pragma unroll
+        for (int e = 0; e < V; e++) {
+            const T ls = __shfl(s[e], last, 64);
+            carry[e] = lf ? ls : carry[e] + ls;
+        }
+        owned = owned || lf;
+        seg_base += tile_heads;
+    }
+    // the segment still open at the end of the range
+    if (active && slot == 0) {
+        const int cseg = seg_base - 1;
+        if (owned)
+            emit<T, KIND, V>(b, cseg, carry, sub, LPR, lane, y, alpha, beta, rd);
+        else if (!starts_at_head)  // no HEAD in the whole range: all of it continues cseg
+            hand_off<T, KIND, V>(b, r, cseg, carry, sub, LPR, lane, w);
+    }
+}
+
+#define VBC_W_CASES(KIND)                                                                          \
+    case 0: run_range<T, KIND, 0>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 1: run_range<T, KIND, 1>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 2: run_range<T, KIND, 2>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 3: run_range<T, KIND, 3>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 4: run_range<T, KIND, 4>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 5: run_range<T, KIND, 5>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 6: run_range<T, KIND, 6>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 7: run_range<T, KIND, 7>(b, r, lane, x, y, alpha, beta, rd); break;                        \
+    case 8: run_range<T, KIND, 8>(b, r, lane, x, y, alpha, beta, rd); break;
+
+// One wave per range; the wave finds its bucket by a scalar scan of the (few) bins.
+template <typename T, int KIND>
+__global__ __launch_bounds__(kBlockThreads) void spmv_ranges(const Bin *__restrict__ bins, int nbins,
+                                                             int total_ranges, const T *__restrict__ x,
+                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= total_ranges) return;
+    int bi = 0;
+    while (bi + 1 < nbins && bins[bi + 1].range0 <= rg) bi++;
+    const Bin b = bins[bi];
+    const int r = rg - b.range0;
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) b.carry_seg[r] = -1;  // overwritten below when the range continues a segment
+    const bool rd = rd_i != 0;
+    switch (b.wkey) { VBC_W_CASES(KIND) default: break; }
+}
+
+// Fix-up: add every continued-segment partial (summed in range order: deterministic) and apply
+// beta to the segments that own no entry (fill list: y indices).
+template <typename T, int KIND>
+__global__ __launch_bounds__(kBlockThreads) void fixup(const Bin *__restrict__ bins, int nbins, int total_ranges,
+                                                       const int32_t *__restrict__ fill, int nfill,
+                                                       T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const int i = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (i < total_ranges) {
+        int bi = 0;
+        while (bi + 1 < nbins && bins[bi + 1].range0 <= i) bi++;
+        const Bin &b = bins[bi];
+        const int r = i - b.range0;
+        const int seg = b.carry_seg[r];
+        if (seg < 0 || (r > 0 && b.carry_seg[r - 1] == seg)) return;
+        const int wc = KIND == 0 ? b.w : 1;
+        T *__restrict__ yo = y + b.out[seg];
+        for (int c = 0; c < wc; c++) {
+            T s = T(0);
+            for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++)
+                s += static_cast<const T *>(b.carry)[(size_t)q * wc + c];
+            yo[c] = __builtin_fma(alpha, s, yo[c]);
+        }
+    } else if (i - total_ranges < nfill) {
+        T *yo = y + fill[i - total_ranges];
+        *yo = rd_i ? beta * *yo : T(0);
+    }
+}
+
+// y = beta * y (forward products with several width buckets accumulate bucket by bucket).
+template <typename T>
+__global__ __launch_bounds__(kBlockThreads) void scale(T *__restrict__ y, int64_t n, T beta, int rd_i)
+{
+    for (int64_t i = blockIdx.x * (int64_t)kBlockThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlockThreads)
+        y[i] = rd_i ? beta * y[i] : T(0);
 }
 
 }  // namespace vbc

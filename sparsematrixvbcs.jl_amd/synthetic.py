@@ -58,3 +58,35 @@ def north_star(dtype=np.float64, scale=1.0, seed=0xDEADBEEF, mixed=False):
         return vbr_1dvbc(m, L, q, w, 8, dtype, seed)
     L = m // 4
     return vbr_1dvbc(m, L, int(round(2.5e7 * scale)), 4, 8, dtype, seed)
+
+
+def fe_grid_2d(N, dof=2, W=8, dtype=np.float64, seed=0xDEADBEEF):
+    """SuiteSparse-like finite-element operator: the 5-point stencil on an N x N node grid with
+    `dof` unknowns per node (dense dof x dof coupling blocks), as a 1DVBC whose stripes are the node
+    columns (what StrictChunker finds: the dof columns of a node share one pattern).  N = 2236,
+    dof = 2 gives 1.0e7 x 1.0e7 with 1.0e8 stored values, no fill -- the 'SuiteSparse-like'
+    north-star size of BASELINE.json with the locality of a mesh (x gathers hit cache)."""
+    rng = np.random.default_rng(seed)
+    nodes = N * N
+    node = np.arange(nodes, dtype=np.int64)
+    a, b = node // N, node % N
+    offs = np.array([-N, -1, 0, 1, N], dtype=np.int64)  # ascending neighbour order
+    valid = np.stack([a > 0, b > 0, np.ones(nodes, bool), b < N - 1, a < N - 1], axis=1)
+    nb = (node[:, None] + offs[None, :])[valid]          # neighbours, row-major by node: sorted
+    cnt = valid.sum(axis=1).astype(np.int64)             # neighbour blocks per stripe
+    rows = (nb[:, None] * dof + np.arange(dof)[None, :]).reshape(-1)  # 0-based x rows
+    L = nodes
+    spl = 1 + np.arange(L + 1, dtype=np.int64) * dof
+    pos = np.empty(L + 1, np.int64)
+    pos[0] = 1
+    np.cumsum(cnt * dof, out=pos[1:])
+    pos[1:] += 1
+    ofs = np.empty(L + 1, np.int64)
+    ofs[0] = 1
+    np.cumsum(cnt * dof * dof, out=ofs[1:])
+    ofs[1:] += 1
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + _simd_pad(W, dtype), dtype)
+    val[:nv] = rng.random(nv, dtype=np.float64 if dtype == np.float64 else np.float32)
+    m = nodes * dof
+    return SparseMatrix1DVBC(W, m, m, SplitPartition(spl), pos, rows + 1, ofs, val)
