@@ -84,6 +84,8 @@ struct vbc_handle {
     bool f_scale = false;         // forward with several buckets: scale y by beta first
     int64_t bytes_t = 0, bytes_f = 0;
     int target_ranges = 4096;     // waves resident on the device (one range each)
+    int tile_k = vbc::kTileKDefault;  // entries per slot per tile
+    int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
 };
 
 namespace vbc {
@@ -130,7 +132,8 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     const int V = w <= 8 ? vec_elems(esz, w) : 1;
     const int LPR = w / V;
     const int RPI = 64 / LPR;
-    const int64_t tile_rows = (int64_t)RPI * kTileK;
+    const int K = h->tile_k;
+    const int64_t tile_rows = (int64_t)RPI * K;
     const int64_t R = (int64_t)ents.size();
     const int64_t ntiles = (R + tile_rows - 1) / tile_rows;
     if (ntiles >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
@@ -149,6 +152,14 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     pb.b.nranges = (int32_t)nr;
     pb.b.tiles_per_range = (int32_t)tpr;
     pb.b.ntiles = (int32_t)ntiles;
+    pb.b.tile_k = K;
+    pb.b.pipe = h->pipe;
+    pb.b.out_affine = 1;
+    pb.b.out_base = out.empty() ? 0 : out[0];
+    pb.b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
+    for (size_t q = 1; q < out.size() && pb.b.out_affine; q++)
+        pb.b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * pb.b.out_stride;
+    if (getenv("VBC_NO_AFFINE")) pb.b.out_affine = 0;  // A/B knob
     range0 += (int)nr;
     const int64_t Rp = ntiles * tile_rows;
     pb.o_key = ar.reserve(Rp * 4);
@@ -164,7 +175,7 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     int64_t heads = 0;
     for (int64_t t = 0; t < Rp; t++) {
         const int64_t tile = t / tile_rows, within = t - tile * tile_rows;
-        const int64_t slot = within / kTileK, k = within - slot * kTileK;
+        const int64_t slot = within / K, k = within - slot * K;
         const int64_t phys = tile * tile_rows + k * RPI + slot;
         if (within == 0 && tile % tpr == 0) rseg[tile / tpr] = (int32_t)heads;
         if (t < R) {
@@ -330,11 +341,16 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipGetDeviceProperties failed"); }
     int occ = 0;
     if (dtype == VBC_F64)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<double, 0>, kBlockThreads, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<double, 0, kTileKDefault, kPipeDefault>, kBlockThreads, 0);
     else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<float, 0>, kBlockThreads, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<float, 0, kTileKDefault, kPipeDefault>, kBlockThreads, 0);
     h->target_ranges = prop.multiProcessorCount * std::max(1, std::min(occ, 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_TILE_K")) {
+        const int k = atoi(e);
+        h->tile_k = (k == 4 || k == 8) ? k : kTileKDefault;
+    }
+    if (const char *e = getenv("VBC_PIPE")) h->pipe = atoi(e) == 2 ? 2 : 3;
 
     Arena ar;
     std::vector<PendingBin> pt;
@@ -387,12 +403,19 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
     T *ys = static_cast<T *>(y);
     if (L.total_ranges > 0) {
         const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
-        if (kind == 0)
-            hipLaunchKernelGGL((spmv_ranges<T, 0>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                               (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
-        else
-            hipLaunchKernelGGL((spmv_ranges<T, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                               (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+        const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;
+#define VBC_LAUNCH(KIND, KK, PP)                                                                         \
+    hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins, \
+                       (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd)
+        const int P = L.bins.empty() ? kPipeDefault : L.bins[0].pipe;
+        if (kind == 0) {
+            if (P == 2) { if (K == 4) VBC_LAUNCH(0, 4, 2); else VBC_LAUNCH(0, 8, 2); }
+            else { if (K == 4) VBC_LAUNCH(0, 4, 3); else VBC_LAUNCH(0, 8, 3); }
+        } else {
+            if (P == 2) { if (K == 4) VBC_LAUNCH(1, 4, 2); else VBC_LAUNCH(1, 8, 2); }
+            else { if (K == 4) VBC_LAUNCH(1, 4, 3); else VBC_LAUNCH(1, 8, 3); }
+        }
+#undef VBC_LAUNCH
         VBC_HIP(hipGetLastError());
     }
     const int work = (L.total_ranges > 1 ? L.total_ranges : 0) + L.nfill;

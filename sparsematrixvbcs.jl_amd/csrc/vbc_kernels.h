@@ -27,8 +27,18 @@ namespace vbc {
 
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlock = kBlockThreads / 64;
-constexpr int kTileK = 8;  // entries per slot per tile
+constexpr int kTileKDefault = 4;  // entries per slot per tile (runtime choice: 4 or 8)
+constexpr int kPipeDefault = 2;   // software-pipeline depth (runtime choice: 2 or 3)
 constexpr uint32_t kHead = 0x80000000u;
+
+// Global-address-space views: the Bin's pointers are loaded from memory, so without these the
+// compiler emits flat_* accesses (which also count in lgkmcnt and force conservative waits).
+template <typename T>
+using gptr = __attribute__((address_space(1))) T *;
+template <typename T>
+__device__ __forceinline__ gptr<T> G(T *p) { return (gptr<T>)p; }
+template <typename T>
+__device__ __forceinline__ gptr<const T> G(const T *p) { return (gptr<const T>)p; }
 
 // One width bucket of a fused launch (read through the scalar cache).
 struct Bin {
@@ -40,6 +50,11 @@ struct Bin {
     int32_t nranges;  // ranges of this bucket
     int32_t tiles_per_range;
     int32_t ntiles;   // tiles of this bucket
+    int32_t tile_k;   // entries per slot per tile (4 or 8)
+    int32_t pipe;     // software-pipeline depth (2 or 3)
+    int32_t out_affine;  // 1: out[s] == out_base + s * out_stride (no table lookup)
+    int32_t out_base;
+    int32_t out_stride;
     const uint32_t *key;  // entries (tile-permuted): HEAD | gather index
     const void *val;      // entries * w values, 16-B aligned
     const int32_t *rseg;  // per range: number of HEADs before the range (segment base)
@@ -54,13 +69,13 @@ __host__ __device__ constexpr int vec_elems(int esz, int w)
 }
 
 template <typename T, int V>
-__device__ __forceinline__ void ld_stream(const T *__restrict__ p, T (&r)[V])
+__device__ __forceinline__ void ld_stream(gptr<const T> p, T (&r)[V])
 {
     if constexpr (V == 1) {
         r[0] = __builtin_nontemporal_load(p);
     } else {
         typedef T vt __attribute__((ext_vector_type(V)));
-        const vt t = __builtin_nontemporal_load(reinterpret_cast<const vt *>(p));
+        const vt t = __builtin_nontemporal_load((gptr<const vt>)p);
 #pragma unroll
         for (int e = 0; e < V; e++) r[e] = t[e];
     }
@@ -82,12 +97,17 @@ __device__ __forceinline__ T slot_sum(const T (&v)[V], int lane, int sub, int LP
 }
 
 // Owner write of one segment: y = alpha * v (+ beta * y).
+__device__ __forceinline__ int out_of(const Bin &b, int seg)
+{
+    return b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
+}
+
 template <typename T, int KIND, int V>
 __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int sub, int LPR, int lane,
                                      T *__restrict__ y, T alpha, T beta, bool rd)
 {
     if constexpr (KIND == 0) {
-        T *__restrict__ yo = y + b.out[seg] + sub * V;
+        gptr<T> yo = G(y) + out_of(b, seg) + sub * V;
 #pragma unroll
         for (int e = 0; e < V; e++) {
             T r = alpha * v[e];
@@ -97,7 +117,7 @@ __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int
     } else {
         const T s = slot_sum<T, V>(v, lane, sub, LPR);
         if (sub == 0) {
-            T *__restrict__ yo = y + b.out[seg];
+            gptr<T> yo = G(y) + out_of(b, seg);
             T r = alpha * s;
             if (rd) r = __builtin_fma(beta, *yo, r);
             *yo = r;
@@ -111,23 +131,22 @@ __device__ __forceinline__ void hand_off(const Bin &b, int r, int seg, const T (
                                          int lane, int w)
 {
     if constexpr (KIND == 0) {
-        T *c = static_cast<T *>(b.carry) + (size_t)r * w + sub * V;
+        gptr<T> c = G(static_cast<T *>(b.carry)) + (size_t)r * w + sub * V;
 #pragma unroll
         for (int e = 0; e < V; e++) c[e] = v[e];
     } else {
         const T s = slot_sum<T, V>(v, lane, sub, LPR);
-        if (sub == 0) static_cast<T *>(b.carry)[r] = s;
+        if (sub == 0) G(static_cast<T *>(b.carry))[r] = s;
     }
-    if (sub == 0) b.carry_seg[r] = seg;
+    if (sub == 0) G(b.carry_seg)[r] = seg;
 }
 
-template <typename T, int KIND, int W_>
+template <typename T, int KIND, int W_, int K, int P>
 __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T *__restrict__ x,
                                           T *__restrict__ y, T alpha, T beta, bool rd)
 {
     constexpr bool kGeneric = (W_ == 0);
     constexpr int V = kGeneric ? 1 : vec_elems(sizeof(T), W_);
-    constexpr int K = kTileK;
     const int w = kGeneric ? b.w : W_;
     const int LPR = w / V;
     const int RPI = b.rpi;
@@ -137,11 +156,12 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     const int t0 = r * b.tiles_per_range;
     const int t1 = min(t0 + b.tiles_per_range, b.ntiles);
     if (t0 >= t1) return;
-    const T *__restrict__ val = static_cast<const T *>(b.val);
-    const uint32_t *__restrict__ key = b.key;
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> xg_ = G(x);
     const size_t tile_rows = (size_t)RPI * K;
 
-    int seg_base = b.rseg[r];  // segments whose HEAD precedes the current tile
+    int seg_base = G(b.rseg)[r];  // segments whose HEAD precedes the current tile
     // A range that does not start at a HEAD continues the segment open before it.
     const bool starts_at_head = (key[(size_t)t0 * tile_rows] & kHead) != 0;
     T carry[V];                // value of the segment open when entering the tile
@@ -149,37 +169,46 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     for (int e = 0; e < V; e++) carry[e] = T(0);
     bool owned = false;        // the open segment's HEAD lies in this range
 
-    for (int t = t0; t < t1; t++) {
-        const size_t base = (size_t)t * tile_rows;
-        uint32_t kk[K];
-        T v[K][V];
-        T xv[K][V];
-        if (active) {
+    // Stage 1: keys and values of a tile (one coalesced sweep per k).
+    auto load_stream = [&](int t, uint32_t (&kk)[K], T (&v)[K][V]) {
+        if (active && t < t1) {
+            const size_t base = (size_t)t * tile_rows + slot;
 #pragma unroll
-            for (int k = 0; k < K; k++) kk[k] = __builtin_nontemporal_load(key + base + (size_t)k * RPI + slot);
+            for (int k = 0; k < K; k++) kk[k] = __builtin_nontemporal_load(key + base + (size_t)k * RPI);
 #pragma unroll
-            for (int k = 0; k < K; k++)
-                ld_stream<T, V>(val + (base + (size_t)k * RPI + slot) * w + sub * V, v[k]);
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const uint32_t gi = kk[k] & ~kHead;
-                if constexpr (KIND == 0) {
-                    const T xg = x[gi];
-#pragma unroll
-                    for (int e = 0; e < V; e++) xv[k][e] = xg;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < V; e++) xv[k][e] = x[gi + sub * V + e];
-                }
-            }
+            for (int k = 0; k < K; k++) ld_stream<T, V>(val + (base + (size_t)k * RPI) * w + sub * V, v[k]);
         } else {
 #pragma unroll
             for (int k = 0; k < K; k++) {
                 kk[k] = 0;
 #pragma unroll
-                for (int e = 0; e < V; e++) v[k][e] = xv[k][e] = T(0);
+                for (int e = 0; e < V; e++) v[k][e] = T(0);
             }
         }
+    };
+    // Stage 2: the x gathers of a tile whose keys have arrived (kind 0: one x per entry).
+    constexpr int XV = KIND == 0 ? 1 : V;
+    auto gather = [&](int t, const uint32_t (&kk)[K], T (&xv)[K][XV]) {
+        if (active && t < t1) {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const uint32_t gi = kk[k] & ~kHead;
+                if constexpr (KIND == 0) {
+                    xv[k][0] = xg_[gi];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < V; e++) xv[k][e] = xg_[gi + sub * V + e];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; k++)
+#pragma unroll
+                for (int e = 0; e < XV; e++) xv[k][e] = T(0);
+        }
+    };
+    // Stage 3: segmented reduction of a tile.
+    auto compute = [&](const uint32_t (&kk)[K], const T (&v)[K][V], const T (&xv)[K][XV]) {
         // HEADs per slot and their exclusive prefix over the slots
         int nh = 0;
 #pragma unroll
@@ -210,7 +239,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
             }
 #pragma unroll
             for (int e = 0; e < V; e++) {
-                const T p = v[k][e] * xv[k][e];
+                const T p = v[k][e] * xv[k][KIND == 0 ? 0 : e];
                 if (seen) cur[e] += p;
                 else lead[e] += p;
             }
@@ -248,12 +277,12 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         // the segment open when entering a slot closes at the slot's first HEAD
         if (active && seen) {
             const int cseg = seg_base + pre - 1;
-            const bool from_tile = ef || owned;  // opened inside this range
-            if (from_tile || !starts_at_head) {
+            const bool from_range = ef || owned;  // its HEAD lies in this range
+            if (from_range || !starts_at_head) {
                 T tot[V];
 #pragma unroll
                 for (int e = 0; e < V; e++) tot[e] = (ef ? es[e] : carry[e] + es[e]) + lead[e];
-                if (from_tile)
+                if (from_range)
                     emit<T, KIND, V>(b, cseg, tot, sub, LPR, lane, y, alpha, beta, rd);
                 else
                     hand_off<T, KIND, V>(b, r, cseg, tot, sub, LPR, lane, w);
@@ -269,6 +298,45 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         }
         owned = owned || lf;
         seg_base += tile_heads;
+    };
+
+    if constexpr (P == 2) {
+        // Two stages, ping-pong buffers: gathers of tile t are issued before the stream loads of
+        // tile t+1, so the counted vmcnt wait in compute(t) never waits on the prefetch.
+        uint32_t kA[K], kB[K];
+        T vA[K][V], vB[K][V], xv[K][XV];
+        load_stream(t0, kA, vA);
+        for (int t = t0; t < t1; t += 2) {
+            gather(t, kA, xv);
+            load_stream(t + 1, kB, vB);
+            compute(kA, vA, xv);
+            if (t + 1 >= t1) break;
+            gather(t + 1, kB, xv);
+            load_stream(t + 2, kA, vA);
+            compute(kB, vB, xv);
+        }
+    } else {
+        // Three stages, rotating buffers: in step t the stream loads of tile t+2 and the gathers of
+        // tile t+1 are in flight while tile t is reduced.
+        uint32_t k0[K], k1[K], k2[K];
+        T v0[K][V], v1[K][V], v2[K][V];
+        T x0[K][XV], x1[K][XV], x2[K][XV];
+        load_stream(t0, k0, v0);
+        gather(t0, k0, x0);
+        load_stream(t0 + 1, k1, v1);
+        for (int t = t0; t < t1; t += 3) {
+            gather(t + 1, k1, x1);
+            load_stream(t + 2, k2, v2);
+            compute(k0, v0, x0);
+            if (t + 1 >= t1) break;
+            gather(t + 2, k2, x2);
+            load_stream(t + 3, k0, v0);
+            compute(k1, v1, x1);
+            if (t + 2 >= t1) break;
+            gather(t + 3, k0, x0);
+            load_stream(t + 4, k1, v1);
+            compute(k2, v2, x2);
+        }
     }
     // the segment still open at the end of the range
     if (active && slot == 0) {
@@ -281,18 +349,18 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
 }
 
 #define VBC_W_CASES(KIND)                                                                          \
-    case 0: run_range<T, KIND, 0>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 1: run_range<T, KIND, 1>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 2: run_range<T, KIND, 2>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 3: run_range<T, KIND, 3>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 4: run_range<T, KIND, 4>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 5: run_range<T, KIND, 5>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 6: run_range<T, KIND, 6>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 7: run_range<T, KIND, 7>(b, r, lane, x, y, alpha, beta, rd); break;                        \
-    case 8: run_range<T, KIND, 8>(b, r, lane, x, y, alpha, beta, rd); break;
+    case 0: run_range<T, KIND, 0, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 1: run_range<T, KIND, 1, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 2: run_range<T, KIND, 2, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 3: run_range<T, KIND, 3, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 4: run_range<T, KIND, 4, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 5: run_range<T, KIND, 5, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 6: run_range<T, KIND, 6, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 7: run_range<T, KIND, 7, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 8: run_range<T, KIND, 8, K, P>(b, r, lane, x, y, alpha, beta, rd); break;
 
 // One wave per range; the wave finds its bucket by a scalar scan of the (few) bins.
-template <typename T, int KIND>
+template <typename T, int KIND, int K, int P>
 __global__ __launch_bounds__(kBlockThreads) void spmv_ranges(const Bin *__restrict__ bins, int nbins,
                                                              int total_ranges, const T *__restrict__ x,
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
@@ -304,7 +372,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_ranges(const Bin *__restri
     const Bin b = bins[bi];
     const int r = rg - b.range0;
     const int lane = threadIdx.x & 63;
-    if (lane == 0) b.carry_seg[r] = -1;  // overwritten below when the range continues a segment
+    if (lane == 0) G(b.carry_seg)[r] = -1;  // overwritten below when the range continues a segment
     const bool rd = rd_i != 0;
     switch (b.wkey) { VBC_W_CASES(KIND) default: break; }
 }
@@ -325,7 +393,7 @@ __global__ __launch_bounds__(kBlockThreads) void fixup(const Bin *__restrict__ b
         const int seg = b.carry_seg[r];
         if (seg < 0 || (r > 0 && b.carry_seg[r - 1] == seg)) return;
         const int wc = KIND == 0 ? b.w : 1;
-        T *__restrict__ yo = y + b.out[seg];
+        T *__restrict__ yo = y + out_of(b, seg);
         for (int c = 0; c < wc; c++) {
             T s = T(0);
             for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++)

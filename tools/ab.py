@@ -1,0 +1,92 @@
+"""Interleaved in-process A/B timing of libvbc layout variants (env knobs read at handle creation).
+
+    python tools/ab.py --workload fe --variants "VBC_TILE_K=4;VBC_TILE_K=8" [--rounds 5 --reps 20]
+Each variant is a separate handle over the same matrix and vectors; rounds interleave the variants
+(MI355X guide §5.4 rule 24) and the median / min per-launch time is reported with the GB/s figure
+of bench.py's byte formula.  Also checks every variant's y against the first (bitwise/relative).
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="fe")
+    ap.add_argument("--variants", default="VBC_TILE_K=4;VBC_TILE_K=8")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--trans", type=int, default=1)
+    ap.add_argument("--scale", type=float, default=1.0)
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    import sparsematrixvbcs_amd as V
+    from sparsematrixvbcs_amd import _lib as L
+
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    if args.workload == "fe":
+        B = V.synthetic.fe_grid_2d(int(round(2236 * args.scale ** 0.5)), dof=2, dtype=dtype)
+    else:
+        B = V.synthetic.north_star(dtype=dtype, scale=args.scale, mixed=(args.workload == "ns-mixed"))
+    esz = np.dtype(dtype).itemsize
+    nbytes = bench.algorithmic_bytes(B, esz)
+    trans = bool(args.trans)
+    nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+    x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, nx).astype(dtype)).cuda()
+    variants = [v for v in args.variants.split(";")]
+    handles = []
+    for v in variants:
+        saved = dict(os.environ)
+        for kv in v.split(","):
+            if "=" in kv:
+                k, val = kv.split("=", 1)
+                os.environ[k.strip()] = val.strip()
+        hp = C.c_void_p()
+        L.check(B._create(C.byref(hp), 0, L.VBC_CREATE_TRANSPOSED if trans else L.VBC_CREATE_FORWARD), "create")
+        os.environ.clear()
+        os.environ.update(saved)
+        handles.append(hp)
+    ys = [torch.empty(ny, dtype=x.dtype, device="cuda") for _ in variants]
+    stream = torch.cuda.current_stream()
+    lib = L.lib()
+
+    def run(i):
+        L.check(lib.vbc_mul(handles[i], int(trans), x.data_ptr(), nx, ys[i].data_ptr(), ny, 1.0, 0.0,
+                            L.VBC_MEM_DEVICE, stream.cuda_stream, 0), "mul")
+
+    for i in range(len(variants)):
+        for _ in range(3):
+            run(i)
+    torch.cuda.synchronize()
+    times = {i: [] for i in range(len(variants))}
+    for _ in range(args.rounds):
+        for i in range(len(variants)):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
+            for a, b in ev:
+                a.record(stream)
+                run(i)
+                b.record(stream)
+            torch.cuda.synchronize()
+            times[i] += [a.elapsed_time(b) for a, b in ev]
+    ref = ys[0].double()
+    for i, v in enumerate(variants):
+        t = np.array(times[i])
+        d = (ys[i].double() - ref).norm().item() / max(ref.norm().item(), 1e-300)
+        print(f"{v:40s} median {np.median(t)*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
+              f"{nbytes / (np.median(t) * 1e-3) / 1e9:7.0f} GB/s  rel-diff-vs-first {d:.2e}", flush=True)
+    for hp in handles:
+        lib.vbc_destroy(hp)
+
+
+if __name__ == "__main__":
+    main()

@@ -23,7 +23,8 @@ KERNEL = "spmv_ranges"
 def run_pass(counters, outdir, bench_args):
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", str(outdir),
            "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), *bench_args]
-    subprocess.run(cmd, check=True, cwd=ROOT)
+    print("pass:", " ".join(counters), flush=True)
+    subprocess.run(cmd, check=True, cwd=ROOT, timeout=180)
     files = glob.glob(str(outdir / "**" / "*counter_collection.csv"), recursive=True)
     vals = {}
     for f in files:
@@ -50,7 +51,13 @@ def main():
     res = {}
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"]] + [g.split(",") for g in args.counters.split(";") if g]
     for i, counters in enumerate(passes):
-        vals = run_pass(counters, out / f"pass{i}", bench_args)
+        try:
+            vals = run_pass(counters, out / f"pass{i}", bench_args)
+        except subprocess.SubprocessError as e:  # a counter set the profiler cannot serve
+            print("pass failed:", counters, e, flush=True)
+            if i < 2:
+                raise
+            continue
         for k, v in vals.items():
             res[k] = dict(mean=sum(v) / len(v), n=len(v), min=min(v), max=max(v))
     fetch_kb = res["FETCH_SIZE"]["mean"]
