@@ -1,13 +1,16 @@
 """Benchmark: 1DVBC SpMV effective GB/s (and GFLOP/s) vs the MI355X HBM roofline (BASELINE.json).
 
 A step is one mul!(y, B', x) -- the transposed 1D-VBR product the reference's paper and benchmark
-time (bin/test_table.jl:80) -- over the NS-1DVBC workload of SURVEY.md §8d: a synthetic
-10^7 x 10^7 matrix with 1e8 nonzeros in 2.5e6 width-4 stripes (costs.jl:63-83 generator), fp64,
-inputs resident in HBM.  N ranks = N GPUs, one process each (torchrun); every rank owns its own
-block-row shard of that size (weak scaling, no data-path collective: the transposed product writes
-disjoint y ranges).  rank 0 prints one JSON line.
+time (bin/test_table.jl:80) -- fp64, inputs resident in HBM.  Primary workload (BASELINE.json
+target: "10M x 10M, ~1e8-nnz SuiteSparse-like matrix"): `fe`, a 2D finite-element operator
+(5-point stencil, 2 unknowns per node, 1.0e7 x 1.0e7, 1.0e8 stored values) in 1DVBC form.
+Secondary (reported in the same line at N=1): `ns`, SURVEY.md §8d's NS-1DVBC, the reference's own
+uniform-random VBR generator (costs.jl:63-83) at 1e7 x 1e7, 1e8 nonzeros, width-4 stripes.
+N ranks = N GPUs, one process each (torchrun); every rank owns its own block-row shard of that size
+(weak scaling, no data-path collective: the transposed product writes disjoint y ranges).
+rank 0 prints one JSON line.
 
-    python bench.py [--gpus N --steps K --warmup W --workload ns|ns-mixed --dtype f64|f32]
+    python bench.py [--gpus N --steps K --warmup W --workload fe|ns|ns-mixed --dtype f64|f32]
 """
 import argparse
 import json
@@ -69,16 +72,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="ns", choices=["ns", "ns-mixed", "fe"])
+    ap.add_argument("--workload", default="fe", choices=["fe", "ns", "ns-mixed"])
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary (uniform) workload")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-
-    import sparsematrixvbcs_amd as V
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -91,13 +93,42 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     dtype = np.float64 if args.dtype == "f64" else np.float32
+    out = measure(args, args.workload, dtype, world, rank, local, device, with_cpu=not args.no_cpu_baseline)
+    if world == 1 and not args.no_secondary:
+        sec = "ns" if args.workload != "ns" else "fe"
+        s = measure(args, sec, dtype, world, rank, local, device, with_cpu=False)
+        out["secondary"] = {k: s[k] for k in ("value", "unit", "ms_per_step", "gflops")}
+        out["secondary"]["workload"] = s["config"]["workload"]
+        out["secondary"]["roofline_frac"] = s["roofline"]["frac"]
+        out["secondary"]["note"] = ("uniform-random rows (costs.jl:63-83 generator): every x gather misses L2; "
+                                    "bound by random-access throughput, see DESIGN.md §6")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
+             "ns-mixed": "NS-1DVBC-mixed-w1..8-1e8nnz-uniform",
+             "fe": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2 (SuiteSparse-like mesh operator)"}
+
+
+def build_matrix(workload, dtype, scale, seed):
+    import sparsematrixvbcs_amd as V
+    if workload == "fe":
+        return V.synthetic.fe_grid_2d(int(round(2236 * scale ** 0.5)), dof=2, dtype=dtype, seed=seed)
+    return V.synthetic.north_star(dtype=dtype, scale=scale, seed=seed, mixed=(workload == "ns-mixed"))
+
+
+def measure(args, workload, dtype, world, rank, local, device, with_cpu):
+    import torch
+    import torch.distributed as dist
+
+    import sparsematrixvbcs_amd as V
+
     esz = np.dtype(dtype).itemsize
-    # each rank: its own block-row shard (different stripes), the same replicated x
-    if args.workload == "fe":
-        B = V.synthetic.fe_grid_2d(int(round(2236 * args.scale ** 0.5)), dof=2, dtype=dtype, seed=0xDEADBEEF + rank)
-    else:
-        B = V.synthetic.north_star(dtype=dtype, scale=args.scale, seed=0xDEADBEEF + rank,
-                                   mixed=(args.workload == "ns-mixed"))
+    # each rank: its own block-row shard (different stripes' values), the same replicated x
+    B = build_matrix(workload, dtype, args.scale, 0xDEADBEEF + rank)
     rng = np.random.default_rng(0xC0FFEE)
     x_host = rng.uniform(-1, 1, B.m).astype(dtype)
     x = torch.from_numpy(x_host).to(device)
@@ -142,11 +173,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_bytes * args.steps / elapsed / 1e9
     achieved = bytes_rank / (kernel_ms * 1e-3) / 1e9
-    workload = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform", "ns-mixed": "NS-1DVBC-mixed-w1..8-1e8nnz-uniform",
-                "fe": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2"}[args.workload]
-    if args.scale != 1.0:
-        workload += f"-scale{args.scale}"
-    traffic, traffic_src = load_traffic(args.workload, args.dtype)
+    wname = WORKLOADS[workload] + (f"-scale{args.scale}" if args.scale != 1.0 else "")
+    traffic, traffic_src = load_traffic(workload, args.dtype)
     out = {
         "metric": "1DVBC SpMV effective GB/s (and GFLOP/s) vs HBM roofline, 1/2/4/8 GPU",
         "value": round(value, 2),
@@ -159,9 +187,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (costs.jl:63-83 VBR generator, seed 0xDEADBEEF+rank; x ~ U[-1,1), seed 0xC0FFEE)",
+        "data": "synthetic (seed 0xDEADBEEF+rank; x ~ U[-1,1), seed 0xC0FFEE); no SuiteSparse files offline",
         "config": {
-            "workload": workload,
+            "workload": wname,
             "op": "mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)",
             "m": B.m, "n_per_rank": B.n, "stripes_per_rank": len(B.Phi), "row_blocks_per_rank": int(B.pos[-1] - 1),
             "nnz_per_rank": nnz, "W": B.W, "index_bytes": 4,
@@ -175,19 +203,19 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "vbc::spmv_ranges<T, 0>",
+            "kernel": "vbc::spmv_ranges<T, 0, K, P> (+ vbc::fixup)",
             "bytes_per_launch": bytes_rank,
             "avg_launch_ms": round(kernel_ms, 5),
             "traffic_source": traffic_src,
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if with_cpu and rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(B, x_host, esz)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    B.release()
+    del x, y
+    torch.cuda.empty_cache()
+    return out
 
 
 if __name__ == "__main__":

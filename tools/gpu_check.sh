@@ -20,5 +20,5 @@ STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *slow* ]] && step slow 900 python -m pytest tests -m "slow" -x -q
 [[ $STEPS == *bench* ]] && step bench 600 python bench.py --steps 50 --warmup 5
 [[ $STEPS == *fe* ]] && step bench_fe 600 python bench.py --steps 50 --warmup 5 --workload fe --no-cpu-baseline
-[[ $STEPS == *prof* ]] && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline
+[[ $STEPS == *prof* ]] && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary
 echo "== done $(date +%T)"

@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--counters", default="", help="extra counter passes, ';'-separated groups")
     args = ap.parse_args()
     out = ROOT / "gpurun_out" / "pmc"
-    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--workload", args.workload,
+    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--workload", args.workload,
                   "--dtype", args.dtype] + args.extra.split()
     res = {}
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"]] + [g.split(",") for g in args.counters.split(";") if g]
