@@ -5,7 +5,7 @@ SparseMatrix1DVBC / SparseMatrixVBC / mul! / TrSpMV! / Base.:*, over libvbc's C 
 (include/vbc.h), whose hand-written gfx950 kernels do every product.  Import it as
 `sparsematrixvbcs_amd` (the repo-root loader) since the directory name is not an identifier.
 """
-from . import _lib, synthetic
+from . import _lib, distributed, synthetic
 from ._lib import ArgumentError, DimensionMismatch, HIPError, UnsupportedDtype
 from .matrices import (DEFAULT_SIMD_SIZE, Adjoint, SparseMatrix1DVBC, SparseMatrixCSC, SparseMatrixVBC,
                        Transpose, adjoint, transpose)
