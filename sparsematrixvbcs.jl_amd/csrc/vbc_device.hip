@@ -8,6 +8,7 @@
 #include <cmath>
 #include <map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "vbc_internal.h"
@@ -83,9 +84,10 @@ struct vbc_handle {
     std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
     bool f_scale = false;         // forward with several buckets: scale y by beta first
     int64_t bytes_t = 0, bytes_f = 0;
-    int target_ranges = 4096;     // waves resident on the device (one range each)
+    int target_ranges_k[2] = {4096, 4096};  // resident waves of the B'x / Bx kernels (one range each)
     int tile_k = vbc::kTileKDefault;  // entries per slot per tile
     int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
+    int diag = 0;                     // ablation variant (VBC_DIAG; tools/ab.py only)
 };
 
 namespace vbc {
@@ -139,7 +141,7 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     if (ntiles >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
     if ((int64_t)out.size() >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "too many segments");
     // ranges: one wave each, about target_ranges over the whole launch, >= 2 tiles per range
-    int64_t nr = (int64_t)std::llround((double)h->target_ranges * (double)R / (double)std::max<int64_t>(total_entries, 1));
+    int64_t nr = (int64_t)std::llround((double)h->target_ranges_k[kind] * (double)R / (double)std::max<int64_t>(total_entries, 1));
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, (ntiles + 1) / 2));
     const int64_t tpr = ntiles > 0 ? (ntiles + nr - 1) / nr : 1;
     nr = ntiles > 0 ? (ntiles + tpr - 1) / tpr : 0;
@@ -154,6 +156,7 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     pb.b.ntiles = (int32_t)ntiles;
     pb.b.tile_k = K;
     pb.b.pipe = h->pipe;
+    pb.b.diag = h->diag;
     pb.b.out_affine = 1;
     pb.b.out_base = out.empty() ? 0 : out[0];
     pb.b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -339,18 +342,29 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (!g.ok) { release(h); return fail(VBC_HIP_ERROR, "hipSetDevice failed"); }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipGetDeviceProperties failed"); }
-    int occ = 0;
-    if (dtype == VBC_F64)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<double, 0, kTileKDefault, kPipeDefault>, kBlockThreads, 0);
-    else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_ranges<float, 0, kTileKDefault, kPipeDefault>, kBlockThreads, 0);
-    h->target_ranges = prop.multiProcessorCount * std::max(1, std::min(occ, 8)) * kWavesPerBlock;
-    if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges = std::max(1, atoi(e));
+    h->tile_k = dtype == VBC_F64 ? 4 : 8;  // measured best (tools/ab.py, FE workload)
     if (const char *e = getenv("VBC_TILE_K")) {
         const int k = atoi(e);
-        h->tile_k = (k == 4 || k == 8) ? k : kTileKDefault;
+        h->tile_k = (k == 4 || k == 8) ? k : h->tile_k;
     }
-    if (const char *e = getenv("VBC_PIPE")) h->pipe = atoi(e) == 2 ? 2 : 3;
+    if (const char *e = getenv("VBC_PIPE")) h->pipe = atoi(e) == 3 ? 3 : 2;
+    if (const char *e = getenv("VBC_DIAG")) h->diag = atoi(e);
+    // one range per resident wave: occupancy of the kernel variant this handle will launch
+    int occ[2] = {0, 0};
+#define VBC_OCC(TT, KK, PP)                                                                           \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], spmv_ranges<TT, 0, KK, PP>, kBlockThreads, 0); \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], spmv_ranges<TT, 1, KK, PP>, kBlockThreads, 0)
+    if (dtype == VBC_F64) {
+        if (h->tile_k == 4) { if (h->pipe == 2) { VBC_OCC(double, 4, 2); } else { VBC_OCC(double, 4, 3); } }
+        else { if (h->pipe == 2) { VBC_OCC(double, 8, 2); } else { VBC_OCC(double, 8, 3); } }
+    } else {
+        if (h->tile_k == 4) { if (h->pipe == 2) { VBC_OCC(float, 4, 2); } else { VBC_OCC(float, 4, 3); } }
+        else { if (h->pipe == 2) { VBC_OCC(float, 8, 2); } else { VBC_OCC(float, 8, 3); } }
+    }
+#undef VBC_OCC
+    for (int kd = 0; kd < 2; kd++)
+        h->target_ranges_k[kd] = prop.multiProcessorCount * std::max(1, std::min(occ[kd], 8)) * kWavesPerBlock;
+    if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
 
     Arena ar;
     std::vector<PendingBin> pt;
@@ -408,6 +422,19 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
     hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins, \
                        (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd)
         const int P = L.bins.empty() ? kPipeDefault : L.bins[0].pipe;
+        const int D = L.bins.empty() ? 0 : L.bins[0].diag;
+        if constexpr (std::is_same<T, double>::value) {
+            if (kind == 0 && K == 4 && P == 2 && D == 1) {
+                hipLaunchKernelGGL((spmv_ranges<T, 0, 4, 2, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                                   (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+                return VBC_OK;
+            }
+            if (kind == 0 && K == 4 && P == 2 && D == 2) {
+                hipLaunchKernelGGL((spmv_ranges<T, 0, 4, 2, 2>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                                   (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+                return VBC_OK;
+            }
+        }
         if (kind == 0) {
             if (P == 2) { if (K == 4) VBC_LAUNCH(0, 4, 2); else VBC_LAUNCH(0, 8, 2); }
             else { if (K == 4) VBC_LAUNCH(0, 4, 3); else VBC_LAUNCH(0, 8, 3); }

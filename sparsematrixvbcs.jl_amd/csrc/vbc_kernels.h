@@ -27,7 +27,7 @@ namespace vbc {
 
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlock = kBlockThreads / 64;
-constexpr int kTileKDefault = 4;  // entries per slot per tile (runtime choice: 4 or 8)
+constexpr int kTileKDefault = 8;  // entries per slot per tile (runtime choice: 4 or 8)
 constexpr int kPipeDefault = 2;   // software-pipeline depth (runtime choice: 2 or 3)
 constexpr uint32_t kHead = 0x80000000u;
 
@@ -52,6 +52,7 @@ struct Bin {
     int32_t ntiles;   // tiles of this bucket
     int32_t tile_k;   // entries per slot per tile (4 or 8)
     int32_t pipe;     // software-pipeline depth (2 or 3)
+    int32_t diag;     // ablation variant (0 = production)
     int32_t out_affine;  // 1: out[s] == out_base + s * out_stride (no table lookup)
     int32_t out_base;
     int32_t out_stride;
@@ -81,16 +82,63 @@ __device__ __forceinline__ void ld_stream(gptr<const T> p, T (&r)[V])
     }
 }
 
-// Kind 1 keeps per-lane column partials; the LPR lanes of a slot are summed when a segment is
-// written.  Called with the whole slot active (its lanes share every control decision).
+// DPP moves (VALU, no LDS traffic): CTRL = row_shr:n (0x110+n), row_bcast:15 (0x142),
+// row_bcast:31 (0x143), wave_shr:1 (0x138); lanes outside RM rows / the row receive 0.
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM, typename T>
+__device__ __forceinline__ T dppv(T v)
+{
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint64_t lo = dpp32<CTRL, RM>((uint32_t)u), hi = dpp32<CTRL, RM>((uint32_t)(u >> 32));
+        return __builtin_bit_cast(T, lo | (hi << 32));
+    } else {
+        return __builtin_bit_cast(T, dpp32<CTRL, RM>(__builtin_bit_cast(uint32_t, v)));
+    }
+}
+template <typename T>
+__device__ __forceinline__ T readlane(T v, int l)
+{
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+        const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+        return __builtin_bit_cast(T, lo | (hi << 32));
+    } else {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    }
+}
+// One step of the segmented inclusive scan (f = segment restarts here).
+template <int CTRL, int RM, typename T, int V>
+__device__ __forceinline__ void seg_step(bool cond, bool &f, T (&s)[V])
+{
+    const bool of = dpp32<CTRL, RM>((uint32_t)f) != 0;
+    T os[V];
+#pragma unroll
+    for (int e = 0; e < V; e++) os[e] = dppv<CTRL, RM>(s[e]);
+    if (cond) {
+        if (!f) {
+#pragma unroll
+            for (int e = 0; e < V; e++) s[e] += os[e];
+        }
+        f = f || of;
+    }
+}
+
+// Kind 1 keeps per-lane column partials; the LPR lanes of a slot (lane stride SS) are summed when a
+// segment is written.  Called with the whole slot active (its lanes share every control decision).
 template <typename T, int V>
-__device__ __forceinline__ T slot_sum(const T (&v)[V], int lane, int sub, int LPR)
+__device__ __forceinline__ T slot_sum(const T (&v)[V], int lane, int sub, int LPR, int SS)
 {
     T s = T(0);
 #pragma unroll
     for (int e = 0; e < V; e++) s += v[e];
     for (int d = 1; d < LPR; d <<= 1) {
-        const T t = __shfl(s, (lane + d) & 63, 64);
+        const T t = __shfl(s, (lane + d * SS) & 63, 64);
         if (sub + d < LPR) s += t;
     }
     return s;
@@ -103,7 +151,7 @@ __device__ __forceinline__ int out_of(const Bin &b, int seg)
 }
 
 template <typename T, int KIND, int V>
-__device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int sub, int LPR, int lane,
+__device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int sub, int LPR, int SS, int lane,
                                      T *__restrict__ y, T alpha, T beta, bool rd)
 {
     if constexpr (KIND == 0) {
@@ -115,7 +163,7 @@ __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int
             yo[e] = r;
         }
     } else {
-        const T s = slot_sum<T, V>(v, lane, sub, LPR);
+        const T s = slot_sum<T, V>(v, lane, sub, LPR, SS);
         if (sub == 0) {
             gptr<T> yo = G(y) + out_of(b, seg);
             T r = alpha * s;
@@ -128,20 +176,22 @@ __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int
 // Hand a continued segment's partial to the fix-up pass.
 template <typename T, int KIND, int V>
 __device__ __forceinline__ void hand_off(const Bin &b, int r, int seg, const T (&v)[V], int sub, int LPR,
-                                         int lane, int w)
+                                         int SS, int lane, int w)
 {
     if constexpr (KIND == 0) {
         gptr<T> c = G(static_cast<T *>(b.carry)) + (size_t)r * w + sub * V;
 #pragma unroll
         for (int e = 0; e < V; e++) c[e] = v[e];
     } else {
-        const T s = slot_sum<T, V>(v, lane, sub, LPR);
+        const T s = slot_sum<T, V>(v, lane, sub, LPR, SS);
         if (sub == 0) G(static_cast<T *>(b.carry))[r] = s;
     }
     if (sub == 0) G(b.carry_seg)[r] = seg;
 }
 
-template <typename T, int KIND, int W_, int K, int P>
+// DIAG (ablation builds only; never selected by default): 1 = loads and gathers but no segmented
+// reduction (a plain fold keeps the loads live), 2 = no x gathers (x taken as 1).
+template <typename T, int KIND, int W_, int K, int P, int DIAG = 0>
 __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T *__restrict__ x,
                                           T *__restrict__ y, T alpha, T beta, bool rd)
 {
@@ -150,9 +200,15 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     const int w = kGeneric ? b.w : W_;
     const int LPR = w / V;
     const int RPI = b.rpi;
-    const int slot = lane / LPR;
-    const int sub = lane - slot * LPR;
-    const bool active = slot < RPI;
+    // DPP path: compile-time power-of-two slot count filling the wave; lanes are sub-major
+    // (lane = sub * RPI + slot) so each column's slots are contiguous lanes for row_shr/row_bcast.
+    constexpr int cLPR = kGeneric ? 0 : W_ / V;
+    constexpr int cRPI = kGeneric ? 0 : 64 / cLPR;
+    constexpr bool kDpp = !kGeneric && (cRPI & (cRPI - 1)) == 0 && cRPI * cLPR == 64 && cRPI >= 8;
+    const int slot = kDpp ? (lane & (cRPI - 1)) : lane / LPR;
+    const int sub = kDpp ? (lane / cRPI) : lane - slot * LPR;
+    const int SS = kDpp ? cRPI : 1;  // lane stride between the columns of one slot
+    const bool active = slot < RPI && sub < LPR;
     const int t0 = r * b.tiles_per_range;
     const int t1 = min(t0 + b.tiles_per_range, b.ntiles);
     if (t0 >= t1) return;
@@ -189,7 +245,12 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     // Stage 2: the x gathers of a tile whose keys have arrived (kind 0: one x per entry).
     constexpr int XV = KIND == 0 ? 1 : V;
     auto gather = [&](int t, const uint32_t (&kk)[K], T (&xv)[K][XV]) {
-        if (active && t < t1) {
+        if constexpr (DIAG == 2) {
+#pragma unroll
+            for (int k = 0; k < K; k++)
+#pragma unroll
+                for (int e = 0; e < XV; e++) xv[k][e] = T(1);
+        } else if (active && t < t1) {
 #pragma unroll
             for (int k = 0; k < K; k++) {
                 const uint32_t gi = kk[k] & ~kHead;
@@ -207,21 +268,42 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
                 for (int e = 0; e < XV; e++) xv[k][e] = T(0);
         }
     };
+    T diag_acc = T(0);
     // Stage 3: segmented reduction of a tile.
     auto compute = [&](const uint32_t (&kk)[K], const T (&v)[K][V], const T (&xv)[K][XV]) {
-        // HEADs per slot and their exclusive prefix over the slots
-        int nh = 0;
+        if constexpr (DIAG == 1) {
 #pragma unroll
-        for (int k = 0; k < K; k++) nh += (int)(kk[k] >> 31);
-        int pre = nh;
-        for (int d = 1; d < RPI; d <<= 1) {
-            const int o = __shfl(pre, (lane - d * LPR) & 63, 64);
-            if (slot >= d) pre += o;
+            for (int k = 0; k < K; k++)
+#pragma unroll
+                for (int e = 0; e < V; e++) diag_acc += v[k][e] * xv[k][KIND == 0 ? 0 : e] + (T)(kk[k] & 1);
+            return;
         }
-        const int tile_heads = __shfl(pre, (RPI - 1) * LPR, 64);
-        pre -= nh;
+        // HEADs per slot and their exclusive prefix over the slots
+        int pre = 0, tile_heads = 0;
+        if constexpr (kDpp) {  // ballots: every column's copy of the slot flags is identical
+            const uint64_t colmask = cRPI == 64 ? ~0ull : ((1ull << cRPI) - 1) << (sub * cRPI);
+            const uint64_t below = colmask & ((1ull << lane) - 1);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const uint64_t bal = __ballot((kk[k] >> 31) != 0);
+                pre += __popcll(bal & below);
+                tile_heads += __popcll(bal & (cRPI == 64 ? ~0ull : (1ull << cRPI) - 1));
+            }
+        } else {
+            int nh = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++) nh += (int)(kk[k] >> 31);
+            pre = nh;
+            for (int d = 1; d < RPI; d <<= 1) {
+                const int o = __shfl(pre, (lane - d * LPR) & 63, 64);
+                if (slot >= d) pre += o;
+            }
+            tile_heads = __shfl(pre, (RPI - 1) * LPR, 64);
+            pre -= nh;
+        }
 
-        // lane-serial pass over the slot's K entries
+        // lane-serial pass over the slot's K entries: one FMA per column into `cur`; at a HEAD the
+        // running sum becomes the slot's lead (first HEAD) or a complete segment (later HEADs).
         T lead[V], cur[V];
 #pragma unroll
         for (int e = 0; e < V; e++) lead[e] = cur[e] = T(0);
@@ -231,17 +313,24 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         for (int k = 0; k < K; k++) {
             if (kk[k] & kHead) {
                 if (seen)  // opened and closed inside this slot: owned and complete
-                    emit<T, KIND, V>(b, seg, cur, sub, LPR, lane, y, alpha, beta, rd);
+                    emit<T, KIND, V>(b, seg, cur, sub, LPR, SS, lane, y, alpha, beta, rd);
+                else {
+#pragma unroll
+                    for (int e = 0; e < V; e++) lead[e] = cur[e];
+                }
                 seg++;
                 seen = true;
 #pragma unroll
                 for (int e = 0; e < V; e++) cur[e] = T(0);
             }
 #pragma unroll
+            for (int e = 0; e < V; e++) cur[e] = __builtin_fma(v[k][e], xv[k][KIND == 0 ? 0 : e], cur[e]);
+        }
+        if (!seen) {
+#pragma unroll
             for (int e = 0; e < V; e++) {
-                const T p = v[k][e] * xv[k][KIND == 0 ? 0 : e];
-                if (seen) cur[e] += p;
-                else lead[e] += p;
+                lead[e] = cur[e];
+                cur[e] = T(0);
             }
         }
         // segmented inclusive scan of (seen, seen ? cur : lead) over the slots
@@ -249,26 +338,40 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         T s[V];
 #pragma unroll
         for (int e = 0; e < V; e++) s[e] = seen ? cur[e] : lead[e];
-        for (int d = 1; d < RPI; d <<= 1) {
-            const int src = (lane - d * LPR) & 63;
-            const bool of = __shfl((int)f, src, 64) != 0;
-            T os[V];
-#pragma unroll
-            for (int e = 0; e < V; e++) os[e] = __shfl(s[e], src, 64);
-            if (slot >= d) {
-                if (!f) {
-#pragma unroll
-                    for (int e = 0; e < V; e++) s[e] += os[e];
-                }
-                f = f || of;
-            }
-        }
-        // value entering each slot (exclusive scan)
-        const int srcx = (lane - LPR) & 63;
-        bool ef = __shfl((int)f, srcx, 64) != 0;
+        bool ef;
         T es[V];
+        if constexpr (kDpp) {
+            const int ls = lane & (cRPI < 16 ? cRPI - 1 : 15);  // slot position inside a DPP row
+            if constexpr (cRPI > 1) seg_step<0x111, 0xF>(ls >= 1, f, s);
+            if constexpr (cRPI > 2) seg_step<0x112, 0xF>(ls >= 2, f, s);
+            if constexpr (cRPI > 4) seg_step<0x114, 0xF>(ls >= 4, f, s);
+            if constexpr (cRPI > 8) seg_step<0x118, 0xF>(ls >= 8, f, s);
+            if constexpr (cRPI > 16) seg_step<0x142, 0xA>((lane & 16) != 0, f, s);
+            if constexpr (cRPI > 32) seg_step<0x143, 0xC>((lane & 32) != 0, f, s);
+            ef = dpp32<0x138, 0xF>((uint32_t)f) != 0;  // wave_shr:1
 #pragma unroll
-        for (int e = 0; e < V; e++) es[e] = __shfl(s[e], srcx, 64);
+            for (int e = 0; e < V; e++) es[e] = dppv<0x138, 0xF>(s[e]);
+        } else {
+            for (int d = 1; d < RPI; d <<= 1) {
+                const int src = (lane - d * LPR) & 63;
+                const bool of = __shfl((int)f, src, 64) != 0;
+                T os[V];
+#pragma unroll
+                for (int e = 0; e < V; e++) os[e] = __shfl(s[e], src, 64);
+                if (slot >= d) {
+                    if (!f) {
+#pragma unroll
+                        for (int e = 0; e < V; e++) s[e] += os[e];
+                    }
+                    f = f || of;
+                }
+            }
+            // value entering each slot (exclusive scan)
+            const int srcx = (lane - LPR) & 63;
+            ef = __shfl((int)f, srcx, 64) != 0;
+#pragma unroll
+            for (int e = 0; e < V; e++) es[e] = __shfl(s[e], srcx, 64);
+        }
         if (slot == 0) {
             ef = false;
 #pragma unroll
@@ -283,19 +386,33 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
 #pragma unroll
                 for (int e = 0; e < V; e++) tot[e] = (ef ? es[e] : carry[e] + es[e]) + lead[e];
                 if (from_range)
-                    emit<T, KIND, V>(b, cseg, tot, sub, LPR, lane, y, alpha, beta, rd);
+                    emit<T, KIND, V>(b, cseg, tot, sub, LPR, SS, lane, y, alpha, beta, rd);
                 else
-                    hand_off<T, KIND, V>(b, r, cseg, tot, sub, LPR, lane, w);
+                    hand_off<T, KIND, V>(b, r, cseg, tot, sub, LPR, SS, lane, w);
             }
         }
         // flow into the next tile
-        const int last = (RPI - 1) * LPR + sub;
-        const bool lf = __shfl((int)f, last, 64) != 0;
+        bool lf;
+        T lsv[V];
+        if constexpr (kDpp) {  // last slot of each column: scalar reads
+            lf = __builtin_amdgcn_readlane((int)f, cRPI - 1) != 0;
 #pragma unroll
-        for (int e = 0; e < V; e++) {
-            const T ls = __shfl(s[e], last, 64);
-            carry[e] = lf ? ls : carry[e] + ls;
+            for (int e = 0; e < V; e++) {
+                lsv[e] = readlane(s[e], cRPI - 1);
+#pragma unroll
+                for (int j = 1; j < cLPR; j++) {
+                    const T o = readlane(s[e], j * cRPI + cRPI - 1);
+                    if (sub == j) lsv[e] = o;
+                }
+            }
+        } else {
+            const int last = (RPI - 1) * LPR + sub;
+            lf = __shfl((int)f, last, 64) != 0;
+#pragma unroll
+            for (int e = 0; e < V; e++) lsv[e] = __shfl(s[e], last, 64);
         }
+#pragma unroll
+        for (int e = 0; e < V; e++) carry[e] = lf ? lsv[e] : carry[e] + lsv[e];
         owned = owned || lf;
         seg_base += tile_heads;
     };
@@ -338,29 +455,33 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
             compute(k2, v2, x2);
         }
     }
+    if constexpr (DIAG == 1) {
+        if (diag_acc == T(1234.5)) y[lane] = diag_acc;  // keep the loads live
+        return;
+    }
     // the segment still open at the end of the range
     if (active && slot == 0) {
         const int cseg = seg_base - 1;
         if (owned)
-            emit<T, KIND, V>(b, cseg, carry, sub, LPR, lane, y, alpha, beta, rd);
+            emit<T, KIND, V>(b, cseg, carry, sub, LPR, SS, lane, y, alpha, beta, rd);
         else if (!starts_at_head)  // no HEAD in the whole range: all of it continues cseg
-            hand_off<T, KIND, V>(b, r, cseg, carry, sub, LPR, lane, w);
+            hand_off<T, KIND, V>(b, r, cseg, carry, sub, LPR, SS, lane, w);
     }
 }
 
 #define VBC_W_CASES(KIND)                                                                          \
-    case 0: run_range<T, KIND, 0, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 1: run_range<T, KIND, 1, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 2: run_range<T, KIND, 2, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 3: run_range<T, KIND, 3, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 4: run_range<T, KIND, 4, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 5: run_range<T, KIND, 5, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 6: run_range<T, KIND, 6, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 7: run_range<T, KIND, 7, K, P>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 8: run_range<T, KIND, 8, K, P>(b, r, lane, x, y, alpha, beta, rd); break;
+    case 0: run_range<T, KIND, 0, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 1: run_range<T, KIND, 1, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 2: run_range<T, KIND, 2, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 3: run_range<T, KIND, 3, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 4: run_range<T, KIND, 4, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 5: run_range<T, KIND, 5, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 6: run_range<T, KIND, 6, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 7: run_range<T, KIND, 7, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 8: run_range<T, KIND, 8, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;
 
 // One wave per range; the wave finds its bucket by a scalar scan of the (few) bins.
-template <typename T, int KIND, int K, int P>
+template <typename T, int KIND, int K, int P, int DIAG = 0>
 __global__ __launch_bounds__(kBlockThreads) void spmv_ranges(const Bin *__restrict__ bins, int nbins,
                                                              int total_ranges, const T *__restrict__ x,
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
