@@ -45,6 +45,10 @@ typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
 #define VBC_CREATE_FORWARD 0x2u    /* build the layout for mul!(y, B, x)                         */
 
 /* mul flags */
+#define VBC_MAT_ROWMAJOR 0x2u         /* vbc_mul_mat: X, Y row-major (right-hand sides interleaved,
+                                         X[i*ldx + j], ld >= nrhs); the fused multi-RHS kernel
+                                         reads one contiguous X row per stored row.  Default:
+                                         column-major (Julia), one SpMV per column. */
 #define VBC_MUL_REFERENCE_QUIRKS 0x1u /* reproduce the reference bit-for-bit in alpha/beta:
                                          forward drops alpha (multiply_1DVBC.jl:48,
                                          multiply_VBC.jl:55-57); transposed overwrites y, ignoring
@@ -95,9 +99,10 @@ int vbc_destroy(vbc_handle *h);
 int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
             double beta, int mem, void *stream, unsigned flags);
 
-/* Multi-RHS Y = α·op(B)·X + β·Y with X, Y column-major (ldx, ldy >= rows).  The reference has no
- * matrix mul! (Base.:* forwards to an undefined method, multiply_1DVBC.jl:184-185), so its
- * semantics is defined column by column as vbc_mul. */
+/* Multi-RHS Y = α·op(B)·X + β·Y.  X is nx × nrhs, Y is ny × nrhs; column-major (ldx >= nx, ldy >=
+ * ny) by default, row-major with VBC_MAT_ROWMAJOR (ldx, ldy >= nrhs).  The reference has no matrix
+ * mul! (Base.:* forwards to an undefined method, multiply_1DVBC.jl:184-185), so the semantics is
+ * defined column by column as vbc_mul.  Fused kernel: transposed, row-major, widths <= 8. */
 int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t ldx, int64_t nx,
                 void *Y, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
                 unsigned flags);

@@ -18,6 +18,7 @@ VBC_F64, VBC_F32 = 0, 1
 VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
 VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD = 0x1, 0x2
 VBC_MUL_REFERENCE_QUIRKS = 0x1
+VBC_MAT_ROWMAJOR = 0x2
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (

@@ -84,6 +84,8 @@ struct vbc_handle {
     std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
     bool f_scale = false;         // forward with several buckets: scale y by beta first
     int64_t bytes_t = 0, bytes_f = 0;
+    void *d_carry_mm = nullptr;   // multi-RHS carry slots (allocated on first use)
+    size_t carry_mm_bytes = 0;
     int target_ranges_k[2] = {4096, 4096};  // resident waves of the B'x / Bx kernels (one range each)
     int tile_k = vbc::kTileKDefault;  // entries per slot per tile
     int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
@@ -299,6 +301,7 @@ static void release(vbc_handle *h)
     for (auto &l : h->lf)
         if (l.d_bins) (void)hipFree(l.d_bins);
     if (h->d_arena) (void)hipFree(h->d_arena);
+    if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
     delete h;
 }
 
@@ -488,6 +491,58 @@ static int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, 
 {
     return h->dtype == VBC_F64 ? mul_device<double>(h, trans, x, y, alpha, beta, stream)
                                : mul_device<float>(h, trans, x, y, alpha, beta, stream);
+}
+
+// Multi-RHS transposed product on the tiled stream (row-major X / Y), in chunks of <= 64 columns.
+template <typename T>
+static int mulmat_t_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy,
+                             double alpha, double beta, hipStream_t s)
+{
+    const Launch &L = h->lt;
+    const int NRmax = 64;
+    int64_t stride = 1;
+    for (const Bin &b : L.bins) stride = std::max<int64_t>(stride, (int64_t)b.nranges * b.w * NRmax);
+    const size_t need = (size_t)std::max<size_t>(L.bins.size(), 1) * stride * sizeof(T);
+    if (h->carry_mm_bytes < need) {
+        if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
+        h->d_carry_mm = nullptr;
+        h->carry_mm_bytes = 0;
+        VBC_HIP(hipMalloc(&h->d_carry_mm, need));
+        h->carry_mm_bytes = need;
+    }
+    T *cm = static_cast<T *>(h->d_carry_mm);
+    const bool rd = beta != 0.0;
+    for (int64_t c0 = 0; c0 < nrhs; c0 += NRmax) {
+        const int nr = (int)std::min<int64_t>(NRmax, nrhs - c0);
+        const T *xs = reinterpret_cast<const T *>(X) + c0;
+        T *ys = reinterpret_cast<T *>(Y) + c0;
+        const int NR = nr <= 16 ? 16 : 64;
+        const int64_t cs = nr <= 16 ? stride / 4 : stride;  // carry slots are sized per NR
+        if (L.total_ranges > 0) {
+            const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
+            const int K = L.bins[0].tile_k;
+#define VBC_MM(NRR, KK)                                                                                  \
+    hipLaunchKernelGGL((spmm_ranges<T, NRR, KK>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins,       \
+                       (int)L.bins.size(), L.total_ranges, xs, ldx, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd)
+            if (NR == 16) { if (K == 4) VBC_MM(16, 4); else VBC_MM(16, 8); }
+            else { if (K == 4) VBC_MM(64, 4); else VBC_MM(64, 8); }
+#undef VBC_MM
+            VBC_HIP(hipGetLastError());
+        }
+        const int nrng = L.total_ranges > 1 ? L.total_ranges : 0;
+        const int64_t work = (int64_t)(nrng + L.nfill) * NR;
+        if (work > 0) {
+            const int grid = (int)((work + kBlockThreads - 1) / kBlockThreads);
+            if (NR == 16)
+                hipLaunchKernelGGL((fixup_mm<T, 16>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
+                                   nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
+            else
+                hipLaunchKernelGGL((fixup_mm<T, 64>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
+                                   nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
+            VBC_HIP(hipGetLastError());
+        }
+    }
+    return VBC_OK;
 }
 
 }  // namespace vbc
@@ -707,34 +762,64 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
                 unsigned flags)
 {
     if (int st = check_mul(h, trans, nx, ny)) return st;
-    if (nrhs < 0 || ldx < std::max<int64_t>(nx, 1) || ldy < std::max<int64_t>(ny, 1))
+    const bool rowmajor = (flags & VBC_MAT_ROWMAJOR) != 0;
+    if (nrhs < 0 || (!rowmajor && (ldx < std::max<int64_t>(nx, 1) || ldy < std::max<int64_t>(ny, 1))) ||
+        (rowmajor && (ldx < std::max<int64_t>(nrhs, 1) || ldy < std::max<int64_t>(nrhs, 1))))
         return fail(VBC_INVALID_ARG, "bad nrhs / leading dimensions");
+    if (X == Y && nrhs > 0) return fail(VBC_INVALID_ARG, "X and Y must not alias");
     apply_quirks(trans, flags, alpha, beta);
     const int64_t esz = h->esz;
     DeviceGuard g(h->device);
     if (!g.ok) return fail(VBC_HIP_ERROR, "hipSetDevice failed");
     hipStream_t s = (hipStream_t)stream;
+    const int64_t xbytes = (rowmajor ? nx * ldx : ldx * nrhs) * esz;
+    const int64_t ybytes = (rowmajor ? ny * ldy : ldy * nrhs) * esz;
     const char *dX = static_cast<const char *>(X);
     char *dY = static_cast<char *>(Y);
-    void *sx = nullptr, *sy = nullptr;
+    void *sx = nullptr, *sy = nullptr, *tx = nullptr, *ty = nullptr;
+    int st = VBC_OK;
     if (mem == VBC_MEM_HOST) {
-        if (hipMalloc(&sx, std::max<int64_t>(ldx * nrhs, 1) * esz) != hipSuccess ||
-            hipMalloc(&sy, std::max<int64_t>(ldy * nrhs, 1) * esz) != hipSuccess) {
+        if (hipMalloc(&sx, std::max<int64_t>(xbytes, 1)) != hipSuccess ||
+            hipMalloc(&sy, std::max<int64_t>(ybytes, 1)) != hipSuccess) {
             if (sx) (void)hipFree(sx);
             return fail(VBC_HIP_ERROR, "hipMalloc of staging buffers failed");
         }
-        (void)hipMemcpyAsync(sx, X, ldx * nrhs * esz, hipMemcpyHostToDevice, s);
-        if (beta != 0.0) (void)hipMemcpyAsync(sy, Y, ldy * nrhs * esz, hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(sx, X, xbytes, hipMemcpyHostToDevice, s);
+        if (beta != 0.0) (void)hipMemcpyAsync(sy, Y, ybytes, hipMemcpyHostToDevice, s);
         dX = static_cast<const char *>(sx);
         dY = static_cast<char *>(sy);
     } else if (mem != VBC_MEM_DEVICE) {
         return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
     }
-    int st = VBC_OK;
-    for (int64_t r = 0; r < nrhs && st == VBC_OK; r++)
-        st = mul_dispatch(h, trans, dX + r * ldx * esz, dY + r * ldy * esz, alpha, beta, s);
+    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0;
+    for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
+    if (fused) {
+        st = h->dtype == VBC_F64 ? mulmat_t_rowmajor<double>(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s)
+                                 : mulmat_t_rowmajor<float>(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
+    } else if (!rowmajor) {
+        for (int64_t r = 0; r < nrhs && st == VBC_OK; r++)
+            st = mul_dispatch(h, trans, dX + r * ldx * esz, dY + r * ldy * esz, alpha, beta, s);
+    } else {  // row-major, per column through contiguous temporaries (strided 2D copies)
+        if (hipMalloc(&tx, std::max<int64_t>(nx, 1) * esz) != hipSuccess ||
+            hipMalloc(&ty, std::max<int64_t>(ny, 1) * esz) != hipSuccess)
+            st = fail(VBC_HIP_ERROR, "hipMalloc of column temporaries failed");
+        for (int64_t r = 0; r < nrhs && st == VBC_OK; r++) {
+            if (nx && hipMemcpy2DAsync(tx, esz, dX + r * esz, ldx * esz, esz, nx, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                st = fail(VBC_HIP_ERROR, "column gather failed");
+            if (st == VBC_OK && beta != 0.0 && ny &&
+                hipMemcpy2DAsync(ty, esz, dY + r * esz, ldy * esz, esz, ny, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                st = fail(VBC_HIP_ERROR, "column gather failed");
+            if (st == VBC_OK) st = mul_dispatch(h, trans, tx, ty, alpha, beta, s);
+            if (st == VBC_OK && ny &&
+                hipMemcpy2DAsync(dY + r * esz, ldy * esz, ty, esz, esz, ny, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                st = fail(VBC_HIP_ERROR, "column scatter failed");
+        }
+        if (hipStreamSynchronize(s) != hipSuccess && st == VBC_OK) st = fail(VBC_HIP_ERROR, "sync failed");
+        if (tx) (void)hipFree(tx);
+        if (ty) (void)hipFree(ty);
+    }
     if (mem == VBC_MEM_HOST) {
-        if (st == VBC_OK && (hipMemcpyAsync(Y, sy, ldy * nrhs * esz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        if (st == VBC_OK && (hipMemcpyAsync(Y, sy, ybytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
                              hipStreamSynchronize(s) != hipSuccess))
             st = fail(VBC_HIP_ERROR, "result copy failed");
         (void)hipFree(sx);

@@ -203,7 +203,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     // DPP path: compile-time power-of-two slot count filling the wave; lanes are sub-major
     // (lane = sub * RPI + slot) so each column's slots are contiguous lanes for row_shr/row_bcast.
     constexpr int cLPR = kGeneric ? 0 : W_ / V;
-    constexpr int cRPI = kGeneric ? 0 : 64 / cLPR;
+    constexpr int cRPI = kGeneric ? 0 : 64 / (cLPR > 0 ? cLPR : 1);
     constexpr bool kDpp = !kGeneric && (cRPI & (cRPI - 1)) == 0 && cRPI * cLPR == 64 && cRPI >= 8;
     const int slot = kDpp ? (lane & (cRPI - 1)) : lane / LPR;
     const int sub = kDpp ? (lane / cRPI) : lane - slot * LPR;
@@ -496,6 +496,255 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_ranges(const Bin *__restri
     if (lane == 0) G(b.carry_seg)[r] = -1;  // overwritten below when the range continues a segment
     const bool rd = rd_i != 0;
     switch (b.wkey) { VBC_W_CASES(KIND) default: break; }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Multi-RHS transposed product Y = alpha * B' X + beta * Y over the SAME tiled entry stream.
+// X (m x nrhs) and Y (n x nrhs) are row-major (right-hand sides interleaved: X[i * ldx + j]), so
+// the NR lanes of a slot gather one contiguous X row.  A wave handles 64/NR slots of a tile per
+// pass (in the tile's logical entry order), keeps w accumulators per lane (column c, rhs j), and
+// joins segments across the pass's slots with a shuffle scan; the open segment flows from pass to
+// pass and tile to tile exactly as in run_range.  Continued segments go to carry_mm (w x NR per
+// range) for fixup_mm.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int W_>
+__device__ __forceinline__ void load_row(gptr<const T> p, T (&r)[W_])
+{
+    constexpr int kVec = (W_ * (int)sizeof(T)) % 16 == 0 ? 16 / (int)sizeof(T) : 1;
+    if constexpr (kVec > 1) {
+        typedef T vt __attribute__((ext_vector_type(kVec)));
+#pragma unroll
+        for (int c = 0; c < W_; c += kVec) {
+            const vt t = __builtin_nontemporal_load((gptr<const vt>)(p + c));
+#pragma unroll
+            for (int e = 0; e < kVec; e++) r[c + e] = t[e];
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < W_; c++) r[c] = __builtin_nontemporal_load(p + c);
+    }
+}
+
+template <typename T, int W_, int NR, int K>
+__device__ __forceinline__ void run_range_mm(const Bin &b, int r, int lane, const T *__restrict__ x, int64_t ldx,
+                                             T *__restrict__ y, int64_t ldy, int nrhs, T *__restrict__ carry_mm,
+                                             T alpha, T beta, bool rd)
+{
+    constexpr int SPP = 64 / NR;  // slots per pass
+    const int RPI = b.rpi;
+    const int sl = lane / NR, j = lane - sl * NR;
+    const bool jok = j < nrhs;
+    const int t0 = r * b.tiles_per_range;
+    const int t1 = min(t0 + b.tiles_per_range, b.ntiles);
+    if (t0 >= t1) return;
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> xg = G(x);
+    gptr<T> yg = G(y);
+    const size_t tile_rows = (size_t)RPI * K;
+    int seg_base = G(b.rseg)[r];
+    const bool starts_at_head = (key[(size_t)t0 * tile_rows] & kHead) != 0;
+    T carry[W_];
+#pragma unroll
+    for (int c = 0; c < W_; c++) carry[c] = T(0);
+    bool owned = false;
+
+    auto emit_mm = [&](int seg, const T (&v)[W_]) {
+        if (!jok) return;
+        const int o = out_of(b, seg);
+#pragma unroll
+        for (int c = 0; c < W_; c++) {
+            gptr<T> yo = yg + (int64_t)(o + c) * ldy + j;
+            T q = alpha * v[c];
+            if (rd) q = __builtin_fma(beta, *yo, q);
+            *yo = q;
+        }
+    };
+    auto hand_mm = [&](int seg, const T (&v)[W_]) {
+        gptr<T> c0 = G(carry_mm) + ((size_t)r * W_) * NR + j;
+#pragma unroll
+        for (int c = 0; c < W_; c++) c0[c * NR] = v[c];
+        if (j == 0) G(b.carry_seg)[r] = seg;
+    };
+
+    for (int t = t0; t < t1; t++) {
+        const size_t base = (size_t)t * tile_rows;
+        for (int p = 0; p < RPI; p += SPP) {
+            const int s = p + sl;
+            const bool sv = s < RPI;
+            const int npass = min(SPP, RPI - p);  // valid slots in this pass
+            uint32_t kk[K];
+            T vv[K][W_], xv[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const size_t e = base + (size_t)k * RPI + s;
+                if (sv) {
+                    kk[k] = __builtin_nontemporal_load(key + e);
+                    load_row<T, W_>(val + e * W_, vv[k]);
+                } else {
+                    kk[k] = 0u;
+#pragma unroll
+                    for (int c = 0; c < W_; c++) vv[k][c] = T(0);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++) xv[k] = (sv && jok) ? xg[(int64_t)(kk[k] & ~kHead) * ldx + j] : T(0);
+            int nh = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++) nh += (int)(kk[k] >> 31);
+            int pre = nh;
+            for (int d = 1; d < SPP; d <<= 1) {
+                const int o = __shfl(pre, (lane - d * NR) & 63, 64);
+                if (sl >= d) pre += o;
+            }
+            const int pass_heads = __shfl(pre, (npass - 1) * NR, 64);
+            pre -= nh;
+
+            T lead[W_], cur[W_];
+#pragma unroll
+            for (int c = 0; c < W_; c++) lead[c] = cur[c] = T(0);
+            int seg = seg_base + pre - 1;
+            bool seen = false;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                if (kk[k] & kHead) {
+                    if (seen) emit_mm(seg, cur);
+                    else {
+#pragma unroll
+                        for (int c = 0; c < W_; c++) lead[c] = cur[c];
+                    }
+                    seg++;
+                    seen = true;
+#pragma unroll
+                    for (int c = 0; c < W_; c++) cur[c] = T(0);
+                }
+#pragma unroll
+                for (int c = 0; c < W_; c++) cur[c] = __builtin_fma(vv[k][c], xv[k], cur[c]);
+            }
+            if (!seen) {
+#pragma unroll
+                for (int c = 0; c < W_; c++) {
+                    lead[c] = cur[c];
+                    cur[c] = T(0);
+                }
+            }
+            // segmented scan over the pass's slots (lane stride NR)
+            bool f = seen;
+            T sc[W_];
+#pragma unroll
+            for (int c = 0; c < W_; c++) sc[c] = seen ? cur[c] : lead[c];
+            for (int d = 1; d < SPP; d <<= 1) {
+                const int src = (lane - d * NR) & 63;
+                const bool of = __shfl((int)f, src, 64) != 0;
+                T os[W_];
+#pragma unroll
+                for (int c = 0; c < W_; c++) os[c] = __shfl(sc[c], src, 64);
+                if (sl >= d) {
+                    if (!f) {
+#pragma unroll
+                        for (int c = 0; c < W_; c++) sc[c] += os[c];
+                    }
+                    f = f || of;
+                }
+            }
+            const int srcx = (lane - NR) & 63;
+            bool ef = __shfl((int)f, srcx, 64) != 0;
+            T es[W_];
+#pragma unroll
+            for (int c = 0; c < W_; c++) es[c] = __shfl(sc[c], srcx, 64);
+            if (sl == 0) {
+                ef = false;
+#pragma unroll
+                for (int c = 0; c < W_; c++) es[c] = T(0);
+            }
+            if (sv && seen) {
+                const int cseg = seg_base + pre - 1;
+                const bool from_range = ef || owned;
+                if (from_range || !starts_at_head) {
+                    T tot[W_];
+#pragma unroll
+                    for (int c = 0; c < W_; c++) tot[c] = (ef ? es[c] : carry[c] + es[c]) + lead[c];
+                    if (from_range) emit_mm(cseg, tot);
+                    else hand_mm(cseg, tot);
+                }
+            }
+            const int last = (npass - 1) * NR + j;
+            const bool lf = __shfl((int)f, last, 64) != 0;
+#pragma unroll
+            for (int c = 0; c < W_; c++) {
+                const T ls = __shfl(sc[c], last, 64);
+                carry[c] = lf ? ls : carry[c] + ls;
+            }
+            owned = owned || lf;
+            seg_base += pass_heads;
+        }
+    }
+    if (sl == 0) {
+        const int cseg = seg_base - 1;
+        if (owned) emit_mm(cseg, carry);
+        else if (!starts_at_head) hand_mm(cseg, carry);
+    }
+}
+
+template <typename T, int NR, int K>
+__global__ __launch_bounds__(kBlockThreads) void spmm_ranges(const Bin *__restrict__ bins, int nbins, int total_ranges,
+                                                             const T *__restrict__ x, int64_t ldx, T *__restrict__ y,
+                                                             int64_t ldy, int nrhs, T *__restrict__ carry_mm, int64_t carry_stride,
+                                                             T alpha, T beta, int rd_i)
+{
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= total_ranges) return;
+    int bi = 0;
+    while (bi + 1 < nbins && bins[bi + 1].range0 <= rg) bi++;
+    const Bin b = bins[bi];
+    const int r = rg - b.range0;
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) G(b.carry_seg)[r] = -1;
+    const bool rd = rd_i != 0;
+    T *cm = carry_mm + (size_t)bi * carry_stride;
+    switch (b.wkey) {
+    case 1: run_range_mm<T, 1, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 2: run_range_mm<T, 2, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 3: run_range_mm<T, 3, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 4: run_range_mm<T, 4, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 5: run_range_mm<T, 5, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 6: run_range_mm<T, 6, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 7: run_range_mm<T, 7, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    case 8: run_range_mm<T, 8, NR, K>(b, r, lane, x, ldx, y, ldy, nrhs, cm, alpha, beta, rd); break;
+    default: break;
+    }
+}
+
+// Fix-up of the multi-RHS product: one thread per (range, rhs); fill list rows per rhs.
+template <typename T, int NR>
+__global__ __launch_bounds__(kBlockThreads) void fixup_mm(const Bin *__restrict__ bins, int nbins, int total_ranges,
+                                                          const int32_t *__restrict__ fill, int nfill,
+                                                          T *__restrict__ y, int64_t ldy, int nrhs,
+                                                          const T *__restrict__ carry_mm, int64_t carry_stride,
+                                                          T alpha, T beta, int rd_i)
+{
+    const int i = blockIdx.x * kBlockThreads + threadIdx.x;
+    const int item = i / NR, j = i % NR;
+    if (j >= nrhs) return;
+    if (item < total_ranges) {
+        int bi = 0;
+        while (bi + 1 < nbins && bins[bi + 1].range0 <= item) bi++;
+        const Bin &b = bins[bi];
+        const int r = item - b.range0;
+        const int seg = b.carry_seg[r];
+        if (seg < 0 || (r > 0 && b.carry_seg[r - 1] == seg)) return;
+        const T *cm = carry_mm + (size_t)bi * carry_stride;
+        const int o = out_of(b, seg);
+        for (int c = 0; c < b.w; c++) {
+            T s = T(0);
+            for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++) s += cm[((size_t)q * b.w + c) * NR + j];
+            T *yo = y + (int64_t)(o + c) * ldy + j;
+            *yo = __builtin_fma(alpha, s, *yo);
+        }
+    } else if (item - total_ranges < nfill) {
+        T *yo = y + (int64_t)fill[item - total_ranges] * ldy + j;
+        *yo = rd_i ? beta * *yo : T(0);
+    }
 }
 
 // Fix-up: add every continued-segment partial (summed in range order: deterministic) and apply

@@ -45,9 +45,17 @@ def _mem_device_stream(x, y, stream):
     return _L.VBC_MEM_HOST, 0, None
 
 
-def _check_vec(a, dtype, name):
-    if a.dtype != dtype if isinstance(a, np.ndarray) else str(a.dtype) != "torch." + np.dtype(dtype).name:
+def _check_dtype(a, dtype, name):
+    if isinstance(a, np.ndarray):
+        same = a.dtype == np.dtype(dtype)
+    else:
+        same = str(a.dtype) == "torch." + np.dtype(dtype).name
+    if not same:
         raise _L.UnsupportedDtype(f"{name} eltype {a.dtype} != matrix eltype {np.dtype(dtype)}")
+
+
+def _check_vec(a, dtype, name):
+    _check_dtype(a, dtype, name)
     contiguous = a.flags.c_contiguous if isinstance(a, np.ndarray) else a.is_contiguous()
     if not contiguous:
         raise _L.ArgumentError(f"{name} must be contiguous (StridedVector with stride 1)")
@@ -76,25 +84,42 @@ def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None
     return y
 
 
+def _layout(M):
+    """'R' for row-major (C-contiguous, right-hand sides interleaved), 'C' for column-major."""
+    if isinstance(M, np.ndarray):
+        if M.flags.c_contiguous and M.shape[1] > 1:
+            return "R", M.strides[0] // M.itemsize
+        if M.flags.f_contiguous:
+            return "C", (M.strides[1] // M.itemsize) if M.shape[1] > 1 else max(M.shape[0], 1)
+    else:
+        if M.stride(1) == 1 and M.shape[1] > 1:
+            return "R", M.stride(0)
+        if M.stride(0) == 1:
+            return "C", M.stride(1) if M.shape[1] > 1 else max(M.shape[0], 1)
+    raise _L.ArgumentError("matrix operands must be row-major or column-major with unit inner stride")
+
+
 def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False):
-    """Multi-RHS Y = α·op(A)·X + β·Y, column by column semantics (no reference kernel exists)."""
+    """Multi-RHS Y = α·op(A)·X + β·Y (column-by-column semantics; the reference has no matrix
+    mul!).  Row-major X / Y (right-hand sides contiguous) use the fused multi-RHS kernel for B'X;
+    column-major (Julia) operands run one SpMV per column."""
     B, trans = _unwrap(A)
     mem, dev, stream = _mem_device_stream(X, Y, stream)
-    if mem == _L.VBC_MEM_HOST:
-        # column-major (Julia) layout expected
-        if not (X.flags.f_contiguous and Y.flags.f_contiguous):
-            raise _L.ArgumentError("host X / Y must be Fortran-ordered (column-major, like Julia)")
-        ldx, ldy = X.shape[0], Y.shape[0]
-    else:
-        # torch: accept a (k, rows) C-contiguous tensor viewed as column-major (rows, k) via .T
-        if not (X.stride(0) == 1 and Y.stride(0) == 1):
-            raise _L.ArgumentError("device X / Y must be column-major: pass M.T of a contiguous (k, rows) tensor")
-        ldx, ldy = X.stride(1), Y.stride(1)
-    nrhs = X.shape[1]
-    if Y.shape[1] != nrhs:
+    _check_dtype(X, B.dtype, "X")
+    _check_dtype(Y, B.dtype, "Y")
+    if X.shape[1] != Y.shape[1]:
         raise _L.DimensionMismatch("X and Y have different numbers of columns")
+    if X.shape[1] <= 1:
+        lx = ly = "C"
+        ldx, ldy = max(X.shape[0], 1), max(Y.shape[0], 1)
+    else:
+        lx, ldx = _layout(X)
+        ly, ldy = _layout(Y)
+    if lx != ly:
+        raise _L.ArgumentError("X and Y must have the same layout")
+    nrhs = X.shape[1]
     h = B.handle(dev, trans)
-    flags = _L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0
+    flags = (_L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0) | (_L.VBC_MAT_ROWMAJOR if lx == "R" else 0)
     _L.check(_L.lib().vbc_mul_mat(h, int(trans), nrhs, _L.ptr(X), max(ldx, 1), X.shape[0], _L.ptr(Y),
                                   max(ldy, 1), Y.shape[0], float(alpha), float(beta), mem, stream, flags),
              "mul!")
@@ -106,11 +131,12 @@ def matmul(A, x):
     m = A.shape[0]
     if _is_torch(x):
         import torch
-        y = torch.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        if x.dim() == 2:
+        y = torch.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)  # same layout as x
+        if x.dim() == 2 and x.stride(0) == 1 and x.shape[1] > 1:
             y = torch.empty((x.shape[1], m), dtype=x.dtype, device=x.device).T
     else:
-        y = np.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, order="F")
+        order = "F" if (x.ndim == 2 and x.flags.f_contiguous and not x.flags.c_contiguous) else "C"
+        y = np.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, order=order)
     return mul_(y, A, x, True, False)
 
 
