@@ -43,6 +43,10 @@ typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
 /* create flags */
 #define VBC_CREATE_TRANSPOSED 0x1u /* build the layout for mul!(y, B', x)  (default if 0 given) */
 #define VBC_CREATE_FORWARD 0x2u    /* build the layout for mul!(y, B, x)                         */
+#define VBC_CREATE_MULTI 0x4u      /* build the panel layout of the multi-RHS transposed product
+                                      Y = α·B'X + β·Y on matrix cores (vbc_mul_mat, trans = 1,
+                                      any operand layout; stripes wider than 16 are cut into
+                                      16-column pieces).  Independent of the SpMV layouts. */
 
 /* mul flags */
 #define VBC_MAT_ROWMAJOR 0x2u         /* vbc_mul_mat: X, Y row-major (right-hand sides interleaved,
@@ -102,7 +106,10 @@ int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_
 /* Multi-RHS Y = α·op(B)·X + β·Y.  X is nx × nrhs, Y is ny × nrhs; column-major (ldx >= nx, ldy >=
  * ny) by default, row-major with VBC_MAT_ROWMAJOR (ldx, ldy >= nrhs).  The reference has no matrix
  * mul! (Base.:* forwards to an undefined method, multiply_1DVBC.jl:184-185), so the semantics is
- * defined column by column as vbc_mul.  Fused kernel: transposed, row-major, widths <= 8. */
+ * defined column by column as vbc_mul.  trans = 1 on a handle with VBC_CREATE_MULTI: one
+ * matrix-core pass per 64 right-hand sides, row- or column-major.  Otherwise the transposed
+ * row-major product with widths <= 8 runs a fused vector kernel over the SpMV layout, and the other
+ * cases run one SpMV per column. */
 int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t ldx, int64_t nx,
                 void *Y, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
                 unsigned flags);
@@ -124,6 +131,9 @@ typedef struct vbc_info {
     int64_t device_bytes;   /* HBM held by the handle */
     int64_t bytes_t;        /* HBM bytes one transposed product moves in this layout */
     int64_t bytes_f;        /* same for the forward product */
+    int32_t bins_m;         /* width buckets of the multi-RHS panel layout (0 = absent) */
+    int32_t reserved_;
+    int64_t bytes_m;        /* matrix bytes (keys + values, panel-padded) one panel pass streams */
 } vbc_info;
 
 int vbc_get_info(const vbc_handle *h, vbc_info *info);

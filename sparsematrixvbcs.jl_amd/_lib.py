@@ -16,7 +16,7 @@ VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR, VBC_UN
     VBC_ASSERTION = range(7)
 VBC_F64, VBC_F32 = 0, 1
 VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
-VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD = 0x1, 0x2
+VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD, VBC_CREATE_MULTI = 0x1, 0x2, 0x4
 VBC_MUL_REFERENCE_QUIRKS = 0x1
 VBC_MAT_ROWMAJOR = 0x2
 
@@ -51,7 +51,8 @@ class vbc_info(C.Structure):
                 ("nblocks", C.c_int64), ("nrows", C.c_int64), ("nval", C.c_int64),
                 ("nnz_hint", C.c_int64), ("dtype", C.c_int32), ("device", C.c_int32),
                 ("bins_t", C.c_int32), ("bins_f", C.c_int32), ("device_bytes", C.c_int64),
-                ("bytes_t", C.c_int64), ("bytes_f", C.c_int64)]
+                ("bytes_t", C.c_int64), ("bytes_f", C.c_int64), ("bins_m", C.c_int32),
+                ("reserved_", C.c_int32), ("bytes_m", C.c_int64)]
 
 
 _lib = None

@@ -13,6 +13,7 @@
 
 #include "vbc_internal.h"
 #include "vbc_kernels.h"
+#include "vbc_panel.h"
 
 namespace vbc {
 
@@ -62,6 +63,16 @@ struct Launch {
     const int32_t *d_fill = nullptr;
 };
 
+// The panel layout of the MFMA multi-RHS transposed product (vbc_panel.h): one launch.
+struct PanelLaunch {
+    std::vector<PanelBin> bins;
+    PanelBin *d_bins = nullptr;
+    int total_ranges = 0;
+    int nfill = 0;
+    size_t o_fill = 0;
+    const int32_t *d_fill = nullptr;
+};
+
 // Host description of the input stripes, common to 1D, 2D (expanded) and CSC inputs.
 struct Stripes {
     int64_t m = 0, n = 0, L = 0;
@@ -79,7 +90,11 @@ struct vbc_handle {
     int dtype = 0, esz = 8, device = 0;
     void *d_arena = nullptr;
     size_t arena_bytes = 0;
-    bool has_t = false, has_f = false;
+    bool has_t = false, has_f = false, has_m = false;
+    vbc::PanelLaunch lm;          // multi-RHS transposed product on matrix cores (VBC_CREATE_MULTI)
+    int64_t bytes_m = 0;          // matrix bytes one panel product streams
+    int target_ranges_m = 4096;
+    int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA (ablation / debugging)
     vbc::Launch lt;               // transposed product: all buckets in one launch
     std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
     bool f_scale = false;         // forward with several buckets: scale y by beta first
@@ -271,6 +286,139 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
     return VBC_OK;
 }
 
+struct PendingPanel {
+    PanelBin b;
+    size_t o_key, o_val, o_out, o_rgrp, o_rseg;
+};
+
+// Panel layout (vbc_panel.h) of the transposed product: per width bucket (stripes wider than 16 are
+// cut into 16-column pieces that share the stripe's rows), S = 16/w consecutive stripes per panel,
+// each panel's rows padded to a multiple of 4, ranges of whole panels balanced by rows.
+static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
+                       std::vector<PendingPanel> &pps, PanelLaunch &L, std::vector<int32_t> &fill)
+{
+    struct Piece {
+        int64_t l;
+        int c0;
+    };
+    std::map<int, std::vector<Piece>> buckets;  // piece width -> pieces
+    for (int64_t l = 0; l < s.L; l++) {
+        if (s.rbeg[l + 1] == s.rbeg[l]) {
+            for (int c = 0; c < s.w[l]; c++) fill.push_back((int32_t)(s.col0[l] + c));
+            continue;
+        }
+        for (int c0 = 0; c0 < s.w[l]; c0 += 16) buckets[std::min(16, s.w[l] - c0)].push_back({l, c0});
+    }
+    const int esz = h->esz;
+    // groups of every bucket first: ranges are spread over the launch in proportion to them
+    std::map<int, std::vector<int64_t>> pgroups;  // w -> groups per panel
+    int64_t total_groups = 0;
+    for (auto &kv : buckets) {
+        const int S = 16 / kv.first;
+        auto &pg = pgroups[kv.first];
+        for (size_t p0 = 0; p0 < kv.second.size(); p0 += S) {
+            int64_t rows = 0;
+            for (size_t p = p0; p < std::min(kv.second.size(), p0 + S); p++)
+                rows += s.rbeg[kv.second[p].l + 1] - s.rbeg[kv.second[p].l];
+            pg.push_back((rows + 3) / 4);
+            total_groups += pg.back();
+        }
+    }
+    if (total_groups >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "matrix too large for the panel layout");
+    int range0 = 0;
+    for (auto &kv : buckets) {
+        const int w = kv.first, S = 16 / w;
+        const std::vector<Piece> &pcs = kv.second;
+        const std::vector<int64_t> &pg = pgroups[w];
+        int64_t G = 0;
+        for (int64_t g : pg) G += g;
+        int64_t nr = (int64_t)std::llround((double)h->target_ranges_m * (double)G / (double)std::max<int64_t>(total_groups, 1));
+        nr = std::max<int64_t>(1, std::min<int64_t>(nr, (int64_t)pg.size()));
+        std::vector<int32_t> rgrp{0}, rseg{0};
+        int64_t acc = 0;
+        for (size_t p = 0; p < pg.size(); p++) {
+            acc += pg[p];
+            // close a range once it holds its share of the bucket's groups
+            if (p + 1 < pg.size() && (int64_t)rgrp.size() < nr && acc * nr >= (int64_t)rgrp.size() * G) {
+                rgrp.push_back((int32_t)acc);
+                rseg.push_back((int32_t)((p + 1) * S));
+            }
+        }
+        rgrp.push_back((int32_t)acc);
+        nr = (int64_t)rseg.size();
+        PendingPanel pp{};
+        pp.b.w = w;
+        pp.b.S = S;
+        pp.b.range0 = range0;
+        pp.b.nranges = (int32_t)nr;
+        range0 += (int)nr;
+        std::vector<int32_t> out(pcs.size());
+        for (size_t p = 0; p < pcs.size(); p++) out[p] = (int32_t)(s.col0[pcs[p].l] + pcs[p].c0);
+        pp.b.out_affine = 1;
+        pp.b.out_base = out[0];
+        pp.b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
+        for (size_t q = 1; q < out.size() && pp.b.out_affine; q++)
+            pp.b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * pp.b.out_stride;
+        const int64_t Rp = acc * 4;
+        const int64_t Ra = Rp + kPanelTail;  // over-read padding (vbc_panel.h)
+        pp.o_key = ar.reserve(Ra * 4);
+        pp.o_val = ar.reserve(Ra * w * esz);
+        pp.o_out = ar.reserve(out.size() * 4);
+        pp.o_rgrp = ar.reserve(rgrp.size() * 4);
+        pp.o_rseg = ar.reserve(rseg.size() * 4);
+        std::memcpy(ar.at<int32_t>(pp.o_out), out.data(), out.size() * 4);
+        std::memcpy(ar.at<int32_t>(pp.o_rgrp), rgrp.data(), rgrp.size() * 4);
+        std::memcpy(ar.at<int32_t>(pp.o_rseg), rseg.data(), rseg.size() * 4);
+        uint32_t *key = ar.at<uint32_t>(pp.o_key);
+        char *vv = ar.at<char>(pp.o_val);
+        int64_t row = 0;
+        for (size_t p0 = 0; p0 < pcs.size(); p0 += S) {
+            for (size_t p = p0; p < std::min(pcs.size(), p0 + S); p++) {
+                const int64_t l = pcs[p].l;
+                const int wl = s.w[l];
+                for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++, row++) {
+                    key[row] = (uint32_t)s.rows[q] | (q == s.rbeg[l] ? kHead : 0u);
+                    std::memcpy(vv + row * w * esz, val + (s.voff[l] + (q - s.rbeg[l]) * wl + pcs[p].c0) * esz,
+                                (size_t)w * esz);
+                }
+            }
+            for (; row % 4; row++) {
+                key[row] = kPanelSentinel;
+                std::memset(vv + row * w * esz, 0, (size_t)w * esz);
+            }
+        }
+        for (; row < Ra; row++) {
+            key[row] = kPanelSentinel;
+            std::memset(vv + row * w * esz, 0, (size_t)w * esz);
+        }
+        h->bytes_m += Rp * (4 + (int64_t)w * esz) + (int64_t)out.size() * 4;
+        pps.push_back(pp);
+    }
+    L.total_ranges = range0;
+    return VBC_OK;
+}
+
+static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, PanelLaunch &L)
+{
+    L.bins.clear();
+    char *base = static_cast<char *>(h->d_arena);
+    for (const PendingPanel &pp : pps) {
+        PanelBin b = pp.b;
+        b.key = reinterpret_cast<const uint32_t *>(base + pp.o_key);
+        b.val = base + pp.o_val;
+        b.out = reinterpret_cast<const int32_t *>(base + pp.o_out);
+        b.rgrp = reinterpret_cast<const int32_t *>(base + pp.o_rgrp);
+        b.rseg = reinterpret_cast<const int32_t *>(base + pp.o_rseg);
+        L.bins.push_back(b);
+    }
+    L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
+    if (!L.bins.empty()) {
+        VBC_HIP(hipMalloc(&L.d_bins, L.bins.size() * sizeof(PanelBin)));
+        VBC_HIP(hipMemcpy(L.d_bins, L.bins.data(), L.bins.size() * sizeof(PanelBin), hipMemcpyHostToDevice));
+    }
+    return VBC_OK;
+}
+
 static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, Launch &L)
 {
     L.bins.clear();
@@ -298,6 +446,7 @@ static void release(vbc_handle *h)
     if (!h) return;
     DeviceGuard g(h->device);
     if (h->lt.d_bins) (void)hipFree(h->lt.d_bins);
+    if (h->lm.d_bins) (void)hipFree(h->lm.d_bins);
     for (auto &l : h->lf)
         if (l.d_bins) (void)hipFree(l.d_bins);
     if (h->d_arena) (void)hipFree(h->d_arena);
@@ -325,7 +474,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     int ndev = 0;
     VBC_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(VBC_INVALID_ARG, "device ordinal out of range");
-    if ((flags & (VBC_CREATE_TRANSPOSED | VBC_CREATE_FORWARD)) == 0) flags |= VBC_CREATE_TRANSPOSED;
+    if ((flags & (VBC_CREATE_TRANSPOSED | VBC_CREATE_FORWARD | VBC_CREATE_MULTI)) == 0) flags |= VBC_CREATE_TRANSPOSED;
 
     vbc_handle *h = new vbc_handle();
     h->m = s.m;
@@ -368,13 +517,31 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     for (int kd = 0; kd < 2; kd++)
         h->target_ranges_k[kd] = prop.multiProcessorCount * std::max(1, std::min(occ[kd], 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
+    if (flags & VBC_CREATE_MULTI) {
+        int om = 0;
+        if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1>, kBlockThreads, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<float, 1>, kBlockThreads, 0);
+        h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
+        if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
+        if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
+    }
 
     Arena ar;
     std::vector<PendingBin> pt;
     std::vector<std::vector<PendingBin>> pf;
-    std::vector<int32_t> fill_t, fill_f;
+    std::vector<PendingPanel> pm;
+    std::vector<int32_t> fill_t, fill_f, fill_m;
     int st = VBC_OK;
-    if (flags & VBC_CREATE_TRANSPOSED) {
+    if (flags & VBC_CREATE_MULTI) {
+        st = build_panel(h, s, v, ar, pm, h->lm, fill_m);
+        h->has_m = st == VBC_OK;
+        if (st == VBC_OK) {
+            h->lm.nfill = (int)fill_m.size();
+            h->lm.o_fill = ar.reserve(fill_m.size() * 4);
+            std::memcpy(ar.at<int32_t>(h->lm.o_fill), fill_m.data(), fill_m.size() * 4);
+        }
+    }
+    if (st == VBC_OK && (flags & VBC_CREATE_TRANSPOSED)) {
         st = build_transposed(h, s, v, ar, pt, h->lt, fill_t);
         h->has_t = st == VBC_OK;
         if (st == VBC_OK) {
@@ -405,6 +572,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         return fail(VBC_HIP_ERROR, "hipMemcpy of the matrix arena failed");
     }
     if (h->has_t && (st = finalize_launch(h, pt, h->lt))) { release(h); return st; }
+    if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)
         if ((st = finalize_launch(h, pf[b], h->lf[b]))) { release(h); return st; }
     if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, h->lf[0]))) { release(h); return st; }
@@ -539,6 +707,39 @@ static int mulmat_t_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t
             else
                 hipLaunchKernelGGL((fixup_mm<T, 64>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
                                    nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
+            VBC_HIP(hipGetLastError());
+        }
+    }
+    return VBC_OK;
+}
+
+// Multi-RHS transposed product on the panel layout (MFMA), X / Y addressed by (row, column) strides,
+// in chunks of <= 64 right-hand sides (four 16-column accumulators).
+template <typename T>
+static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
+                        int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s)
+{
+    const PanelLaunch &L = h->lm;
+    const bool rd = beta != 0.0;
+    for (int64_t c0 = 0; c0 < nrhs; c0 += 64) {
+        const int nr = (int)std::min<int64_t>(64, nrhs - c0);
+        const T *xs = reinterpret_cast<const T *>(X) + c0 * sxc;
+        T *ys = reinterpret_cast<T *>(Y) + c0 * syc;
+        if (L.total_ranges > 0) {
+            const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
+#define VBC_PANEL(NB)                                                                                     \
+    hipLaunchKernelGGL((spmm_panel<T, NB>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(), \
+                       L.total_ranges, xs, sxr, sxc, ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu)
+            if (nr <= 16) VBC_PANEL(1);
+            else if (nr <= 32) VBC_PANEL(2);
+            else VBC_PANEL(4);
+#undef VBC_PANEL
+            VBC_HIP(hipGetLastError());
+        }
+        if (L.nfill > 0) {
+            const int64_t work = (int64_t)L.nfill * nr;
+            hipLaunchKernelGGL((fill_rows_mm<T>), dim3((int)((work + kBlockThreads - 1) / kBlockThreads)), dim3(kBlockThreads),
+                               0, s, L.d_fill, L.nfill, ys, syr, syc, nr, (T)beta, (int)rd);
             VBC_HIP(hipGetLastError());
         }
     }
@@ -706,16 +907,20 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->device_bytes = (int64_t)h->arena_bytes;
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
+    info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : 0;
+    info->bytes_m = h->bytes_m;
     return VBC_OK;
 }
 
-static int check_mul(const vbc_handle *h, int trans, int64_t nx, int64_t ny)
+static int check_mul(const vbc_handle *h, int trans, int64_t nx, int64_t ny, bool mat = false)
 {
     if (!h) return fail(VBC_INVALID_ARG, "NULL handle");
     // DimensionMismatch checks: multiply_1DVBC.jl:44-45 (forward), :139-140 (transposed)
     const int64_t want_x = trans ? h->m : h->n, want_y = trans ? h->n : h->m;
     if (nx != want_x || ny != want_y) return fail(VBC_DIM_MISMATCH, "DimensionMismatch");
-    if (trans && !h->has_t) return fail(VBC_INVALID_ARG, "handle built without VBC_CREATE_TRANSPOSED");
+    if (trans && !h->has_t && !(mat && h->has_m))
+        return fail(VBC_INVALID_ARG, mat ? "handle built without VBC_CREATE_TRANSPOSED or VBC_CREATE_MULTI"
+                                         : "handle built without VBC_CREATE_TRANSPOSED");
     if (!trans && !h->has_f) return fail(VBC_INVALID_ARG, "handle built without VBC_CREATE_FORWARD");
     return VBC_OK;
 }
@@ -761,7 +966,7 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
                 void *Y, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
                 unsigned flags)
 {
-    if (int st = check_mul(h, trans, nx, ny)) return st;
+    if (int st = check_mul(h, trans, nx, ny, true)) return st;
     const bool rowmajor = (flags & VBC_MAT_ROWMAJOR) != 0;
     if (nrhs < 0 || (!rowmajor && (ldx < std::max<int64_t>(nx, 1) || ldy < std::max<int64_t>(ny, 1))) ||
         (rowmajor && (ldx < std::max<int64_t>(nrhs, 1) || ldy < std::max<int64_t>(nrhs, 1))))
@@ -791,9 +996,14 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
     } else if (mem != VBC_MEM_DEVICE) {
         return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
     }
-    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0;
+    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t;
     for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
-    if (fused) {
+    if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
+        const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
+        const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;
+        st = h->dtype == VBC_F64 ? mulmat_panel<double>(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s)
+                                 : mulmat_panel<float>(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
+    } else if (fused) {
         st = h->dtype == VBC_F64 ? mulmat_t_rowmajor<double>(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s)
                                  : mulmat_t_rowmajor<float>(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
     } else if (!rowmajor) {

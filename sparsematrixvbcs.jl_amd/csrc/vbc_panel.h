@@ -1,0 +1,242 @@
+// gfx950 multi-RHS transposed product on matrix cores (device code, included by vbc_device.hip).
+//
+// Y = alpha * B' X + beta * Y for k right-hand sides (multiply_1DVBC.jl:90-134 and
+// multiply_VBC.jl:93-147 applied column by column; the reference itself has no matrix mul!,
+// multiply_1DVBC.jl:184-185).  For a stripe l of width w with stored rows r (2D tiles expanded into
+// their u rows), Y[cols of l, :] = V_l' X[rows of l, :] is a (w x R_l) * (R_l x k) dense product,
+// so the stripe's rows are fed to v_mfma_{f32,f64}_16x16x4 four at a time:
+//     A (16 x 4)  = val of 4 stored rows, output column c on the M axis,
+//     B (4 x 16)  = the 4 gathered X rows, 16 right-hand sides on the N axis,
+//     C (16 x 16) += A B.
+// A *panel* packs S = 16/w consecutive stripes of one width bucket onto the 16 M rows (stripe s of
+// the panel owns rows s*w .. s*w+w-1), so narrow stripes still fill the accumulator: a row only
+// contributes to the M rows of its own stripe (the A operand is masked by the row's stripe index,
+// which the wave derives from the HEAD bits of the keys with one ballot per 64 rows).  Each panel's
+// rows are padded to a multiple of 4 (sentinel key, zero val), so a 4-row group never straddles two
+// panels; at a panel boundary the accumulator is written out (w*S output columns x 16 RHS, 64-B
+// rows of Y) and cleared.  A wave owns a contiguous run of whole panels: no carries, no fix-up, and
+// a fixed summation order (rows in stored order, one fma per row, MFMA k-order) -- deterministic.
+// IEEE: a non-finite X value times a masked-out zero would put NaN into the other stripes of the
+// panel, so a batch whose gathered X holds an Inf / NaN is multiplied on the VALU instead (the same
+// k-ordered fma chain, so finite results are unchanged) with each row confined to its own stripe.
+// X and Y are addressed through (row, column) strides, so row-major and column-major operands take
+// the same kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace vbc {
+
+constexpr uint32_t kPanelSentinel = 0x7FFFFFFFu;  // padding row: no HEAD, never a valid row (m < 2^31)
+
+// One width bucket of the panel layout.
+struct PanelBin {
+    int32_t w;          // stripe width (1..16)
+    int32_t S;          // stripes per panel = 16 / w
+    int32_t range0;     // first range (wave) of this bucket in the launch
+    int32_t nranges;
+    int32_t out_affine;  // out[s] == out_base + s * out_stride
+    int32_t out_base;
+    int32_t out_stride;
+    int32_t pad_;
+    const uint32_t *key;  // rows (panel-padded): HEAD | x row, or kPanelSentinel
+    const void *val;      // rows * w values
+    const int32_t *out;   // per stripe: first y column
+    const int32_t *rgrp;  // per range + 1: first 4-row group
+    const int32_t *rseg;  // per range: first stripe
+};
+
+template <typename T>
+struct MfmaAcc;
+template <>
+struct MfmaAcc<float> {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ v4 mma(float a, float b, v4 c)
+    {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // C/D map of the 16x16x4 f32 form: col = lane & 15, row = (lane >> 4) * 4 + reg
+    static __device__ __forceinline__ int row(int lane, int reg) { return (lane >> 4) * 4 + reg; }
+};
+template <>
+struct MfmaAcc<double> {
+    typedef double v4 __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ v4 mma(double a, double b, v4 c)
+    {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // f64 16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
+    static __device__ __forceinline__ int row(int lane, int reg) { return (lane >> 4) + 4 * reg; }
+};
+
+__device__ __forceinline__ int panel_out(const PanelBin &b, int seg)
+{
+    return b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
+}
+
+// kBatch groups (4 rows each) are loaded before any of them is multiplied: one coalesced key load
+// per 64 rows, then every val and X load of the batch in flight together.
+constexpr int kPanelBatch = 16;
+constexpr int kPanelTail = 8 * kPanelBatch;  // padding rows after each bin (batch over-read + key prefetch)
+
+template <typename T, int NB>
+__global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__restrict__ bins, int nbins,
+                                                            int total_ranges, const T *__restrict__ X, int64_t sxr,
+                                                            int64_t sxc, T *__restrict__ Y, int64_t syr, int64_t syc,
+                                                            int nrhs, T alpha, T beta, int rd_i, int force_valu)
+{
+    using M = MfmaAcc<T>;
+    typedef typename M::v4 v4;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= total_ranges) return;
+    int bi = 0;
+    while (bi + 1 < nbins && bins[bi + 1].range0 <= rg) bi++;
+    const PanelBin b = bins[bi];
+    const int r = rg - b.range0;
+    const int g0 = b.rgrp[r], g1 = b.rgrp[r + 1];
+    if (g0 >= g1) return;
+    int seg_base = b.rseg[r];
+    const int lane = threadIdx.x & 63;
+    const int w = b.w, S = b.S;
+    // A operand: M row c = lane & 15 (stripe c / w of the panel, column c % w), k = lane >> 4.
+    const int ca = lane & 15, kr = lane >> 4;
+    const int sa = ca / w, cola = ca - sa * w;
+    const bool arow = sa < S;
+    // B operand / C column: right-hand side j = lane & 15.
+    const int j = lane & 15;
+    // C rows held by this lane: stripe and column for each of the 4 accumulator registers.
+    int cs[4], cc[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int c = M::row(lane, q);
+        cs[q] = c / w;
+        cc[q] = c - cs[q] * w;
+        if (cs[q] >= S) cs[q] = 64;  // unused M row: never stored
+    }
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const T> xg = G(X);
+    gptr<T> yg = G(Y);
+    const T zero = T(0);
+
+    v4 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++) acc[nb] = v4{zero, zero, zero, zero};
+    int cnt = 0;  // stripes started in the current panel
+
+    auto flush = [&]() {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (cs[q] < cnt) {
+                const int64_t o = panel_out(b, seg_base + cs[q]) + cc[q];
+#pragma unroll
+                for (int nb = 0; nb < NB; nb++) {
+                    const int jj = nb * 16 + j;
+                    if (jj < nrhs) {
+                        gptr<T> yo = yg + o * syr + (int64_t)jj * syc;
+                        T v = alpha * acc[nb][q];
+                        if (rd_i) v = __builtin_fma(beta, *yo, v);
+                        *yo = v;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int nb = 0; nb < NB; nb++) acc[nb] = v4{zero, zero, zero, zero};
+    };
+
+    // Loads are unconditional (no divergent branches, so the waitcnt pass keeps them all in flight):
+    // the bin arrays carry kPanelTail padding rows, rows past the range are masked by value, and
+    // the keys of batch b+1 are prefetched while batch b is multiplied.
+    uint32_t kraw = __builtin_nontemporal_load(key + (size_t)g0 * 4 + lane);
+    for (int gb = g0; gb < g1; gb += kPanelBatch) {
+        const int ng = min(kPanelBatch, g1 - gb);
+        const uint32_t kv = lane < 4 * ng ? kraw : kPanelSentinel;
+        kraw = __builtin_nontemporal_load(key + (size_t)(gb + kPanelBatch) * 4 + lane);
+        const uint64_t hm = __ballot((kv & kHead) != 0);
+        T av[kPanelBatch], xv[kPanelBatch][NB];
+#pragma unroll
+        for (int q = 0; q < kPanelBatch; q++) {
+            const uint32_t rk = (uint32_t)__shfl((int)kv, 4 * q + kr, 64);
+            const size_t row = (size_t)(gb + q) * 4 + kr;
+            av[q] = __builtin_nontemporal_load(val + row * w + cola);
+            const bool ok = rk != kPanelSentinel;
+            const int64_t xr = ok ? (int64_t)(rk & ~kHead) * sxr : 0;
+#pragma unroll
+            for (int nb = 0; nb < NB; nb++) {
+                const int jj = nb * 16 + j;
+                const bool okj = ok && jj < nrhs;
+                const T t = xg[xr + (int64_t)(jj < nrhs ? jj : 0) * sxc];
+                xv[q][nb] = okj ? t : zero;
+            }
+        }
+        bool bad = false;
+#pragma unroll
+        for (int q = 0; q < kPanelBatch; q++)
+#pragma unroll
+            for (int nb = 0; nb < NB; nb++) bad = bad || !__builtin_isfinite(xv[q][nb]);
+        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(bad) != 0 || force_valu ? 1 : 0);
+        if (!any_bad) {
+#pragma unroll
+            for (int q = 0; q < kPanelBatch; q++) {
+                if (q < ng) {
+                    const uint32_t h4 = (uint32_t)(hm >> (4 * q)) & 0xFu;
+                    if ((h4 & 1u) && cnt == S) {  // first row of the next panel
+                        flush();
+                        seg_base += S;
+                        cnt = 0;
+                    }
+                    const int rseg = cnt - 1 + __builtin_popcount(h4 & ((2u << kr) - 1u));
+                    const T a = (arow && rseg == sa) ? av[q] : zero;
+#pragma unroll
+                    for (int nb = 0; nb < NB; nb++) acc[nb] = M::mma(a, xv[q][nb], acc[nb]);
+                    cnt += __builtin_popcount(h4);
+                }
+            }
+        } else {
+            // VALU, one row at a time: row k only feeds the accumulator rows of its own stripe
+            for (int q = 0; q < ng; q++) {
+                const uint32_t h4 = (uint32_t)(hm >> (4 * q)) & 0xFu;
+                if ((h4 & 1u) && cnt == S) {
+                    flush();
+                    seg_base += S;
+                    cnt = 0;
+                }
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t rk = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)kv, 4 * q + k, 64));
+                    if (rk == kPanelSentinel) continue;
+                    const int rs = cnt - 1 + __builtin_popcount(h4 & ((2u << k) - 1u));
+                    const size_t row = (size_t)(gb + q) * 4 + k;
+                    const int64_t xr = (int64_t)(rk & ~kHead) * sxr;
+#pragma unroll
+                    for (int reg = 0; reg < 4; reg++) {
+                        const T a = cs[reg] == rs ? val[row * w + cc[reg]] : zero;
+#pragma unroll
+                        for (int nb = 0; nb < NB; nb++) {
+                            const int jj = nb * 16 + j;
+                            const T xval = jj < nrhs ? xg[xr + (int64_t)jj * sxc] : zero;
+                            if (cs[reg] == rs) acc[nb][reg] = __builtin_fma(a, xval, acc[nb][reg]);
+                        }
+                    }
+                }
+                cnt += __builtin_popcount(h4);
+            }
+        }
+    }
+    flush();
+}
+
+// Y rows of the stripes that store no row (and belong to no panel): beta * Y or 0.
+template <typename T>
+__global__ __launch_bounds__(kBlockThreads) void fill_rows_mm(const int32_t *__restrict__ fill, int nfill, T *__restrict__ Y,
+                                                              int64_t syr, int64_t syc, int nrhs, T beta, int rd_i)
+{
+    const int64_t i = blockIdx.x * (int64_t)kBlockThreads + threadIdx.x;
+    if (i >= (int64_t)nfill * nrhs) return;
+    const int f = (int)(i / nrhs), jj = (int)(i - (int64_t)f * nrhs);
+    T *yo = Y + (int64_t)fill[f] * syr + (int64_t)jj * syc;
+    *yo = rd_i ? beta * *yo : T(0);
+}
+
+}  // namespace vbc

@@ -69,13 +69,15 @@ class _DeviceMatrix:
         self._handles = _Handles()
         self._finalizer = weakref.finalize(self, _Handles.release, self._handles)
 
-    def handle(self, device=0, trans=True):
-        flags = _L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD
+    def handle(self, device=0, trans=True, multi=False):
+        """libvbc handle for mul!(y, B', x) (trans), mul!(y, B, x), or -- multi=True -- the
+        matrix-core multi-RHS product Y = B'X (a separate panel layout, built on first use)."""
+        flags = _L.VBC_CREATE_MULTI if multi else (_L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD)
         return self._handles.get((int(device), flags), lambda out: self._create(out, int(device), flags))
 
-    def info(self, device=0, trans=True):
+    def info(self, device=0, trans=True, multi=False):
         inf = _L.vbc_info()
-        _L.check(_L.lib().vbc_get_info(self.handle(device, trans), C.byref(inf)), "info")
+        _L.check(_L.lib().vbc_get_info(self.handle(device, trans, multi), C.byref(inf)), "info")
         return {f: getattr(inf, f) for f, _ in _L.vbc_info._fields_}
 
     def release(self):

@@ -61,13 +61,13 @@ def _check_vec(a, dtype, name):
         raise _L.ArgumentError(f"{name} must be contiguous (StridedVector with stride 1)")
 
 
-def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None):
-    """LinearAlgebra.mul!(y, A, x, α, β); returns y."""
+def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None, engine="auto"):
+    """LinearAlgebra.mul!(y, A, x, α, β); returns y.  Matrix x / y go to mulmat_ (engine)."""
     B, trans = _unwrap(A)
     if not isinstance(B, _DeviceMatrix):
         raise TypeError(f"mul_ expects SparseMatrix1DVBC / SparseMatrixVBC / SparseMatrixCSC, got {type(B)}")
     if len(y.shape) != 1 or len(x.shape) != 1:
-        return mulmat_(y, A, x, alpha, beta, stream=stream, quirks=quirks)
+        return mulmat_(y, A, x, alpha, beta, stream=stream, quirks=quirks, engine=engine)
     mem, dev, stream = _mem_device_stream(x, y, stream)
     if device is not None and mem == _L.VBC_MEM_HOST:
         dev = device
@@ -99,10 +99,14 @@ def _layout(M):
     raise _L.ArgumentError("matrix operands must be row-major or column-major with unit inner stride")
 
 
-def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False):
+MFMA_MIN_RHS = 2
+
+
+def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="auto"):
     """Multi-RHS Y = α·op(A)·X + β·Y (column-by-column semantics; the reference has no matrix
-    mul!).  Row-major X / Y (right-hand sides contiguous) use the fused multi-RHS kernel for B'X;
-    column-major (Julia) operands run one SpMV per column."""
+    mul!).  engine="mfma" (default for B'X with >= MFMA_MIN_RHS columns): the matrix-core panel
+    product, row- or column-major operands; engine="vector": the SpMV layout (fused vector kernel for
+    row-major B'X, one SpMV per column otherwise)."""
     B, trans = _unwrap(A)
     mem, dev, stream = _mem_device_stream(X, Y, stream)
     _check_dtype(X, B.dtype, "X")
@@ -118,7 +122,12 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False):
     if lx != ly:
         raise _L.ArgumentError("X and Y must have the same layout")
     nrhs = X.shape[1]
-    h = B.handle(dev, trans)
+    if engine not in ("auto", "mfma", "vector"):
+        raise _L.ArgumentError(f"engine must be 'auto', 'mfma' or 'vector', got {engine!r}")
+    if engine == "mfma" and not trans:
+        raise _L.ArgumentError("the matrix-core engine computes B'X (pass an adjoint)")
+    mfma = trans and (engine == "mfma" or (engine == "auto" and nrhs >= MFMA_MIN_RHS))
+    h = B.handle(dev, trans, multi=mfma)
     flags = (_L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0) | (_L.VBC_MAT_ROWMAJOR if lx == "R" else 0)
     _L.check(_L.lib().vbc_mul_mat(h, int(trans), nrhs, _L.ptr(X), max(ldx, 1), X.shape[0], _L.ptr(Y),
                                   max(ldy, 1), Y.shape[0], float(alpha), float(beta), mem, stream, flags),

@@ -8,7 +8,7 @@ matrix (constructors_1DVBC.jl:9-92), without materialising the CSC.
 """
 import numpy as np
 
-from .matrices import SparseMatrix1DVBC, _simd_pad
+from .matrices import SparseMatrix1DVBC, SparseMatrixVBC, _simd_pad
 from .partition import SplitPartition
 
 
@@ -90,3 +90,41 @@ def fe_grid_2d(N, dof=2, W=8, dtype=np.float64, seed=0xDEADBEEF):
     val[:nv] = rng.random(nv, dtype=np.float64 if dtype == np.float64 else np.float32)
     m = nodes * dof
     return SparseMatrix1DVBC(W, m, m, SplitPartition(spl), pos, rows + 1, ofs, val)
+
+
+def vbr_2d(K, L, q, u, w, U=None, W=None, dtype=np.float32, seed=0xDEADBEEF, pad=True):
+    """The reference's 2D VBR generator (costs.jl:200-220): q distinct (block row k, stripe l) pairs
+    drawn uniformly from K x L, each a dense u x w tile of rand(Tv); m = u*K, n = w*L.  Fields are
+    produced directly in the SparseMatrixVBC{U,W} layout (constructors_VBC.jl:95-105: per stripe,
+    blocks in ascending k, tile row-major, idx = block-row id) -- what
+    SparseMatrixVBC{U,W}(A, pack_stripe(A', EquiChunker(u)), pack_stripe(A, EquiChunker(w))) holds."""
+    U = u if U is None else U
+    W = w if W is None else W
+    rng = np.random.default_rng(seed)
+    keys = np.unique(rng.integers(0, np.int64(K) * L, size=int(q), dtype=np.int64))  # sorted by (l, k)
+    stripe = keys // K
+    krow = keys - stripe * K
+    counts = np.bincount(stripe, minlength=L).astype(np.int64)
+    pspl = 1 + np.arange(K + 1, dtype=np.int64) * u
+    spl = 1 + np.arange(L + 1, dtype=np.int64) * w
+    pos = np.empty(L + 1, np.int64)
+    pos[0] = 1
+    np.cumsum(counts, out=pos[1:])
+    pos[1:] += 1
+    ofs = 1 + np.concatenate([[0], np.cumsum(counts * (u * w))]).astype(np.int64)
+    nv = int(ofs[-1] - 1)
+    padn = _simd_pad(W, dtype) if pad else 0
+    val = np.empty(nv + padn, dtype)
+    val[:nv] = rng.random(nv, dtype=np.float64 if dtype == np.float64 else np.float32)
+    val[nv:] = 0
+    return SparseMatrixVBC(U, W, u * K, w * L, SplitPartition(pspl), SplitPartition(spl), pos, krow + 1, ofs, val)
+
+
+def c5(dtype=np.float32, scale=1.0, u=8, w=8, seed=0xDEADBEEF):
+    """Config C5 (BASELINE.json): 2D SparseMatrixVBC, dense u x w tiles, for the 16-RHS product.
+    Full size: K = L = 2^18 block rows / stripes (m = n = 2,097,152 at u = w = 8), 6 tiles per stripe
+    on average (q = 1,572,864) -> 1.0e8 stored values."""
+    K = max(4, int(round(2 ** 18 * scale)))
+    L = max(4, int(round(2 ** 18 * scale * 8 / w)))
+    q = int(round(6 * L * 64 / (u * w)))
+    return vbr_2d(K, L, q, u, w, dtype=dtype, seed=seed)

@@ -1,0 +1,175 @@
+"""GPU parity of the matrix-core multi-RHS product Y = α·B'X + β·Y (vbc_panel.h, VBC_CREATE_MULTI).
+
+The reference has no matrix mul! (multiply_1DVBC.jl:184-185), so parity is column by column against
+the oracle's transposed products (multiply_1DVBC.jl:90-134, multiply_VBC.jl:93-147).  Tolerances as
+test_gpu_parity.py: one-hot probes bit-exact; random X normwise 1e-12 (fp64) / 1e-5 (fp32 vs the
+fp64 product).
+"""
+import numpy as np
+import pytest
+
+import sparsematrixvbcs_amd as V
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+DEV = "cuda:0"
+TOL64, TOL32 = 1e-12, 1e-5
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    d = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (d if d else 1.0)
+
+
+def as_dev(M, layout):
+    """Device copy of M in row-major ("R") or column-major ("C") storage."""
+    if layout == "R":
+        return torch.from_numpy(np.ascontiguousarray(M)).to(DEV)
+    return torch.from_numpy(np.ascontiguousarray(M.T)).to(DEV).T
+
+
+def ref_cols(R, X, Y0, alpha, beta):
+    """Oracle B'X + β Y0, one transposed product per column, in fp64."""
+    Rd = R
+    if R.val.dtype != np.float64:
+        Rd = type(R).__new__(type(R))
+        Rd.__dict__.update(R.__dict__)
+        Rd.val = R.val.astype(np.float64)
+    return np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64),
+                           np.ascontiguousarray(Y0[:, j], dtype=np.float64), alpha, beta, trans=True,
+                           ref_semantics=False) for j in range(X.shape[1])], axis=1)
+
+
+def ref_1d(B):
+    return O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+
+
+def ref_2d(B):
+    return O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+
+
+def test_golden_one_hot_mfma(golden):
+    """Every matrix of test/matrices.jl as 1DVBC and 2D VBC: identity blocks of 16 columns through
+    the panel product give exactly the rows of A (runtests.jl:63-87 protocol, 16 at a time)."""
+    for key, g in golden.items():
+        A = g["A"]
+        m, n = A.shape
+        D = A.toarray()
+        mats = [V.SparseMatrix1DVBC[4](A, V.StrictChunker(4)),
+                V.SparseMatrixVBC[4, 4](A, V.AlternatingPacker(V.StrictChunker(4), V.StrictChunker(4)))]
+        for B in mats:
+            for layout in ("R", "C"):
+                for j0 in range(0, m, 16):
+                    k = min(16, m - j0)
+                    X = np.zeros((m, k))
+                    X[np.arange(j0, j0 + k), np.arange(k)] = 1.0
+                    Y = as_dev(np.full((n, k), np.nan), layout)
+                    V.mul_(Y, B.T, as_dev(X, layout), engine="mfma")
+                    assert np.array_equal(Y.cpu().numpy(), D[j0:j0 + k, :].T), (key, type(B).__name__, layout)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("nrhs", [1, 2, 5, 16, 17, 33, 64, 70])
+def test_mfma_1dvbc_random(nrhs, dtype):
+    """Widths 1..16 (every panel packing S = 16/w), a w > 16 stripe (cut into 16-column pieces),
+    empty stripes (fill list), alpha/beta, row- and column-major operands vs the oracle."""
+    tol = TOL64 if dtype == np.float64 else TOL32
+    rng = np.random.default_rng(100 + nrhs)
+    for widths, q in ((list(range(1, 17)), 2000), ([2], 100), ([16], 900), ([1, 20, 7, 33], 150)):
+        L = 60
+        w = np.array([widths[i % len(widths)] for i in range(L)])
+        B = V.synthetic.vbr_1dvbc(900, L, q, w, W=40, dtype=dtype, seed=nrhs * 7 + int(w.sum()))
+        if q <= 150:
+            assert (np.diff(B.pos) == 0).any()  # some stripes empty: the fill list writes them
+        R = ref_1d(B)
+        for layout in ("R", "C"):
+            X = rng.uniform(-1, 1, (B.m, nrhs)).astype(dtype)
+            Y0 = rng.uniform(-1, 1, (B.n, nrhs)).astype(dtype)
+            for alpha, beta in ((1.0, 0.0), (1.5, 0.5), (-2.0, 1.0)):
+                Yd = as_dev(Y0, layout)
+                V.mul_(Yd, B.T, as_dev(X, layout), alpha, beta, engine="mfma")
+                assert rel(Yd.cpu().numpy(), ref_cols(R, X, Y0, alpha, beta)) <= tol, (widths, layout, alpha, beta)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("uw", [(8, 8), (4, 16), (16, 4), (3, 5), (1, 1)])
+def test_mfma_vbc2d_random(uw, dtype):
+    """C5 shape at small size: 2D VBC u x w tiles (costs.jl:200-220 generator), 16 RHS."""
+    u, w = uw
+    tol = TOL64 if dtype == np.float64 else TOL32
+    B = V.synthetic.vbr_2d(40, 30, 200, u, w, dtype=dtype, seed=u * 31 + w)
+    R = ref_2d(B)
+    rng = np.random.default_rng(u + w)
+    X = rng.uniform(-1, 1, (B.m, 16)).astype(dtype)
+    Y0 = rng.uniform(-1, 1, (B.n, 16)).astype(dtype)
+    for layout in ("R", "C"):
+        Yd = as_dev(Y0, layout)
+        V.mul_(Yd, B.T, as_dev(X, layout), 1.0, 0.25, engine="mfma")
+        assert rel(Yd.cpu().numpy(), ref_cols(R, X, Y0, 1.0, 0.25)) <= tol, layout
+
+
+def test_mfma_matches_vector_engine_and_is_deterministic():
+    """Same product through the matrix-core and the vector engines; repeated runs bitwise equal."""
+    B = V.synthetic.vbr_1dvbc(5000, 900, 20000, np.arange(900) % 8 + 1, W=8, dtype=np.float64, seed=3)
+    X = torch.rand((B.m, 16), dtype=torch.float64, device=DEV)
+    Y1 = torch.empty((B.n, 16), dtype=torch.float64, device=DEV)
+    Y2 = torch.empty_like(Y1)
+    Y3 = torch.empty_like(Y1)
+    V.mul_(Y1, B.T, X, engine="mfma")
+    V.mul_(Y2, B.T, X, engine="vector")
+    V.mul_(Y3, B.T, X, engine="mfma")
+    assert rel(Y1.cpu().numpy(), Y2.cpu().numpy()) <= 1e-13
+    assert torch.equal(Y1, Y3)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_mfma_nonfinite_confined_to_own_stripe(dtype):
+    """An Inf / NaN in X reaches exactly the columns whose stripes store that row (as in the
+    reference's per-stripe loop), never the other stripes sharing its panel."""
+    B = V.synthetic.vbr_1dvbc(300, 64, 600, 2, W=2, dtype=dtype, seed=11)
+    R = ref_1d(B)
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-1, 1, (B.m, 16)).astype(dtype)
+    X[17, 3] = np.inf
+    X[101, 0] = np.nan
+    X[250, 9] = -np.inf
+    Yd = as_dev(np.zeros((B.n, 16), dtype), "R")
+    V.mul_(Yd, B.T, as_dev(X, "R"), engine="mfma")
+    got = Yd.cpu().numpy()
+    ref = ref_cols(R, X, np.zeros((B.n, 16), dtype), 1.0, 0.0)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    assert rel(got[fin], ref[fin]) <= (TOL64 if dtype == np.float64 else TOL32)
+
+
+def test_mfma_quirks_and_errors():
+    """Reference α/β quirks (transposed overwrites y) and the boundary errors of vbc_mul_mat."""
+    B = V.synthetic.vbr_1dvbc(200, 40, 300, 4, W=4, seed=2)
+    R = ref_1d(B)
+    X = np.random.default_rng(0).uniform(-1, 1, (B.m, 8))
+    Y0 = np.ones((B.n, 8))
+    Yd = as_dev(Y0, "R")
+    V.mul_(Yd, B.T, as_dev(X, "R"), 3.0, 2.0, quirks=True, engine="mfma")
+    assert rel(Yd.cpu().numpy(), ref_cols(R, X, Y0, 1.0, 0.0)) <= TOL64
+    with pytest.raises(V.DimensionMismatch):
+        V.mul_(torch.zeros((B.n + 1, 8), dtype=torch.float64, device=DEV), B.T, as_dev(X, "R"), engine="mfma")
+    with pytest.raises(V.ArgumentError):
+        V.mul_(torch.zeros((B.m, 8), dtype=torch.float64, device=DEV), B, as_dev(np.zeros((B.n, 8)), "R"),
+               engine="mfma")
+
+
+def test_mfma_host_memory_and_info():
+    """numpy operands (staged through HBM) and the panel layout's vbc_info fields."""
+    B = V.synthetic.vbr_2d(20, 20, 80, 4, 4, dtype=np.float64, seed=9)
+    R = ref_2d(B)
+    X = np.random.default_rng(1).uniform(-1, 1, (B.m, 16))
+    Y = np.zeros((B.n, 16))
+    V.mul_(Y, B.T, X, engine="mfma")
+    assert rel(Y, ref_cols(R, X, np.zeros((B.n, 16)), 1.0, 0.0)) <= TOL64
+    inf = B.info(multi=True)
+    assert inf["bins_m"] == 1 and inf["bins_t"] == 0 and inf["bytes_m"] > 0

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--trans", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--nrhs", type=int, default=0, help=">0: time the multi-RHS product (row-major X / Y)")
     args = ap.parse_args()
     import torch
 
@@ -34,35 +35,46 @@ def main():
     from sparsematrixvbcs_amd import _lib as L
 
     dtype = np.float64 if args.dtype == "f64" else np.float32
-    if args.workload == "fe":
+    if args.workload == "c5":
+        B = V.synthetic.c5(dtype=dtype, scale=args.scale)
+    elif args.workload == "fe":
         B = V.synthetic.fe_grid_2d(int(round(2236 * args.scale ** 0.5)), dof=2, dtype=dtype)
     else:
         B = V.synthetic.north_star(dtype=dtype, scale=args.scale, mixed=(args.workload == "ns-mixed"))
     esz = np.dtype(dtype).itemsize
-    nbytes = bench.algorithmic_bytes(B, esz)
     trans = bool(args.trans)
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
-    x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, nx).astype(dtype)).cuda()
+    k = max(args.nrhs, 1)
+    nbytes = bench.algorithmic_bytes(B, esz) + (k - 1) * esz * (B.m + B.n) if args.workload != "c5" else \
+        (len(B.val) * esz + 4 * len(B.idx) + (k * esz) * (B.m + B.n))
+    x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, (nx, k) if args.nrhs else nx).astype(dtype)).cuda()
     variants = [v for v in args.variants.split(";")]
     handles = []
     for v in variants:
         saved = dict(os.environ)
         for kv in v.split(","):
             if "=" in kv:
-                k, val = kv.split("=", 1)
-                os.environ[k.strip()] = val.strip()
+                ek, ev_ = kv.split("=", 1)
+                os.environ[ek.strip()] = ev_.strip()
         hp = C.c_void_p()
-        L.check(B._create(C.byref(hp), 0, L.VBC_CREATE_TRANSPOSED if trans else L.VBC_CREATE_FORWARD), "create")
+        flags = L.VBC_CREATE_TRANSPOSED if trans else L.VBC_CREATE_FORWARD
+        if "@multi" in v:  # matrix-core panel layout (multi-RHS transposed product)
+            flags = L.VBC_CREATE_MULTI
+        L.check(B._create(C.byref(hp), 0, flags), "create")
         os.environ.clear()
         os.environ.update(saved)
         handles.append(hp)
-    ys = [torch.empty(ny, dtype=x.dtype, device="cuda") for _ in variants]
+    ys = [torch.empty((ny, k) if args.nrhs else ny, dtype=x.dtype, device="cuda") for _ in variants]
     stream = torch.cuda.current_stream()
     lib = L.lib()
 
     def run(i):
-        L.check(lib.vbc_mul(handles[i], int(trans), x.data_ptr(), nx, ys[i].data_ptr(), ny, 1.0, 0.0,
-                            L.VBC_MEM_DEVICE, stream.cuda_stream, 0), "mul")
+        if args.nrhs:
+            L.check(lib.vbc_mul_mat(handles[i], int(trans), k, x.data_ptr(), k, nx, ys[i].data_ptr(), k, ny,
+                                    1.0, 0.0, L.VBC_MEM_DEVICE, stream.cuda_stream, L.VBC_MAT_ROWMAJOR), "mul_mat")
+        else:
+            L.check(lib.vbc_mul(handles[i], int(trans), x.data_ptr(), nx, ys[i].data_ptr(), ny, 1.0, 0.0,
+                                L.VBC_MEM_DEVICE, stream.cuda_stream, 0), "mul")
 
     for i in range(len(variants)):
         for _ in range(3):
@@ -82,7 +94,8 @@ def main():
     for i, v in enumerate(variants):
         t = np.array(times[i])
         d = (ys[i].double() - ref).norm().item() / max(ref.norm().item(), 1e-300)
-        print(f"{v:40s} median {np.median(t)*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
+        flops = 2.0 * len(B.val) * k / (np.median(t) * 1e-3) / 1e12
+        print(f"{v:40s} {flops:6.2f} TFLOP/s median {np.median(t)*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
               f"{nbytes / (np.median(t) * 1e-3) / 1e9:7.0f} GB/s  rel-diff-vs-first {d:.2e}", flush=True)
     for hp in handles:
         lib.vbc_destroy(hp)
