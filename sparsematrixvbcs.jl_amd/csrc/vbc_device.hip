@@ -95,6 +95,8 @@ struct vbc_handle {
     int64_t bytes_m = 0;          // matrix bytes one panel product streams
     int target_ranges_m = 4096;
     int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA (ablation / debugging)
+    int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
+    int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::Launch lt;               // transposed product: all buckets in one launch
     std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
     bool f_scale = false;         // forward with several buckets: scale y by beta first
@@ -361,6 +363,7 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
             pp.b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * pp.b.out_stride;
         const int64_t Rp = acc * 4;
         const int64_t Ra = Rp + kPanelTail;  // over-read padding (vbc_panel.h)
+        h->panel_val_bytes = std::max<int64_t>(h->panel_val_bytes, Ra * w * esz);
         pp.o_key = ar.reserve(Ra * 4);
         pp.o_val = ar.reserve(Ra * w * esz);
         pp.o_out = ar.reserve(out.size() * 4);
@@ -519,11 +522,12 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
     if (flags & VBC_CREATE_MULTI) {
         int om = 0;
-        if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1>, kBlockThreads, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<float, 1>, kBlockThreads, 0);
+        if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1, true>, kBlockThreads, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<float, 1, true>, kBlockThreads, 0);
         h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
         if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
         if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
+        if (const char *e = getenv("VBC_PANEL_NOBUF")) h->panel_nobuf = atoi(e) != 0;
     }
 
     Arena ar;
@@ -727,12 +731,23 @@ static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_
         T *ys = reinterpret_cast<T *>(Y) + c0 * syc;
         if (L.total_ranges > 0) {
             const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
-#define VBC_PANEL(NB)                                                                                     \
-    hipLaunchKernelGGL((spmm_panel<T, NB>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(), \
-                       L.total_ranges, xs, sxr, sxc, ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu)
-            if (nr <= 16) VBC_PANEL(1);
-            else if (nr <= 32) VBC_PANEL(2);
-            else VBC_PANEL(4);
+            // byte extent of X as read by this chunk: rows 0..m-1, columns 0..nr-1
+            const int64_t span = ((h->m - 1) * sxr + (int64_t)(nr - 1) * sxc + 1) * (int64_t)sizeof(T);
+            const bool buf = span + 64 * sxc * (int64_t)sizeof(T) < (int64_t(1) << 31) &&
+                             h->panel_val_bytes < (int64_t(1) << 31) && !h->panel_nobuf;
+            const uint32_t xb = (uint32_t)span;
+#define VBC_PANEL(NB, BUF)                                                                                    \
+    hipLaunchKernelGGL((spmm_panel<T, NB, BUF>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(), \
+                       L.total_ranges, xs, sxr, sxc, xb, ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu)
+            if (buf) {
+                if (nr <= 16) VBC_PANEL(1, true);
+                else if (nr <= 32) VBC_PANEL(2, true);
+                else VBC_PANEL(4, true);
+            } else {
+                if (nr <= 16) VBC_PANEL(1, false);
+                else if (nr <= 32) VBC_PANEL(2, false);
+                else VBC_PANEL(4, false);
+            }
 #undef VBC_PANEL
             VBC_HIP(hipGetLastError());
         }

@@ -40,6 +40,10 @@ __device__ __forceinline__ gptr<T> G(T *p) { return (gptr<T>)p; }
 template <typename T>
 __device__ __forceinline__ gptr<const T> G(const T *p) { return (gptr<const T>)p; }
 
+// Fused multiply-add in T (__builtin_fma is the double version: on floats it would widen).
+__device__ __forceinline__ float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fmadd(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
 // One width bucket of a fused launch (read through the scalar cache).
 struct Bin {
     int32_t kind;     // 0: B'x, 1: Bx
@@ -159,7 +163,7 @@ __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int
 #pragma unroll
         for (int e = 0; e < V; e++) {
             T r = alpha * v[e];
-            if (rd) r = __builtin_fma(beta, yo[e], r);
+            if (rd) r = fmadd(beta, yo[e], r);
             yo[e] = r;
         }
     } else {
@@ -167,7 +171,7 @@ __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int
         if (sub == 0) {
             gptr<T> yo = G(y) + out_of(b, seg);
             T r = alpha * s;
-            if (rd) r = __builtin_fma(beta, *yo, r);
+            if (rd) r = fmadd(beta, *yo, r);
             *yo = r;
         }
     }
@@ -324,7 +328,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
                 for (int e = 0; e < V; e++) cur[e] = T(0);
             }
 #pragma unroll
-            for (int e = 0; e < V; e++) cur[e] = __builtin_fma(v[k][e], xv[k][KIND == 0 ? 0 : e], cur[e]);
+            for (int e = 0; e < V; e++) cur[e] = fmadd(v[k][e], xv[k][KIND == 0 ? 0 : e], cur[e]);
         }
         if (!seen) {
 #pragma unroll
@@ -556,7 +560,7 @@ __device__ __forceinline__ void run_range_mm(const Bin &b, int r, int lane, cons
         for (int c = 0; c < W_; c++) {
             gptr<T> yo = yg + (int64_t)(o + c) * ldy + j;
             T q = alpha * v[c];
-            if (rd) q = __builtin_fma(beta, *yo, q);
+            if (rd) q = fmadd(beta, *yo, q);
             *yo = q;
         }
     };
@@ -619,7 +623,7 @@ __device__ __forceinline__ void run_range_mm(const Bin &b, int r, int lane, cons
                     for (int c = 0; c < W_; c++) cur[c] = T(0);
                 }
 #pragma unroll
-                for (int c = 0; c < W_; c++) cur[c] = __builtin_fma(vv[k][c], xv[k], cur[c]);
+                for (int c = 0; c < W_; c++) cur[c] = fmadd(vv[k][c], xv[k], cur[c]);
             }
             if (!seen) {
 #pragma unroll
@@ -739,7 +743,7 @@ __global__ __launch_bounds__(kBlockThreads) void fixup_mm(const Bin *__restrict_
             T s = T(0);
             for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++) s += cm[((size_t)q * b.w + c) * NR + j];
             T *yo = y + (int64_t)(o + c) * ldy + j;
-            *yo = __builtin_fma(alpha, s, *yo);
+            *yo = fmadd(alpha, s, *yo);
         }
     } else if (item - total_ranges < nfill) {
         T *yo = y + (int64_t)fill[item - total_ranges] * ldy + j;
@@ -768,7 +772,7 @@ __global__ __launch_bounds__(kBlockThreads) void fixup(const Bin *__restrict__ b
             T s = T(0);
             for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++)
                 s += static_cast<const T *>(b.carry)[(size_t)q * wc + c];
-            yo[c] = __builtin_fma(alpha, s, yo[c]);
+            yo[c] = fmadd(alpha, s, yo[c]);
         }
     } else if (i - total_ranges < nfill) {
         T *yo = y + fill[i - total_ranges];

@@ -75,35 +75,55 @@ __device__ __forceinline__ int panel_out(const PanelBin &b, int seg)
     return b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
 }
 
-// kBatch groups (4 rows each) are loaded before any of them is multiplied: one coalesced key load
-// per 64 rows, then every val and X load of the batch in flight together.
+// kPanelBatch groups (4 rows each) are loaded before any of them is multiplied: one coalesced key
+// load per 64 rows, then every val and X load of the batch in flight together.
 constexpr int kPanelBatch = 16;
 constexpr int kPanelTail = 8 * kPanelBatch;  // padding rows after each bin (batch over-read + key prefetch)
 
-template <typename T, int NB>
+// Raw buffer loads (32-bit offsets, hardware bounds check) for operands below 4 GiB.
+template <typename T>
+__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff);
+template <>
+__device__ __forceinline__ float buf_load<float>(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+}
+template <>
+__device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+
+// BUF: X and the bins' val are addressed by 32-bit offsets through buffer descriptors (the host picks
+// it when both, plus the column offsets, stay below 2 GiB); otherwise 64-bit global addresses.
+template <typename T, int NB, bool BUF>
 __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__restrict__ bins, int nbins,
                                                             int total_ranges, const T *__restrict__ X, int64_t sxr,
-                                                            int64_t sxc, T *__restrict__ Y, int64_t syr, int64_t syc,
-                                                            int nrhs, T alpha, T beta, int rd_i, int force_valu)
+                                                            int64_t sxc, uint32_t xbytes, T *__restrict__ Y,
+                                                            int64_t syr, int64_t syc, int nrhs, T alpha, T beta,
+                                                            int rd_i, int force_valu)
 {
     using M = MfmaAcc<T>;
     typedef typename M::v4 v4;
-    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    __shared__ uint32_t xch[kWavesPerBlock][64][2];  // per wave: {X row offset, stripe-in-panel} of 64 rows
+    const int wv = threadIdx.x >> 6;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + wv));
     if (rg >= total_ranges) return;
     int bi = 0;
     while (bi + 1 < nbins && bins[bi + 1].range0 <= rg) bi++;
     const PanelBin b = bins[bi];
     const int r = rg - b.range0;
-    const int g0 = b.rgrp[r], g1 = b.rgrp[r + 1];
+    const int g0 = __builtin_amdgcn_readfirstlane(b.rgrp[r]), g1 = __builtin_amdgcn_readfirstlane(b.rgrp[r + 1]);
     if (g0 >= g1) return;
-    int seg_base = b.rseg[r];
+    int seg_base = __builtin_amdgcn_readfirstlane(b.rseg[r]);
     const int lane = threadIdx.x & 63;
     const int w = b.w, S = b.S;
+    constexpr int esz = (int)sizeof(T);
     // A operand: M row c = lane & 15 (stripe c / w of the panel, column c % w), k = lane >> 4.
     const int ca = lane & 15, kr = lane >> 4;
-    const int sa = ca / w, cola = ca - sa * w;
-    const bool arow = sa < S;
-    // B operand / C column: right-hand side j = lane & 15.
+    const int sa = ca / w, cola = ca - sa * w;  // sa >= S: unused M row, never matches a stripe
+    // B operand / C column: right-hand side j = lane & 15 (columns >= nrhs read a valid column and
+    // only feed C columns that are never stored).
     const int j = lane & 15;
     // C rows held by this lane: stripe and column for each of the 4 accumulator registers.
     int cs[4], cc[4];
@@ -114,16 +134,33 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
         cc[q] = c - cs[q] * w;
         if (cs[q] >= S) cs[q] = 64;  // unused M row: never stored
     }
+    uint32_t jofs[NB];
+    int64_t jofs64[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++) {
+        const int jc = min(nb * 16 + j, nrhs - 1);
+        jofs64[nb] = (int64_t)jc * sxc;
+        jofs[nb] = (uint32_t)(jofs64[nb] * esz);
+    }
+    const uint32_t sxr_b = (uint32_t)(sxr * esz);
     const gptr<const uint32_t> key = G(b.key);
     const gptr<const T> val = G(static_cast<const T *>(b.val));
     const gptr<const T> xg = G(X);
     gptr<T> yg = G(Y);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(X), 0, (int)xbytes, 0x00020000);
+    // the bin's val pointer comes from memory: make its wave-uniformity explicit (no waterfall loop)
+    const uint64_t vp = (uint64_t)(uintptr_t)b.val;
+    const uint64_t vpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(vp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vp);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)vpu, 0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t voff_lane = (uint32_t)((kr * w + cola) * esz);  // val offset of this lane's A element in a group
     const T zero = T(0);
 
     v4 acc[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; nb++) acc[nb] = v4{zero, zero, zero, zero};
-    int cnt = 0;  // stripes started in the current panel
+    int cnt = 0;   // stripes started in the current panel
+    int segc = 0;  // stripes started in this range before the current batch
 
     auto flush = [&]() {
 #pragma unroll
@@ -136,7 +173,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
                     if (jj < nrhs) {
                         gptr<T> yo = yg + o * syr + (int64_t)jj * syc;
                         T v = alpha * acc[nb][q];
-                        if (rd_i) v = __builtin_fma(beta, *yo, v);
+                        if (rd_i) v = fmadd(beta, *yo, v);
                         *yo = v;
                     }
                 }
@@ -155,28 +192,49 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
         const uint32_t kv = lane < 4 * ng ? kraw : kPanelSentinel;
         kraw = __builtin_nontemporal_load(key + (size_t)(gb + kPanelBatch) * 4 + lane);
         const uint64_t hm = __ballot((kv & kHead) != 0);
+        // per row (lane = row of the batch): X offset and stripe index within its panel
+        {
+            const int hc = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)) +
+                           (int)(kv >> 31);
+            const int gseg = segc + hc - 1;  // range-relative stripe of this row (ranges start at panels)
+            const bool ok = kv != kPanelSentinel;
+            const uint32_t xo = ok ? (kv & ~kHead) * sxr_b : xbytes;  // past X: the buffer load returns 0
+            xch[wv][lane][0] = xo;
+            xch[wv][lane][1] = (uint32_t)(gseg - (gseg / S) * S);
+        }
         T av[kPanelBatch], xv[kPanelBatch][NB];
+        uint32_t rsv[kPanelBatch];
 #pragma unroll
         for (int q = 0; q < kPanelBatch; q++) {
-            const uint32_t rk = (uint32_t)__shfl((int)kv, 4 * q + kr, 64);
-            const size_t row = (size_t)(gb + q) * 4 + kr;
-            av[q] = __builtin_nontemporal_load(val + row * w + cola);
-            const bool ok = rk != kPanelSentinel;
-            const int64_t xr = ok ? (int64_t)(rk & ~kHead) * sxr : 0;
+            const uint32_t xo = xch[wv][4 * q + kr][0];
+            rsv[q] = xch[wv][4 * q + kr][1];
+            if constexpr (BUF) {
+                av[q] = buf_load<T>(vrs, voff_lane + (uint32_t)(q * 4 * w * esz), (uint32_t)((size_t)gb * 4 * w * esz));
 #pragma unroll
-            for (int nb = 0; nb < NB; nb++) {
-                const int jj = nb * 16 + j;
-                const bool okj = ok && jj < nrhs;
-                const T t = xg[xr + (int64_t)(jj < nrhs ? jj : 0) * sxc];
-                xv[q][nb] = okj ? t : zero;
+                for (int nb = 0; nb < NB; nb++) xv[q][nb] = buf_load<T>(xrs, xo + jofs[nb], 0u);
+            } else {
+                const size_t row = (size_t)(gb + q) * 4 + kr;
+                av[q] = __builtin_nontemporal_load(val + row * w + cola);
+                const uint32_t rk = (uint32_t)__shfl((int)kv, 4 * q + kr, 64);
+                const bool ok = rk != kPanelSentinel;
+                const int64_t xr = ok ? (int64_t)(rk & ~kHead) * sxr : 0;
+#pragma unroll
+                for (int nb = 0; nb < NB; nb++) {
+                    const T t = xg[xr + jofs64[nb]];
+                    xv[q][nb] = ok ? t : zero;
+                }
             }
         }
-        bool bad = false;
+        // an Inf / NaN among the gathered X: x * 0 is NaN exactly for non-finite x (val is folded in
+        // too, which keeps its loads ahead of this wait; a non-finite val only costs the VALU path)
+        T chk = zero;
 #pragma unroll
-        for (int q = 0; q < kPanelBatch; q++)
+        for (int q = 0; q < kPanelBatch; q++) {
+            chk = fmadd(av[q], zero, chk);
 #pragma unroll
-            for (int nb = 0; nb < NB; nb++) bad = bad || !__builtin_isfinite(xv[q][nb]);
-        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(bad) != 0 || force_valu ? 1 : 0);
+            for (int nb = 0; nb < NB; nb++) chk = fmadd(xv[q][nb], zero, chk);
+        }
+        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(chk != chk) != 0 || force_valu ? 1 : 0);
         if (!any_bad) {
 #pragma unroll
             for (int q = 0; q < kPanelBatch; q++) {
@@ -187,8 +245,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
                         seg_base += S;
                         cnt = 0;
                     }
-                    const int rseg = cnt - 1 + __builtin_popcount(h4 & ((2u << kr) - 1u));
-                    const T a = (arow && rseg == sa) ? av[q] : zero;
+                    const T a = (int)rsv[q] == sa ? av[q] : zero;
 #pragma unroll
                     for (int nb = 0; nb < NB; nb++) acc[nb] = M::mma(a, xv[q][nb], acc[nb]);
                     cnt += __builtin_popcount(h4);
@@ -216,13 +273,14 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
                         for (int nb = 0; nb < NB; nb++) {
                             const int jj = nb * 16 + j;
                             const T xval = jj < nrhs ? xg[xr + (int64_t)jj * sxc] : zero;
-                            if (cs[reg] == rs) acc[nb][reg] = __builtin_fma(a, xval, acc[nb][reg]);
+                            if (cs[reg] == rs) acc[nb][reg] = fmadd(a, xval, acc[nb][reg]);
                         }
                     }
                 }
                 cnt += __builtin_popcount(h4);
             }
         }
+        segc += __builtin_popcountll(hm);
     }
     flush();
 }
