@@ -14,6 +14,10 @@
 #ifndef VBC_H
 #define VBC_H
 
+#ifndef VBC_API
+#define VBC_API __attribute__((visibility("default")))  /* the library builds with -fvisibility=hidden */
+#endif
+
 #include <stddef.h>
 #include <stdint.h>
 
@@ -70,23 +74,23 @@ typedef struct vbc_handle vbc_handle; /* opaque; immutable after create */
  * spl[L+1] = Φ.spl, pos[L+1], idx[pos[L+1]-1], ofs[L+1]: 1-based Int64.  val has nval >=
  * ofs[L+1]-1 elements (the reference's SIMD tail pad, constructors_1DVBC.jl:35-39, is ignored).
  * `device` is the HIP ordinal; `flags` selects which product layouts to build (0 = transposed). */
-int vbc1d_create(vbc_handle **out, int64_t m, int64_t n, int64_t W, int64_t L, const int64_t *spl,
+VBC_API int vbc1d_create(vbc_handle **out, int64_t m, int64_t n, int64_t W, int64_t L, const int64_t *spl,
                  const int64_t *pos, const int64_t *idx, const int64_t *ofs, const void *val,
                  int64_t nval, int dtype, int device, unsigned flags);
 
 /* SparseMatrixVBC{U,W,Tv,Int64}(m, n, Π, Φ, pos, idx, ofs, val)  (SparseMatrixVBCs.jl:62-82).
  * pspl[K+1] = Π.spl; idx holds block-row ids k (constructors_VBC.jl:123). */
-int vbc2d_create(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K,
+VBC_API int vbc2d_create(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K,
                  const int64_t *pspl, int64_t L, const int64_t *spl, const int64_t *pos,
                  const int64_t *idx, const int64_t *ofs, const void *val, int64_t nval, int dtype,
                  int device, unsigned flags);
 
 /* SparseMatrixCSC{Tv,Int64} (colptr[n+1], rowval, nzval), the operand of TrSpMV!(y, A, x)
  * (TrSpMV.jl:1-20).  Internally a 1DVBC with unit-width stripes. */
-int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t *colptr,
+VBC_API int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t *colptr,
                    const int64_t *rowval, const void *nzval, int dtype, int device, unsigned flags);
 
-int vbc_destroy(vbc_handle *h);
+VBC_API int vbc_destroy(vbc_handle *h);
 
 /* ---------------------------------------------------------------------------------------------
  * Products
@@ -100,7 +104,7 @@ int vbc_destroy(vbc_handle *h);
  * enqueued on `stream` (a hipStream_t; NULL = null stream) without synchronising.
  * mem = VBC_MEM_HOST: x, y are host pointers; the call stages them and returns when y is final.
  * x and y must not alias (the reference has the same precondition). */
-int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
+VBC_API int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
             double beta, int mem, void *stream, unsigned flags);
 
 /* Multi-RHS Y = α·op(B)·X + β·Y.  X is nx × nrhs, Y is ny × nrhs; column-major (ldx >= nx, ldy >=
@@ -110,7 +114,7 @@ int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_
  * matrix-core pass per 64 right-hand sides, row- or column-major.  Otherwise the transposed
  * row-major product with widths <= 8 runs a fused vector kernel over the SpMV layout, and the other
  * cases run one SpMV per column. */
-int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t ldx, int64_t nx,
+VBC_API int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t ldx, int64_t nx,
                 void *Y, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
                 unsigned flags);
 
@@ -136,13 +140,13 @@ typedef struct vbc_info {
     int64_t bytes_m;        /* matrix bytes (keys + values, panel-padded) one panel pass streams */
 } vbc_info;
 
-int vbc_get_info(const vbc_handle *h, vbc_info *info);
+VBC_API int vbc_get_info(const vbc_handle *h, vbc_info *info);
 
 /* Copies the thread's last error message (NUL-terminated, truncated to n). Returns its length. */
-int vbc_last_error(char *buf, size_t n);
+VBC_API int vbc_last_error(char *buf, size_t n);
 
 /* Library version (major*10000 + minor*100 + patch). */
-int vbc_version(void);
+VBC_API int vbc_version(void);
 
 #ifdef __cplusplus
 }

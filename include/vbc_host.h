@@ -19,6 +19,10 @@
 #ifndef VBC_HOST_H
 #define VBC_HOST_H
 
+#ifndef VBC_API
+#define VBC_API __attribute__((visibility("default")))  /* the library builds with -fvisibility=hidden */
+#endif
+
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -26,15 +30,15 @@ extern "C" {
 #endif
 
 /* EquiChunker(w): stripes of exactly w columns (last one shorter). */
-int vbcx_partition_equi(int64_t n, int64_t w, int64_t *spl, int64_t *L);
+VBC_API int vbcx_partition_equi(int64_t n, int64_t w, int64_t *spl, int64_t *L);
 
 /* StrictChunker(W): maximal runs of consecutive columns with identical row patterns, width <= W. */
-int vbcx_partition_strict(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+VBC_API int vbcx_partition_strict(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
                           int64_t W, int64_t *spl, int64_t *L);
 
 /* OverlapChunker(ρ, W): greedy; column j joins the open stripe while
  * |S(j) ∩ S(first)| >= ρ · max(|S(j)|, |S(first)|) and width < W (S = row pattern). */
-int vbcx_partition_overlap(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+VBC_API int vbcx_partition_overlap(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
                            double rho, int64_t W, int64_t *spl, int64_t *L);
 
 /* DynamicTotalChunker(model, W): optimal (minimum total cost) contiguous partition with width <= W
@@ -42,29 +46,29 @@ int vbcx_partition_overlap(int64_t m, int64_t n, const int64_t *colptr, const in
  *     cost(stripe) = c_stripe + c_col·w + c_pin·pins + c_row·rows + c_cell·w·rows
  * where rows = distinct rows of the stripe.  model_SparseMatrix1DVBC_memory(Tv, Ti) (costs.jl:10)
  * is (3Ti, 0, 0, Ti, Tv); model_SparseMatrix1DVBC_blocks() (costs.jl:8) is (0, 0, 0, 1, 0). */
-int vbcx_partition_dynamic(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+VBC_API int vbcx_partition_dynamic(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
                            int64_t W, double c_stripe, double c_col, double c_pin, double c_row,
                            double c_cell, int64_t *spl, int64_t *L);
 
 /* SparseMatrix1DVBC{W}(A, Φ) (constructors_1DVBC.jl:9-92): pass 1 fills pos[L+1], ofs[L+1]. */
-int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
+VBC_API int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
                      const int64_t *spl, int64_t *pos, int64_t *ofs);
 /* pass 2 fills idx[pos[L]-1] and val[ofs[L]-1 + pad] (pad trailing zeros, :35-39).
  * dtype: VBC_F64 / VBC_F32 (nzval and val have that eltype). */
-int vbcx_1dvbc_fill(int64_t m, int64_t n, int64_t W, const int64_t *colptr, const int64_t *rowval,
+VBC_API int vbcx_1dvbc_fill(int64_t m, int64_t n, int64_t W, const int64_t *colptr, const int64_t *rowval,
                     const void *nzval, int dtype, int64_t L, const int64_t *spl, const int64_t *pos,
                     const int64_t *ofs, int64_t *idx, void *val, int64_t pad);
 
 /* SparseMatrixVBC{U,W}(A, Π, Φ) (constructors_VBC.jl:15-133). */
-int vbcx_vbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t K,
+VBC_API int vbcx_vbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t K,
                    const int64_t *pspl, int64_t L, const int64_t *spl, int64_t *pos, int64_t *ofs);
-int vbcx_vbc_fill(int64_t m, int64_t n, int64_t U, int64_t W, const int64_t *colptr,
+VBC_API int vbcx_vbc_fill(int64_t m, int64_t n, int64_t U, int64_t W, const int64_t *colptr,
                   const int64_t *rowval, const void *nzval, int dtype, int64_t K,
                   const int64_t *pspl, int64_t L, const int64_t *spl, const int64_t *pos,
                   const int64_t *ofs, int64_t *idx, void *val, int64_t pad);
 
 /* Row pattern of Aᵀ (CSR of A) for row partitioning: rowptr[m+1], colval[nnz], 1-based. */
-int vbcx_transpose_pattern(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+VBC_API int vbcx_transpose_pattern(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
                            int64_t *rowptr, int64_t *colval);
 
 #ifdef __cplusplus

@@ -94,7 +94,7 @@ struct vbc_handle {
     vbc::PanelLaunch lm;          // multi-RHS transposed product on matrix cores (VBC_CREATE_MULTI)
     int64_t bytes_m = 0;          // matrix bytes one panel product streams
     int target_ranges_m = 4096;
-    int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA (ablation / debugging)
+    int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::Launch lt;               // transposed product: all buckets in one launch
@@ -304,13 +304,11 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
         int c0;
     };
     std::map<int, std::vector<Piece>> buckets;  // piece width -> pieces
-    for (int64_t l = 0; l < s.L; l++) {
-        if (s.rbeg[l + 1] == s.rbeg[l]) {
-            for (int c = 0; c < s.w[l]; c++) fill.push_back((int32_t)(s.col0[l] + c));
-            continue;
-        }
+    // Stripes that store no row stay in the layout with one HEAD sentinel row (zero contribution), so
+    // uniform-width matrices keep an affine stripe -> column map and no fill list is needed.
+    (void)fill;
+    for (int64_t l = 0; l < s.L; l++)
         for (int c0 = 0; c0 < s.w[l]; c0 += 16) buckets[std::min(16, s.w[l] - c0)].push_back({l, c0});
-    }
     const int esz = h->esz;
     // groups of every bucket first: ranges are spread over the launch in proportion to them
     std::map<int, std::vector<int64_t>> pgroups;  // w -> groups per panel
@@ -321,7 +319,7 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
         for (size_t p0 = 0; p0 < kv.second.size(); p0 += S) {
             int64_t rows = 0;
             for (size_t p = p0; p < std::min(kv.second.size(), p0 + S); p++)
-                rows += s.rbeg[kv.second[p].l + 1] - s.rbeg[kv.second[p].l];
+                rows += std::max<int64_t>(1, s.rbeg[kv.second[p].l + 1] - s.rbeg[kv.second[p].l]);
             pg.push_back((rows + 3) / 4);
             total_groups += pg.back();
         }
@@ -364,6 +362,7 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
         const int64_t Rp = acc * 4;
         const int64_t Ra = Rp + kPanelTail;  // over-read padding (vbc_panel.h)
         h->panel_val_bytes = std::max<int64_t>(h->panel_val_bytes, Ra * w * esz);
+        pp.b.val_bytes = (int32_t)std::min<int64_t>(Ra * w * esz, 0x7FFFFFFF);
         pp.o_key = ar.reserve(Ra * 4);
         pp.o_val = ar.reserve(Ra * w * esz);
         pp.o_out = ar.reserve(out.size() * 4);
@@ -383,6 +382,11 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
                     key[row] = (uint32_t)s.rows[q] | (q == s.rbeg[l] ? kHead : 0u);
                     std::memcpy(vv + row * w * esz, val + (s.voff[l] + (q - s.rbeg[l]) * wl + pcs[p].c0) * esz,
                                 (size_t)w * esz);
+                }
+                if (s.rbeg[l + 1] == s.rbeg[l]) {  // empty stripe: one HEAD sentinel row
+                    key[row] = kPanelSentinel | kHead;
+                    std::memset(vv + row * w * esz, 0, (size_t)w * esz);
+                    row++;
                 }
             }
             for (; row % 4; row++) {
@@ -522,11 +526,12 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
     if (flags & VBC_CREATE_MULTI) {
         int om = 0;
-        if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1, true>, kBlockThreads, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<float, 1, true>, kBlockThreads, 0);
+        if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1, true, true>, kBlockThreads, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<float, 1, true, true>, kBlockThreads, 0);
         h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
         if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
         if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
+        if (const char *e = getenv("VBC_PANEL_DIAG")) h->panel_valu |= atoi(e) & ~1;
         if (const char *e = getenv("VBC_PANEL_NOBUF")) h->panel_nobuf = atoi(e) != 0;
     }
 
@@ -731,23 +736,29 @@ static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_
         T *ys = reinterpret_cast<T *>(Y) + c0 * syc;
         if (L.total_ranges > 0) {
             const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
-            // byte extent of X as read by this chunk: rows 0..m-1, columns 0..nr-1
+            // byte extents of X and Y as addressed by this chunk (rows 0..m-1 / 0..n-1, columns 0..nr-1)
             const int64_t span = ((h->m - 1) * sxr + (int64_t)(nr - 1) * sxc + 1) * (int64_t)sizeof(T);
-            const bool buf = span + 64 * sxc * (int64_t)sizeof(T) < (int64_t(1) << 31) &&
-                             h->panel_val_bytes < (int64_t(1) << 31) && !h->panel_nobuf;
-            const uint32_t xb = (uint32_t)span;
-#define VBC_PANEL(NB, BUF)                                                                                    \
-    hipLaunchKernelGGL((spmm_panel<T, NB, BUF>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(), \
-                       L.total_ranges, xs, sxr, sxc, xb, ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu)
-            if (buf) {
-                if (nr <= 16) VBC_PANEL(1, true);
-                else if (nr <= 32) VBC_PANEL(2, true);
-                else VBC_PANEL(4, true);
-            } else {
-                if (nr <= 16) VBC_PANEL(1, false);
-                else if (nr <= 32) VBC_PANEL(2, false);
-                else VBC_PANEL(4, false);
-            }
+            const int64_t yspan = ((h->n - 1) * syr + (int64_t)(nr - 1) * syc + 1) * (int64_t)sizeof(T);
+            const int64_t lim = int64_t(1) << 31;
+            const bool buf = span + 64 * sxc * (int64_t)sizeof(T) < lim && h->panel_val_bytes < lim && !h->panel_nobuf;
+            bool affine = true;
+            for (const PanelBin &pb : L.bins) affine = affine && pb.out_affine;
+            const bool fast = buf && affine && !rd && yspan < lim;
+            const uint32_t xb = (uint32_t)span, yb = (uint32_t)std::min<int64_t>(yspan, lim - 1);
+#define VBC_PANEL(NB, BUF, FAST)                                                                              \
+    hipLaunchKernelGGL((spmm_panel<T, NB, BUF, FAST>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins,        \
+                       (int)L.bins.size(), L.total_ranges, xs, sxr, sxc, xb, ys, syr, syc, yb, nr, (T)alpha, (T)beta, \
+                       (int)rd, h->panel_valu)
+#define VBC_PANEL_NB(BUF, FAST)                                                                               \
+    do {                                                                                                      \
+        if (nr <= 16) VBC_PANEL(1, BUF, FAST);                                                                \
+        else if (nr <= 32) VBC_PANEL(2, BUF, FAST);                                                           \
+        else VBC_PANEL(4, BUF, FAST);                                                                         \
+    } while (0)
+            if (fast) VBC_PANEL_NB(true, true);
+            else if (buf) VBC_PANEL_NB(true, false);
+            else VBC_PANEL_NB(false, false);
+#undef VBC_PANEL_NB
 #undef VBC_PANEL
             VBC_HIP(hipGetLastError());
         }

@@ -28,7 +28,9 @@
 
 namespace vbc {
 
-constexpr uint32_t kPanelSentinel = 0x7FFFFFFFu;  // padding row: no HEAD, never a valid row (m < 2^31)
+// Padding row (no x row: never a valid row, m < 2^31).  Without HEAD it pads a panel to a multiple of
+// 4 rows; with HEAD it is the single row of a stripe that stores none (its columns get beta * Y).
+constexpr uint32_t kPanelSentinel = 0x7FFFFFFFu;
 
 // One width bucket of the panel layout.
 struct PanelBin {
@@ -39,7 +41,7 @@ struct PanelBin {
     int32_t out_affine;  // out[s] == out_base + s * out_stride
     int32_t out_base;
     int32_t out_stride;
-    int32_t pad_;
+    int32_t val_bytes;   // bytes of val (incl. tail padding), or 0x7FFFFFFF when >= 2 GiB (no BUF path)
     const uint32_t *key;  // rows (panel-padded): HEAD | x row, or kPanelSentinel
     const void *val;      // rows * w values
     const int32_t *out;   // per stripe: first y column
@@ -77,8 +79,14 @@ __device__ __forceinline__ int panel_out(const PanelBin &b, int seg)
 
 // kPanelBatch groups (4 rows each) are loaded before any of them is multiplied: one coalesced key
 // load per 64 rows, then every val and X load of the batch in flight together.
-constexpr int kPanelBatch = 16;
-constexpr int kPanelTail = 8 * kPanelBatch;  // padding rows after each bin (batch over-read + key prefetch)
+#ifndef VBC_PANEL_BATCH
+#define VBC_PANEL_BATCH 16
+#endif
+constexpr int kPanelBatch = VBC_PANEL_BATCH;
+constexpr int kPanelTail = 8 * kPanelBatch;
+// Offset of a masked buffer access: at least every num_records used (operands < 2 GiB) and, plus any
+// soffset below 2 GiB, still inside 32 bits -- the access is dropped (store) or reads 0 (load).
+constexpr uint32_t kOobOff = 0x80000000u;  // padding rows after each bin (batch over-read + key prefetch)
 
 // Raw buffer loads (32-bit offsets, hardware bounds check) for operands below 4 GiB.
 template <typename T>
@@ -94,14 +102,32 @@ __device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_rsrc_t rs, ui
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
 }
 
+template <typename T>
+__device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff);
+template <>
+__device__ __forceinline__ void buf_store<float>(float v, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, voff, soff, 0);
+}
+template <>
+__device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
+{
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
+}
+
+// diag (ablation, VBC_PANEL_DIAG): 1 VALU path, 2 no Y stores, 4 X gathers hit cache, 8 val hits cache.
 // BUF: X and the bins' val are addressed by 32-bit offsets through buffer descriptors (the host picks
 // it when both, plus the column offsets, stay below 2 GiB); otherwise 64-bit global addresses.
-template <typename T, int NB, bool BUF>
+// FAST (with BUF; beta = 0, affine stripe -> column map, Y below 2 GiB): a full panel is written by
+// 4*NB buffer stores at per-lane constant offsets plus one uniform panel offset -- no address
+// arithmetic, no loads, no branches in the flush.
+template <typename T, int NB, bool BUF, bool FAST>
 __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__restrict__ bins, int nbins,
                                                             int total_ranges, const T *__restrict__ X, int64_t sxr,
                                                             int64_t sxc, uint32_t xbytes, T *__restrict__ Y,
-                                                            int64_t syr, int64_t syc, int nrhs, T alpha, T beta,
-                                                            int rd_i, int force_valu)
+                                                            int64_t syr, int64_t syc, uint32_t ybytes, int nrhs,
+                                                            T alpha, T beta, int rd_i, int diag)
 {
     using M = MfmaAcc<T>;
     typedef typename M::v4 v4;
@@ -119,6 +145,9 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
     const int lane = threadIdx.x & 63;
     const int w = b.w, S = b.S;
     constexpr int esz = (int)sizeof(T);
+    // A-operand masking: fp64 masks by address (an out-of-range buffer offset reads 0, saving the
+    // select and its registers); fp32 selects after the load (cheaper with many masked lanes).
+    constexpr bool kOobMask = sizeof(T) == 8;
     // A operand: M row c = lane & 15 (stripe c / w of the panel, column c % w), k = lane >> 4.
     const int ca = lane & 15, kr = lane >> 4;
     const int sa = ca / w, cola = ca - sa * w;  // sa >= S: unused M row, never matches a stripe
@@ -152,17 +181,26 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
     const uint64_t vp = (uint64_t)(uintptr_t)b.val;
     const uint64_t vpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(vp >> 32)) << 32) |
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vp);
-    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)vpu, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)vpu, 0, b.val_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(Y, 0, (int)ybytes, 0x00020000);
     const uint32_t voff_lane = (uint32_t)((kr * w + cola) * esz);  // val offset of this lane's A element in a group
+    // FAST flush: per-lane byte offset of C(reg) for right-hand side block 0 within a panel whose first
+    // stripe is column out_base + seg_base * out_stride (past Y: the store is dropped)
+    uint32_t yoff[4];
+    const uint32_t ycol_b = (uint32_t)(16 * syc * esz);  // + per right-hand-side block
+    const int32_t ostr = b.out_stride;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        yoff[q] = (cs[q] < S && j < nrhs) ? (uint32_t)((((int64_t)cs[q] * ostr + cc[q]) * syr + (int64_t)j * syc) * esz)
+                                          : kOobOff;
     const T zero = T(0);
 
     v4 acc[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; nb++) acc[nb] = v4{zero, zero, zero, zero};
-    int cnt = 0;   // stripes started in the current panel
-    int segc = 0;  // stripes started in this range before the current batch
 
-    auto flush = [&]() {
+    // general flush of the open panel holding `cnt` stripes (any map, beta, 64-bit addresses)
+    auto flush_general = [&](int cnt) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (cs[q] < cnt) {
@@ -170,7 +208,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) {
                     const int jj = nb * 16 + j;
-                    if (jj < nrhs) {
+                    if (jj < nrhs && !(diag & 2)) {
                         gptr<T> yo = yg + o * syr + (int64_t)jj * syc;
                         T v = alpha * acc[nb][q];
                         if (rd_i) v = fmadd(beta, *yo, v);
@@ -182,26 +220,56 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
 #pragma unroll
         for (int nb = 0; nb < NB; nb++) acc[nb] = v4{zero, zero, zero, zero};
     };
+    // a full panel (S stripes) ends: FAST stores or the general flush
+    auto flush_full = [&]() {
+        if constexpr (FAST) {
+            const uint32_t pb = (uint32_t)((int64_t)(b.out_base + (int64_t)seg_base * ostr) * syr * esz);
+            if (!(diag & 2)) {
+#pragma unroll
+                for (int nb = 0; nb < NB; nb++) {
+                    if (nb * 16 < nrhs) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const uint32_t yo = (nb == 0 || nb * 16 + j < nrhs) ? yoff[q] : kOobOff;
+                            buf_store<T>(alpha * acc[nb][q], yrs, yo, pb + (uint32_t)nb * ycol_b);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int nb = 0; nb < NB; nb++) acc[nb] = v4{zero, zero, zero, zero};
+        } else {
+            flush_general(S);
+        }
+        seg_base += S;
+    };
 
     // Loads are unconditional (no divergent branches, so the waitcnt pass keeps them all in flight):
     // the bin arrays carry kPanelTail padding rows, rows past the range are masked by value, and
     // the keys of batch b+1 are prefetched while batch b is multiplied.
+    int segc = 0;  // stripes started in this range before the current batch
     uint32_t kraw = __builtin_nontemporal_load(key + (size_t)g0 * 4 + lane);
     for (int gb = g0; gb < g1; gb += kPanelBatch) {
         const int ng = min(kPanelBatch, g1 - gb);
         const uint32_t kv = lane < 4 * ng ? kraw : kPanelSentinel;
         kraw = __builtin_nontemporal_load(key + (size_t)(gb + kPanelBatch) * 4 + lane);
         const uint64_t hm = __ballot((kv & kHead) != 0);
-        // per row (lane = row of the batch): X offset and stripe index within its panel
+        // per row (lane = row of the batch): X offset, stripe index within its panel, panel starts
+        uint64_t fmask;  // bit 4q: a new panel starts at group q (flush the previous one first)
         {
+            const bool head = (kv & kHead) != 0;
             const int hc = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)) +
-                           (int)(kv >> 31);
+                           (int)head;
             const int gseg = segc + hc - 1;  // range-relative stripe of this row (ranges start at panels)
-            const bool ok = kv != kPanelSentinel;
-            const uint32_t xo = ok ? (kv & ~kHead) * sxr_b : xbytes;  // past X: the buffer load returns 0
+            const int rs = gseg - (gseg / S) * S;
+            fmask = __ballot(head && rs == 0 && gseg > 0);
+            const bool ok = (kv & ~kHead) != kPanelSentinel;
+            uint32_t xo = ok ? (kv & ~kHead) * sxr_b : xbytes;  // past X: the buffer load returns 0
+            if (diag & 4) xo = ok ? (uint32_t)(lane & 3) * sxr_b : xbytes;  // ablation: X gathers hit cache
             xch[wv][lane][0] = xo;
-            xch[wv][lane][1] = (uint32_t)(gseg - (gseg / S) * S);
+            xch[wv][lane][1] = (uint32_t)rs;
         }
+        segc += (int)__builtin_popcountll(hm);
         T av[kPanelBatch], xv[kPanelBatch][NB];
         uint32_t rsv[kPanelBatch];
 #pragma unroll
@@ -209,14 +277,15 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
             const uint32_t xo = xch[wv][4 * q + kr][0];
             rsv[q] = xch[wv][4 * q + kr][1];
             if constexpr (BUF) {
-                av[q] = buf_load<T>(vrs, voff_lane + (uint32_t)(q * 4 * w * esz), (uint32_t)((size_t)gb * 4 * w * esz));
+                const uint32_t vo = (!kOobMask || (int)rsv[q] == sa) ? voff_lane + (uint32_t)(q * 4 * w * esz) : kOobOff;
+                av[q] = buf_load<T>(vrs, vo, (diag & 8) ? 0u : (uint32_t)((size_t)gb * 4 * w * esz));
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) xv[q][nb] = buf_load<T>(xrs, xo + jofs[nb], 0u);
             } else {
                 const size_t row = (size_t)(gb + q) * 4 + kr;
                 av[q] = __builtin_nontemporal_load(val + row * w + cola);
                 const uint32_t rk = (uint32_t)__shfl((int)kv, 4 * q + kr, 64);
-                const bool ok = rk != kPanelSentinel;
+                const bool ok = (rk & ~kHead) != kPanelSentinel;
                 const int64_t xr = ok ? (int64_t)(rk & ~kHead) * sxr : 0;
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) {
@@ -234,55 +303,44 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
 #pragma unroll
             for (int nb = 0; nb < NB; nb++) chk = fmadd(xv[q][nb], zero, chk);
         }
-        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(chk != chk) != 0 || force_valu ? 1 : 0);
+        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(chk != chk) != 0 || (diag & 1) ? 1 : 0);
         if (!any_bad) {
 #pragma unroll
             for (int q = 0; q < kPanelBatch; q++) {
                 if (q < ng) {
-                    const uint32_t h4 = (uint32_t)(hm >> (4 * q)) & 0xFu;
-                    if ((h4 & 1u) && cnt == S) {  // first row of the next panel
-                        flush();
-                        seg_base += S;
-                        cnt = 0;
-                    }
-                    const T a = (int)rsv[q] == sa ? av[q] : zero;
+                    if (__builtin_expect((fmask >> (4 * q)) & 1, 0)) flush_full();
+                    const T a = (BUF && kOobMask) ? av[q] : ((int)rsv[q] == sa ? av[q] : zero);
 #pragma unroll
                     for (int nb = 0; nb < NB; nb++) acc[nb] = M::mma(a, xv[q][nb], acc[nb]);
-                    cnt += __builtin_popcount(h4);
                 }
             }
         } else {
-            // VALU, one row at a time: row k only feeds the accumulator rows of its own stripe
+            // VALU, one row at a time from memory: row k only feeds the accumulator rows of its own
+            // stripe (rare: only batches whose X holds an Inf / NaN, or VBC_PANEL_VALU)
             for (int q = 0; q < ng; q++) {
-                const uint32_t h4 = (uint32_t)(hm >> (4 * q)) & 0xFu;
-                if ((h4 & 1u) && cnt == S) {
-                    flush();
-                    seg_base += S;
-                    cnt = 0;
-                }
+                if ((fmask >> (4 * q)) & 1) flush_full();
                 for (int k = 0; k < 4; k++) {
                     const uint32_t rk = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)kv, 4 * q + k, 64));
-                    if (rk == kPanelSentinel) continue;
-                    const int rs = cnt - 1 + __builtin_popcount(h4 & ((2u << k) - 1u));
+                    if ((rk & ~kHead) == kPanelSentinel) continue;
+                    const int rsk = __builtin_amdgcn_readfirstlane((int)xch[wv][4 * q + k][1]);
                     const size_t row = (size_t)(gb + q) * 4 + k;
                     const int64_t xr = (int64_t)(rk & ~kHead) * sxr;
 #pragma unroll
                     for (int reg = 0; reg < 4; reg++) {
-                        const T a = cs[reg] == rs ? val[row * w + cc[reg]] : zero;
+                        if (cs[reg] != rsk) continue;
+                        const T a = val[row * w + cc[reg]];
 #pragma unroll
                         for (int nb = 0; nb < NB; nb++) {
                             const int jj = nb * 16 + j;
                             const T xval = jj < nrhs ? xg[xr + (int64_t)jj * sxc] : zero;
-                            if (cs[reg] == rs) acc[nb][reg] = fmadd(a, xval, acc[nb][reg]);
+                            acc[nb][reg] = fmadd(a, xval, acc[nb][reg]);
                         }
                     }
                 }
-                cnt += __builtin_popcount(h4);
             }
         }
-        segc += __builtin_popcountll(hm);
     }
-    flush();
+    flush_general(segc - ((segc - 1) / S) * S);  // the last panel (the bin's last may hold < S stripes)
 }
 
 // Y rows of the stripes that store no row (and belong to no panel): beta * Y or 0.

@@ -17,7 +17,7 @@ def declared_symbols():
     syms = set()
     for h in (ROOT / "include").glob("*.h"):
         text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
-        syms |= set(re.findall(r"^\s*int\s+(vbcx?_?\w+)\s*\(", text, flags=re.M))
+        syms |= set(re.findall(r"^\s*(?:VBC_API\s+)?int\s+(vbcx?_?\w+)\s*\(", text, flags=re.M))
     return syms
 
 
@@ -28,6 +28,11 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(str(L.LIB_PATH))
     for s in sorted(syms):
         assert hasattr(lib, s), s
+    # built with -fvisibility=hidden: the C ABI is the only dynamic interface
+    out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True, text=True)
+    if out.returncode == 0:
+        exported = {ln.split()[-1] for ln in out.stdout.splitlines() if " T " in ln}
+        assert exported == syms, exported ^ syms
 
 
 def test_library_is_gfx950_code_object():

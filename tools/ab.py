@@ -49,11 +49,23 @@ def main():
         (len(B.val) * esz + 4 * len(B.idx) + (k * esz) * (B.m + B.n))
     x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, (nx, k) if args.nrhs else nx).astype(dtype)).cuda()
     variants = [v for v in args.variants.split(";")]
-    handles = []
+    handles, libs = [], []
+    main_lib = L.lib()
     for v in variants:
+        # "@lib=path": this variant runs another build of libvbc (compile-time variants, same process)
+        lp = [t.split("=", 1)[1] for t in v.split(",") if t.strip().startswith("@lib=")]
+        if lp:
+            saved_path, saved_lib = L.LIB_PATH, L._lib
+            L.LIB_PATH, L._lib = Path(lp[0]).resolve(), None
+            vlib = L.lib()
+            L.LIB_PATH = saved_path
+        else:
+            vlib, saved_lib = main_lib, main_lib
+        L._lib = vlib
+        libs.append(vlib)
         saved = dict(os.environ)
         for kv in v.split(","):
-            if "=" in kv:
+            if "=" in kv and not kv.strip().startswith("@"):
                 ek, ev_ = kv.split("=", 1)
                 os.environ[ek.strip()] = ev_.strip()
         hp = C.c_void_p()
@@ -64,11 +76,11 @@ def main():
         os.environ.clear()
         os.environ.update(saved)
         handles.append(hp)
+        L._lib = main_lib
     ys = [torch.empty((ny, k) if args.nrhs else ny, dtype=x.dtype, device="cuda") for _ in variants]
     stream = torch.cuda.current_stream()
-    lib = L.lib()
-
     def run(i):
+        lib = libs[i]
         if args.nrhs:
             L.check(lib.vbc_mul_mat(handles[i], int(trans), k, x.data_ptr(), k, nx, ys[i].data_ptr(), k, ny,
                                     1.0, 0.0, L.VBC_MEM_DEVICE, stream.cuda_stream, L.VBC_MAT_ROWMAJOR), "mul_mat")
@@ -97,8 +109,8 @@ def main():
         flops = 2.0 * len(B.val) * k / (np.median(t) * 1e-3) / 1e12
         print(f"{v:40s} {flops:6.2f} TFLOP/s median {np.median(t)*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
               f"{nbytes / (np.median(t) * 1e-3) / 1e9:7.0f} GB/s  rel-diff-vs-first {d:.2e}", flush=True)
-    for hp in handles:
-        lib.vbc_destroy(hp)
+    for i, hp in enumerate(handles):
+        libs[i].vbc_destroy(hp)
 
 
 if __name__ == "__main__":
