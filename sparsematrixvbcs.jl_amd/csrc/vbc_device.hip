@@ -598,9 +598,19 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
     if (L.total_ranges > 0) {
         const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
         const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;
+        // load-free owner writes when every bucket maps segments affinely and beta = 0
+        bool faste = !rd;
+        for (const Bin &bb : L.bins) faste = faste && bb.out_affine;
+        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
 #define VBC_LAUNCH(KIND, KK, PP)                                                                         \
-    hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins, \
-                       (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd)
+    do {                                                                                                 \
+        if (faste)                                                                                       \
+            hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP, 0, true>), dim3(grid), dim3(kBlockThreads), 0, stream, \
+                               L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
+        else                                                                                             \
+            hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP>), dim3(grid), dim3(kBlockThreads), 0, stream, \
+                               L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
+    } while (0)
         const int P = L.bins.empty() ? kPipeDefault : L.bins[0].pipe;
         const int D = L.bins.empty() ? 0 : L.bins[0].diag;
         if constexpr (std::is_same<T, double>::value) {

@@ -154,24 +154,27 @@ __device__ __forceinline__ int out_of(const Bin &b, int seg)
     return b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
 }
 
-template <typename T, int KIND, int V>
+// FASTE (every bin affine, beta = 0): no loads at all -- a load here would make the waitcnt pass
+// drain the software pipeline's in-flight stream at every owner write.
+template <typename T, int KIND, int V, bool FASTE = false>
 __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int sub, int LPR, int SS, int lane,
                                      T *__restrict__ y, T alpha, T beta, bool rd)
 {
+    const int o = FASTE ? b.out_base + seg * b.out_stride : out_of(b, seg);
     if constexpr (KIND == 0) {
-        gptr<T> yo = G(y) + out_of(b, seg) + sub * V;
+        gptr<T> yo = G(y) + o + sub * V;
 #pragma unroll
         for (int e = 0; e < V; e++) {
             T r = alpha * v[e];
-            if (rd) r = fmadd(beta, yo[e], r);
+            if (!FASTE && rd) r = fmadd(beta, yo[e], r);
             yo[e] = r;
         }
     } else {
         const T s = slot_sum<T, V>(v, lane, sub, LPR, SS);
         if (sub == 0) {
-            gptr<T> yo = G(y) + out_of(b, seg);
+            gptr<T> yo = G(y) + o;
             T r = alpha * s;
-            if (rd) r = fmadd(beta, *yo, r);
+            if (!FASTE && rd) r = fmadd(beta, *yo, r);
             *yo = r;
         }
     }
@@ -195,7 +198,7 @@ __device__ __forceinline__ void hand_off(const Bin &b, int r, int seg, const T (
 
 // DIAG (ablation builds only; never selected by default): 1 = loads and gathers but no segmented
 // reduction (a plain fold keeps the loads live), 2 = no x gathers (x taken as 1).
-template <typename T, int KIND, int W_, int K, int P, int DIAG = 0>
+template <typename T, int KIND, int W_, int K, int P, int DIAG = 0, bool FASTE = false>
 __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T *__restrict__ x,
                                           T *__restrict__ y, T alpha, T beta, bool rd)
 {
@@ -212,7 +215,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     const int slot = kDpp ? (lane & (cRPI - 1)) : lane / LPR;
     const int sub = kDpp ? (lane / cRPI) : lane - slot * LPR;
     const int SS = kDpp ? cRPI : 1;  // lane stride between the columns of one slot
-    const bool active = slot < RPI && sub < LPR;
+    const bool active = kDpp || (slot < RPI && sub < LPR);
     const int t0 = r * b.tiles_per_range;
     const int t1 = min(t0 + b.tiles_per_range, b.ntiles);
     if (t0 >= t1) return;
@@ -229,32 +232,36 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     for (int e = 0; e < V; e++) carry[e] = T(0);
     bool owned = false;        // the open segment's HEAD lies in this range
 
-    // Stage 1: keys and values of a tile (one coalesced sweep per k).
+    // Stage 1: keys and values of a tile (one coalesced sweep per k).  Loads are unconditional --
+    // a tile past the range re-reads the range's last tile (never reduced), idle lanes read slot 0
+    // and drop it -- so no branch hides them from the waitcnt pass (which would otherwise wait for
+    // the whole in-flight stream at the merge).
+    const int lslot = active ? slot : 0, lsub = active ? sub : 0;
     auto load_stream = [&](int t, uint32_t (&kk)[K], T (&v)[K][V]) {
-        if (active && t < t1) {
-            const size_t base = (size_t)t * tile_rows + slot;
+        const size_t base = (size_t)min(t, t1 - 1) * tile_rows + lslot;
 #pragma unroll
-            for (int k = 0; k < K; k++) kk[k] = __builtin_nontemporal_load(key + base + (size_t)k * RPI);
+        for (int k = 0; k < K; k++) kk[k] = __builtin_nontemporal_load(key + base + (size_t)k * RPI);
 #pragma unroll
-            for (int k = 0; k < K; k++) ld_stream<T, V>(val + (base + (size_t)k * RPI) * w + sub * V, v[k]);
-        } else {
+        for (int k = 0; k < K; k++) ld_stream<T, V>(val + (base + (size_t)k * RPI) * w + lsub * V, v[k]);
+        if constexpr (!kDpp) {
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                kk[k] = 0;
+                kk[k] = active ? kk[k] : 0u;
 #pragma unroll
-                for (int e = 0; e < V; e++) v[k][e] = T(0);
+                for (int e = 0; e < V; e++) v[k][e] = active ? v[k][e] : T(0);
             }
         }
     };
     // Stage 2: the x gathers of a tile whose keys have arrived (kind 0: one x per entry).
     constexpr int XV = KIND == 0 ? 1 : V;
     auto gather = [&](int t, const uint32_t (&kk)[K], T (&xv)[K][XV]) {
+        (void)t;
         if constexpr (DIAG == 2) {
 #pragma unroll
             for (int k = 0; k < K; k++)
 #pragma unroll
                 for (int e = 0; e < XV; e++) xv[k][e] = T(1);
-        } else if (active && t < t1) {
+        } else {
 #pragma unroll
             for (int k = 0; k < K; k++) {
                 const uint32_t gi = kk[k] & ~kHead;
@@ -262,14 +269,9 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
                     xv[k][0] = xg_[gi];
                 } else {
 #pragma unroll
-                    for (int e = 0; e < V; e++) xv[k][e] = xg_[gi + sub * V + e];
+                    for (int e = 0; e < V; e++) xv[k][e] = xg_[gi + lsub * V + e];
                 }
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; k++)
-#pragma unroll
-                for (int e = 0; e < XV; e++) xv[k][e] = T(0);
         }
     };
     T diag_acc = T(0);
@@ -317,7 +319,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         for (int k = 0; k < K; k++) {
             if (kk[k] & kHead) {
                 if (seen)  // opened and closed inside this slot: owned and complete
-                    emit<T, KIND, V>(b, seg, cur, sub, LPR, SS, lane, y, alpha, beta, rd);
+                    emit<T, KIND, V, FASTE>(b, seg, cur, sub, LPR, SS, lane, y, alpha, beta, rd);
                 else {
 #pragma unroll
                     for (int e = 0; e < V; e++) lead[e] = cur[e];
@@ -390,7 +392,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
 #pragma unroll
                 for (int e = 0; e < V; e++) tot[e] = (ef ? es[e] : carry[e] + es[e]) + lead[e];
                 if (from_range)
-                    emit<T, KIND, V>(b, cseg, tot, sub, LPR, SS, lane, y, alpha, beta, rd);
+                    emit<T, KIND, V, FASTE>(b, cseg, tot, sub, LPR, SS, lane, y, alpha, beta, rd);
                 else
                     hand_off<T, KIND, V>(b, r, cseg, tot, sub, LPR, SS, lane, w);
             }
@@ -467,25 +469,25 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     if (active && slot == 0) {
         const int cseg = seg_base - 1;
         if (owned)
-            emit<T, KIND, V>(b, cseg, carry, sub, LPR, SS, lane, y, alpha, beta, rd);
+            emit<T, KIND, V, FASTE>(b, cseg, carry, sub, LPR, SS, lane, y, alpha, beta, rd);
         else if (!starts_at_head)  // no HEAD in the whole range: all of it continues cseg
             hand_off<T, KIND, V>(b, r, cseg, carry, sub, LPR, SS, lane, w);
     }
 }
 
 #define VBC_W_CASES(KIND)                                                                          \
-    case 0: run_range<T, KIND, 0, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 1: run_range<T, KIND, 1, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 2: run_range<T, KIND, 2, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 3: run_range<T, KIND, 3, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 4: run_range<T, KIND, 4, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 5: run_range<T, KIND, 5, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 6: run_range<T, KIND, 6, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 7: run_range<T, KIND, 7, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;                     \
-    case 8: run_range<T, KIND, 8, K, P, DIAG>(b, r, lane, x, y, alpha, beta, rd); break;
+    case 0: run_range<T, KIND, 0, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;              \
+    case 1: run_range<T, KIND, 1, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 2: run_range<T, KIND, 2, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 3: run_range<T, KIND, 3, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 4: run_range<T, KIND, 4, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 5: run_range<T, KIND, 5, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 6: run_range<T, KIND, 6, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 7: run_range<T, KIND, 7, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;                     \
+    case 8: run_range<T, KIND, 8, K, P, DIAG, FASTE>(b, r, lane, x, y, alpha, beta, rd); break;
 
 // One wave per range; the wave finds its bucket by a scalar scan of the (few) bins.
-template <typename T, int KIND, int K, int P, int DIAG = 0>
+template <typename T, int KIND, int K, int P, int DIAG = 0, bool FASTE = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_ranges(const Bin *__restrict__ bins, int nbins,
                                                              int total_ranges, const T *__restrict__ x,
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
