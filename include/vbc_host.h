@@ -50,6 +50,13 @@ VBC_API int vbcx_partition_dynamic(int64_t m, int64_t n, const int64_t *colptr, 
                            int64_t W, double c_stripe, double c_col, double c_pin, double c_row,
                            double c_cell, int64_t *spl, int64_t *L);
 
+/* DynamicTotalChunker over a ColumnBlockComponentCostModel (costs.jl:12, the TrSpMV time model):
+ *     cost(stripe of width w with R distinct rows) = alpha[w-1] + beta[w-1]·R,   1 <= w <= W,
+ * alpha / beta hold W entries (model_SparseMatrix1DVBC_TrSpMV_time fits them, costs.py). */
+VBC_API int vbcx_partition_dynamic_table(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                                         int64_t W, const double *alpha, const double *beta, int64_t *spl,
+                                         int64_t *L);
+
 /* SparseMatrix1DVBC{W}(A, Φ) (constructors_1DVBC.jl:9-92): pass 1 fills pos[L+1], ofs[L+1]. */
 VBC_API int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
                      const int64_t *spl, int64_t *pos, int64_t *ofs);

@@ -5,12 +5,13 @@ SparseMatrix1DVBC / SparseMatrixVBC / mul! / TrSpMV! / Base.:*, over libvbc's C 
 (include/vbc.h), whose hand-written gfx950 kernels do every product.  Import it as
 `sparsematrixvbcs_amd` (the repo-root loader) since the directory name is not an identifier.
 """
-from . import _lib, distributed, synthetic
+from . import _lib, costs, distributed, io, synthetic
 from ._lib import ArgumentError, DimensionMismatch, HIPError, UnsupportedDtype
 from .matrices import (DEFAULT_SIMD_SIZE, Adjoint, SparseMatrix1DVBC, SparseMatrixCSC, SparseMatrixVBC,
                        Transpose, adjoint, transpose)
 from .multiply import TrSpMV_, matmul, mul_, mulmat_
-from .partition import (AlternatePacker, AlternatingPacker, ConstrainedCost, DynamicTotalChunker,
+from .costs import model_SparseMatrix1DVBC_TrSpMV_time
+from .partition import (AlternatePacker, AlternatingPacker, ColumnBlockCostModel, ConstrainedCost, DynamicTotalChunker,
                         EquiChunker, OverlapChunker, SplitPartition, StrictChunker, VertexCount,
                         model_SparseMatrix1DVBC_blocks, model_SparseMatrix1DVBC_memory, pack_plaid,
                         pack_stripe)
@@ -24,6 +25,7 @@ __all__ = [
     "transpose", "mul_", "mulmat_", "matmul", "TrSpMV_", "SplitPartition", "EquiChunker",
     "StrictChunker", "OverlapChunker", "DynamicTotalChunker", "ConstrainedCost", "VertexCount",
     "AlternatingPacker", "AlternatePacker", "pack_stripe", "pack_plaid",
-    "model_SparseMatrix1DVBC_blocks", "model_SparseMatrix1DVBC_memory", "DimensionMismatch",
+    "model_SparseMatrix1DVBC_blocks", "model_SparseMatrix1DVBC_memory", "model_SparseMatrix1DVBC_TrSpMV_time",
+    "ColumnBlockCostModel", "DimensionMismatch",
     "ArgumentError", "HIPError", "UnsupportedDtype", "DEFAULT_SIMD_SIZE",
 ]

@@ -25,7 +25,7 @@ ABI_SYMBOLS = (
     "vbc1d_create", "vbc2d_create", "vbc_csc_create", "vbc_destroy", "vbc_mul", "vbc_mul_mat",
     "vbc_get_info", "vbc_last_error", "vbc_version",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
-    "vbcx_partition_dynamic", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
+    "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
     "vbcx_vbc_fill", "vbcx_transpose_pattern",
 )
 
@@ -65,6 +65,15 @@ def lib():
         if not LIB_PATH.exists():
             raise ImportError(f"libvbc.so not found at {LIB_PATH}; build it with `make -C {PKG_DIR}` "
                               "or __graft_entry__.build()")
+        # PyTorch bundles its own HIP / HSA runtimes under the same sonames as /opt/rocm's
+        # (libamdhip64.so.7, libhsa-runtime64.so.1) but links them by their unversioned names: if
+        # libvbc were loaded first, torch would load a second pair of runtimes and whichever
+        # initialised second would see no device.  Importing torch first makes libvbc bind to the
+        # runtime already in the process (one runtime, shared streams and memory).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(LIB_PATH))
         P, I64, INT, U, D = C.c_void_p, C.c_int64, C.c_int, C.c_uint, C.c_double
         L.vbc1d_create.argtypes = [C.POINTER(P), I64, I64, I64, I64, P, P, P, P, P, I64, INT, INT, U]
@@ -80,6 +89,7 @@ def lib():
         L.vbcx_partition_strict.argtypes = [I64, I64, P, P, I64, P, P]
         L.vbcx_partition_overlap.argtypes = [I64, I64, P, P, D, I64, P, P]
         L.vbcx_partition_dynamic.argtypes = [I64, I64, P, P, I64, D, D, D, D, D, P, P]
+        L.vbcx_partition_dynamic_table.argtypes = [I64, I64, P, P, I64, P, P, P, P]
         L.vbcx_1dvbc_count.argtypes = [I64, I64, P, P, I64, P, P, P]
         L.vbcx_1dvbc_fill.argtypes = [I64, I64, I64, P, P, P, INT, I64, P, P, P, P, P, I64]
         L.vbcx_vbc_count.argtypes = [I64, I64, P, P, I64, P, I64, P, P, P]

@@ -1,0 +1,96 @@
+"""The TrSpMV time cost model, re-fitted to the gfx950 kernel (costs.jl:12-136).
+
+The reference times mul!(y, B', x) on random VBR matrices of every width w = W..1 (its own
+generator, costs.jl:45-83: d = 8 stored rows per stripe, sizes around a cache level) and fits, by
+relative least squares, a per-stripe cost alpha[w] and a per-stored-row cost beta[w] (plus a per-row
+term it then drops); the widths' costs are made monotone (costs.jl:124-128).  The partitioner then
+minimises sum(alpha[w] + beta[w]·rows) (DynamicTotalChunker over ColumnBlockCostModel).
+
+Here the same protocol times libvbc's kernel on the GPU.  Sizes follow costs.jl's "exceed" branch
+scaled to this device's last-level cache (the 256 MiB MALL): the model describes the HBM-streaming
+regime the kernel runs in.  Fitted parameters are cached as JSON (the reference's DiskCache): key =
+(W, Tv, Ti, Tu, device name, libvbc version).
+"""
+import json
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib as _L
+from .partition import ColumnBlockCostModel
+
+CACHE_DIR = Path(os.environ.get("VBC_AUTOTUNE_DIR", Path.home() / ".cache" / "sparsematrixvbcs_amd" / "autotune"))
+LLC_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MI355X_MICROARCH.md)
+
+
+def _key(W, Tv, Ti, Tu, device):
+    import torch
+    name = torch.cuda.get_device_name(device).replace(" ", "_").replace("/", "_")
+    return f"1DVBC_TrSpMV_W{W}_{np.dtype(Tv).name}_{np.dtype(Ti).name}_{np.dtype(Tu).name}_{name}_v{_L.lib().vbc_version()}"
+
+
+def model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv=np.float64, Ti=np.int64, Tu=np.float64, device=0, reps=20,
+                                            llc_bytes=LLC_BYTES, seed=0xDEADBEEF):
+    """Time the transposed product on the reference's random VBR matrices (costs.jl:14-99).
+    Returns (ms, ns, Ls, ws, qs, T) with T in seconds (median kernel time over `reps`)."""
+    import torch
+    from .synthetic import vbr_1dvbc
+    from .multiply import mul_
+    ms, ns, Ls, ws, qs, T = [], [], [], [], [], []
+    isz, vsz, usz = np.dtype(Ti).itemsize, np.dtype(Tv).itemsize, np.dtype(Tu).itemsize
+    d = 8
+    for w in range(W, 0, -1):
+        C = 2 * llc_bytes
+        L0 = int(np.ceil(C / ((3 + d) * isz + 2 * w * usz + d * w * vsz)))
+        m0 = L0 * w
+        q0 = L0 * d
+        for (m, L, q) in ((m0, L0, q0), (m0, 2 * L0, q0), (2 * m0, L0, q0), (m0, L0, 2 * q0)):
+            B = vbr_1dvbc(m, L, q, w, W=W, dtype=Tv, seed=seed + w * 131 + L + q)
+            x = torch.ones(B.m, dtype=torch.float64 if np.dtype(Tu) == np.float64 else torch.float32, device=device)
+            y = torch.ones(B.n, dtype=x.dtype, device=device)
+            for _ in range(3):
+                mul_(y, B.T, x)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for a, b in ev:
+                a.record()
+                mul_(y, B.T, x)
+                b.record()
+            torch.cuda.synchronize(device)
+            t = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e-3
+            ms.append(m); ns.append(B.n); Ls.append(L); ws.append(w); qs.append(int(B.pos[-1] - 1)); T.append(t)
+            B.release()
+    return ms, ns, Ls, ws, qs, T
+
+
+def fit_time_params(W, ms, Ls, ws, qs, T):
+    """costs.jl:101-136: rows [m, onehot_w(L), onehot_w(q)], weights 1/T, least squares against 1;
+    alpha_col = per-stripe, beta_col = per-stored-row cost of width w, both made monotone in w."""
+    D = np.zeros((len(T), 1 + 2 * W))
+    for i in range(len(T)):
+        D[i, 0] = ms[i]
+        D[i, ws[i]] = Ls[i]
+        D[i, W + ws[i]] = qs[i]
+    Tm = np.asarray(T, dtype=np.float64)
+    P, *_ = np.linalg.lstsq(D / Tm[:, None], np.ones(len(T)), rcond=None)
+    alpha = P[1:1 + W].copy()
+    beta = P[1 + W:].copy()
+    for w in range(1, W):  # monotonize (costs.jl:124-128)
+        alpha[w] = max(alpha[w], alpha[w - 1])
+        beta[w] = max(beta[w], beta[w - 1])
+    return float(P[0]), alpha, beta
+
+
+def model_SparseMatrix1DVBC_TrSpMV_time(W, Tv=np.float64, Ti=np.int64, Tu=np.float64, device=0, refit=False,
+                                        **kwargs):
+    """ColumnBlockCostModel(alpha, beta) of this GPU's transposed product (cached; costs.jl:12)."""
+    CACHE_DIR.mkdir(parents=True, exist_ok=True)
+    path = CACHE_DIR / (_key(W, Tv, Ti, Tu, device) + ".json")
+    if path.exists() and not refit:
+        d = json.loads(path.read_text())
+        return ColumnBlockCostModel(d["alpha"], d["beta"])
+    ms, ns, Ls, ws, qs, T = model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv, Ti, Tu, device, **kwargs)
+    a_row, alpha, beta = fit_time_params(W, ms, Ls, ws, qs, T)
+    path.write_text(json.dumps({"W": W, "alpha": alpha.tolist(), "beta": beta.tolist(), "alpha_row": a_row,
+                                "data": {"m": ms, "n": ns, "L": Ls, "w": ws, "q": qs, "t": T}}, indent=1))
+    return ColumnBlockCostModel(alpha, beta)

@@ -215,6 +215,36 @@ int vbcx_partition_dynamic(int64_t m, int64_t n, const int64_t *colptr, const in
     return VBC_OK;
 }
 
+int vbcx_partition_dynamic_table(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                                 int64_t W, const double *alpha, const double *beta, int64_t *spl, int64_t *L)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (W < 1 || !alpha || !beta) return fail(VBC_INVALID_ARG, "W must be > 0 with W alpha / beta entries");
+    const double inf = std::numeric_limits<double>::infinity();
+    std::vector<double> f(n + 1, inf);
+    std::vector<int64_t> back(n + 1, 0), stamp(m, -1);
+    f[0] = 0.0;
+    for (int64_t e = 1; e <= n; e++) {
+        int64_t rows = 0;
+        for (int64_t w = 1; w <= W && w <= e; w++) {
+            const int64_t j = e - w;  // add column j (0-based) to the stripe [j, e)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t i = rowval[p] - 1;
+                if (stamp[i] != e) { stamp[i] = e; rows++; }
+            }
+            const double c = alpha[w - 1] + beta[w - 1] * (double)rows;
+            if (f[j] + c < f[e]) { f[e] = f[j] + c; back[e] = j; }
+        }
+    }
+    std::vector<int64_t> cuts;
+    for (int64_t e = n; e > 0; e = back[e]) cuts.push_back(back[e]);
+    int64_t l = 0;
+    for (auto it = cuts.rbegin(); it != cuts.rend(); ++it) spl[l++] = *it + 1;
+    spl[l] = n + 1;
+    *L = l;
+    return VBC_OK;
+}
+
 int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
                      const int64_t *spl, int64_t *pos, int64_t *ofs)
 {

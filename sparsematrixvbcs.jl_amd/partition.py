@@ -67,6 +67,20 @@ def model_SparseMatrix1DVBC_memory(Tv=np.float64, Ti=np.int64):
 
 
 # --- chunkers ---------------------------------------------------------------------------------
+class ColumnBlockCostModel:
+    """ColumnBlockComponentCostModel (costs.jl:12): cost(stripe of width w, R rows) = alpha[w] + beta[w]·R.
+    model_SparseMatrix1DVBC_TrSpMV_time (costs.py) fits alpha / beta to the GPU kernel."""
+
+    def __init__(self, alpha, beta):
+        self.alpha = np.ascontiguousarray(alpha, dtype=np.float64)
+        self.beta = np.ascontiguousarray(beta, dtype=np.float64)
+        if self.alpha.shape != self.beta.shape or self.alpha.ndim != 1:
+            raise _L.ArgumentError("alpha and beta must be vectors of the same length W")
+
+    def __repr__(self):
+        return f"ColumnBlockCostModel(alpha={self.alpha.tolist()}, beta={self.beta.tolist()})"
+
+
 class EquiChunker:
     def __init__(self, w=1):
         self.w = int(w)
@@ -138,9 +152,15 @@ class DynamicTotalChunker:
         m, n = A.shape
         spl = np.zeros(n + 1, np.int64)
         L = np.zeros(1, np.int64)
-        _L.check(_L.lib().vbcx_partition_dynamic(m, n, colptr.ctypes.data, rowval.ctypes.data, self.W,
-                                                 *self.model.c, spl.ctypes.data, L.ctypes.data),
-                 "DynamicTotalChunker")
+        if isinstance(self.model, ColumnBlockCostModel):
+            W = min(self.W, len(self.model.alpha))
+            _L.check(_L.lib().vbcx_partition_dynamic_table(m, n, colptr.ctypes.data, rowval.ctypes.data, W,
+                                                           self.model.alpha.ctypes.data, self.model.beta.ctypes.data,
+                                                           spl.ctypes.data, L.ctypes.data), "DynamicTotalChunker")
+        else:
+            _L.check(_L.lib().vbcx_partition_dynamic(m, n, colptr.ctypes.data, rowval.ctypes.data, self.W,
+                                                     *self.model.c, spl.ctypes.data, L.ctypes.data),
+                     "DynamicTotalChunker")
         return SplitPartition(spl[:L[0] + 1])
 
 

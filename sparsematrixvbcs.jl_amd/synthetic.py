@@ -128,3 +128,55 @@ def c5(dtype=np.float32, scale=1.0, u=8, w=8, seed=0xDEADBEEF):
     L = max(4, int(round(2 ** 18 * scale * 8 / w)))
     q = int(round(6 * L * 64 / (u * w)))
     return vbr_2d(K, L, q, u, w, dtype=dtype, seed=seed)
+
+
+# SuiteSparse matrices of BASELINE.json's configs C2-C4 (not available offline): (n, nnz) from the
+# reference's own output (ct20stif: src/ref.out:29-32) and the SuiteSparse index (ldoor).
+STANDINS = {"Boeing/ct20stif": (52329, 2600295), "GHS_psdef/ldoor": (952203, 42493817)}
+
+
+def fe_stiffness_3d(n, nnz, dof=3, dtype=np.float64, seed=0xDEADBEEF):
+    """A symmetric 3D finite-element stiffness stand-in with exactly n rows and nnz within 9 of the
+    target: n/dof mesh nodes on a near-cubic grid (row-major), each node coupled to itself and to a
+    random symmetric subset of its 18 face/edge neighbours, every coupling a dense dof x dof block of
+    U[-1, 1) values (symmetric: block(j, i) = block(i, j)').  Returns a sorted scipy CSC matrix."""
+    import scipy.sparse as sp
+    if n % dof:
+        raise ValueError("n must be a multiple of dof")
+    rng = np.random.default_rng(seed)
+    N = n // dof
+    g = int(np.ceil(N ** (1 / 3)))
+    node = np.arange(N, dtype=np.int64)
+    a, b, c = node // (g * g), (node // g) % g, node % g
+    offs = [(da, db, dc) for da in (-1, 0, 1) for db in (-1, 0, 1) for dc in (-1, 0, 1)
+            if 0 < abs(da) + abs(db) + abs(dc) <= 2]
+    pairs = []
+    for da, db, dc in offs:
+        if (da, db, dc) <= (0, 0, 0):  # each unordered pair once (lexicographically positive offsets)
+            continue
+        aa, bb, cc = a + da, b + db, c + dc
+        ok = (aa >= 0) & (aa < g) & (bb >= 0) & (bb < g) & (cc >= 0) & (cc < g)
+        nb = aa * g * g + bb * g + cc
+        ok &= nb < N
+        pairs.append(np.stack([node[ok], nb[ok]], axis=1))
+    pairs = np.concatenate(pairs)
+    want = int(round(nnz / (dof * dof)))  # blocks: N diagonal + 2 per kept pair
+    keep = max(0, min(len(pairs), (want - N) // 2))
+    pairs = pairs[np.sort(rng.choice(len(pairs), keep, replace=False))]
+    bi = np.concatenate([node, pairs[:, 0], pairs[:, 1]])
+    bj = np.concatenate([node, pairs[:, 1], pairs[:, 0]])
+    blk = rng.uniform(-1, 1, (N + keep, dof, dof))
+    diag = (blk[:N] + np.transpose(blk[:N], (0, 2, 1))) / 2
+    vals = np.concatenate([diag, blk[N:], np.transpose(blk[N:], (0, 2, 1))])
+    r = (bi[:, None, None] * dof + np.arange(dof)[None, :, None]).repeat(dof, axis=2)
+    cidx = (bj[:, None, None] * dof + np.arange(dof)[None, None, :]).repeat(dof, axis=1)
+    A = sp.csc_matrix((vals.reshape(-1).astype(dtype), (r.reshape(-1), cidx.reshape(-1))), shape=(n, n))
+    A.sum_duplicates()
+    A.sort_indices()
+    return A
+
+
+def standin(name, dtype=np.float64, seed=0xDEADBEEF):
+    """fe_stiffness_3d with the n and nnz of a SuiteSparse matrix of BASELINE.json (C2-C4)."""
+    n, nnz = STANDINS[name]
+    return fe_stiffness_3d(n, nnz, 3, dtype, seed)

@@ -1,0 +1,144 @@
+"""Host-side rows of SURVEY.md §8f: Matrix Market input + built-layout cache (row 3), the TrSpMV time
+cost model and its partitioner (row 4), and the SuiteSparse stand-ins of configs C2-C4."""
+import itertools
+
+import numpy as np
+import pytest
+import scipy.io
+import scipy.sparse as sp
+
+import sparsematrixvbcs_amd as V
+from oracle import oracle as O
+
+
+def test_mdopen_reads_local_matrix_market(tmp_path):
+    A = sp.random(40, 30, 0.2, format="csc", random_state=3)
+    (tmp_path / "HB").mkdir()
+    scipy.io.mmwrite(str(tmp_path / "HB" / "tiny.mtx"), A)
+    d = V.io.mdopen("HB/tiny", root=tmp_path)
+    assert d.A.shape == (40, 30) and (abs(d.A - A) > 0).nnz == 0
+    S = sp.random(25, 25, 0.2, format="csc", random_state=4)
+    S = sp.tril(S).tocsc()
+    scipy.io.mmwrite(str(tmp_path / "sym.mtx"), S + sp.tril(S, -1).T, symmetry="symmetric")
+    full = V.io.mdopen("sym", root=tmp_path).A
+    assert (abs(full - full.T) > 0).nnz == 0 and full.nnz == (S + sp.tril(S, -1).T).nnz
+    with pytest.raises(FileNotFoundError):
+        V.io.mdopen("Boeing/ct20stif", root=tmp_path)
+
+
+def test_built_layout_cache_roundtrip(tmp_path, golden):
+    A = golden["HB__west0132"]["A"] if "HB__west0132" in golden else next(iter(golden.values()))["A"]
+    for B in (V.SparseMatrix1DVBC[4](A, V.StrictChunker(4)),
+              V.SparseMatrixVBC[4, 4](A, V.AlternatingPacker(V.StrictChunker(4), V.StrictChunker(4)))):
+        p = tmp_path / f"{type(B).__name__}.npz"
+        calls = []
+        B1 = V.io.cached_build(lambda: calls.append(1) or B, p)
+        B2 = V.io.cached_build(lambda: calls.append(1) or B, p)
+        assert calls == [1]
+        for f in ("pos", "idx", "ofs", "val"):
+            assert np.array_equal(getattr(B1, f), getattr(B2, f))
+        assert np.array_equal(B1.Phi.spl, B2.Phi.spl) and (B1.m, B1.n, B1.W) == (B2.m, B2.n, B2.W)
+
+
+def test_memory_column_matches_reference_formula():
+    """mem = sizeof(Φ) + sizeof(pos) + sizeof(idx) + sizeof(ofs) + sizeof(val) (test_table.jl:80)."""
+    B = V.synthetic.vbr_1dvbc(100, 20, 60, 3, W=8, seed=1)
+    L, q = len(B.Phi), int(B.pos[-1] - 1)
+    assert V.io.memory_bytes(B) == 8 + 8 * (L + 1) + 8 * q + 8 * (L + 1) + 8 * len(B.val)
+
+
+@pytest.mark.parametrize("name", sorted(V.synthetic.STANDINS))
+def test_standins_match_suitesparse_shape(name):
+    n, nnz = V.synthetic.STANDINS[name]
+    if n > 100000:
+        pytest.skip("large stand-in: exercised by tools/test_table.py on the GPU box")
+    A = V.synthetic.standin(name)
+    assert A.shape == (n, n) and abs(A.nnz - nnz) <= 9
+    assert (abs(A - A.T) > 1e-15).nnz == 0
+    assert set(V.StrictChunker(8).partition(A).widths().tolist()) == {3}  # node dof columns share a pattern
+
+
+def _brute_force_best(A, W, alpha, beta):
+    m, n = A.shape
+    A = A.tocsc()
+    best = (np.inf, None)
+    for cuts in itertools.product([0, 1], repeat=n - 1):
+        spl = [0] + [j + 1 for j, c in enumerate(cuts) if c] + [n]
+        if max(np.diff(spl)) > W:
+            continue
+        cost = 0.0
+        for a, b in zip(spl[:-1], spl[1:]):
+            rows = np.unique(A[:, a:b].indices).size
+            cost += alpha[b - a - 1] + beta[b - a - 1] * rows
+        if cost < best[0] - 1e-12:
+            best = (cost, spl)
+    return best
+
+
+def test_time_model_partitioner_is_optimal():
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        A = sp.random(12, 9, 0.3, format="csc", random_state=trial)
+        W = 4
+        alpha = np.sort(rng.uniform(1, 3, W))
+        beta = np.sort(rng.uniform(0.1, 1, W))
+        P = V.DynamicTotalChunker(V.ConstrainedCost(V.ColumnBlockCostModel(alpha, beta), V.VertexCount(), W)).partition(A)
+        spl = P.spl - 1
+        cost = sum(alpha[b - a - 1] + beta[b - a - 1] * np.unique(A[:, a:b].indices).size
+                   for a, b in zip(spl[:-1], spl[1:]))
+        best, _ = _brute_force_best(A, W, alpha, beta)
+        assert abs(cost - best) < 1e-9
+
+
+def test_time_model_fit_recovers_parameters():
+    """costs.jl:101-136 restated: exact synthetic timings t = a_row*m + alpha_w*L + beta_w*q are
+    recovered by the weighted least squares, then monotonized."""
+    W = 4
+    a_row, alpha, beta = 1e-9, np.array([2e-9, 3e-9, 3.5e-9, 5e-9]), np.array([1e-9, 1.5e-9, 2.5e-9, 3e-9])
+    ms, Ls, ws, qs, T = [], [], [], [], []
+    for w in range(W, 0, -1):
+        for (m, L, q) in ((1000, 100, 800), (1000, 200, 800), (2000, 100, 800), (1000, 100, 1600)):
+            ms.append(m); Ls.append(L); ws.append(w); qs.append(q)
+            T.append(a_row * m + alpha[w - 1] * L + beta[w - 1] * q)
+    r, a, b = V.costs.fit_time_params(W, ms, Ls, ws, qs, T)
+    assert np.allclose(a, alpha, rtol=1e-6) and np.allclose(b, beta, rtol=1e-6) and abs(r - a_row) < 1e-15
+
+
+@pytest.mark.gpu
+def test_gpu_time_model_fit(tmp_path, monkeypatch):
+    """The model fitted to the GPU kernel (small sizes) is positive, monotone and cached; its
+    partition builds a matrix whose product matches the oracle."""
+    monkeypatch.setattr(V.costs, "CACHE_DIR", tmp_path)
+    mdl = V.model_SparseMatrix1DVBC_TrSpMV_time(4, np.float64, np.int64, np.float64, llc_bytes=2 ** 22, reps=5)
+    assert (mdl.alpha >= 0).all() and (np.diff(mdl.alpha) >= 0).all() and (np.diff(mdl.beta) >= 0).all()
+    assert list(tmp_path.glob("*.json"))
+    A = V.synthetic.standin("Boeing/ct20stif")
+    B = V.SparseMatrix1DVBC[4](A, V.DynamicTotalChunker(V.ConstrainedCost(mdl, V.VertexCount(), 4)))
+    import torch
+    x = np.random.default_rng(1).random(B.m)
+    y = torch.empty(B.n, dtype=torch.float64, device="cuda:0")
+    V.mul_(y, B.T, torch.from_numpy(x).cuda())
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    yr = O.mul(R, x, np.zeros(B.n), trans=True, nthreads=8)
+    assert np.linalg.norm(y.cpu().numpy() - yr) <= 1e-12 * np.linalg.norm(yr)
+
+
+@pytest.mark.gpu
+def test_library_loaded_before_torch_shares_its_runtime():
+    """Host calls first (libvbc loaded before torch is imported), then GPU work through torch and
+    libvbc in the same process: one HIP runtime (see _lib.lib)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np, scipy.sparse as sp\n"
+            "import sparsematrixvbcs_amd as V\n"
+            "A = sp.random(50, 40, 0.1, format='csc', random_state=0)\n"
+            "V.StrictChunker(4).partition(A)\n"
+            "import torch\n"
+            "B = V.SparseMatrix1DVBC[4](A, V.StrictChunker(4))\n"
+            "x = torch.rand(50, dtype=torch.float64, device='cuda')\n"
+            "y = V.mul_(torch.empty(40, dtype=torch.float64, device='cuda'), B.T, x)\n"
+            "assert torch.allclose(y.cpu(), torch.from_numpy(A.T @ x.cpu().numpy()))\n"
+            "print('ok')\n") % str(V._lib.PKG_DIR.parent)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -35,7 +35,11 @@ def main():
     from sparsematrixvbcs_amd import _lib as L
 
     dtype = np.float64 if args.dtype == "f64" else np.float32
-    if args.workload == "c5":
+    if args.workload in ("ct20stif", "ldoor"):
+        name = {"ct20stif": "Boeing/ct20stif", "ldoor": "GHS_psdef/ldoor"}[args.workload]
+        A = V.synthetic.standin(name).T.tocsc().astype(dtype)
+        B = V.SparseMatrix1DVBC[8](A, V.StrictChunker(8))
+    elif args.workload == "c5":
         B = V.synthetic.c5(dtype=dtype, scale=args.scale)
     elif args.workload == "fe":
         B = V.synthetic.fe_grid_2d(int(round(2236 * args.scale ** 0.5)), dof=2, dtype=dtype)
@@ -45,7 +49,7 @@ def main():
     trans = bool(args.trans)
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
     k = max(args.nrhs, 1)
-    nbytes = bench.algorithmic_bytes(B, esz) + (k - 1) * esz * (B.m + B.n) if args.workload != "c5" else \
+    nbytes = bench.algorithmic_bytes(B, esz) + (k - 1) * esz * (B.m + B.n) if args.workload not in ("c5",) else \
         (len(B.val) * esz + 4 * len(B.idx) + (k * esz) * (B.m + B.n))
     x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, (nx, k) if args.nrhs else nx).astype(dtype)).cuda()
     variants = [v for v in args.variants.split(";")]

@@ -1,0 +1,138 @@
+"""The reference's benchmark table (bin/test_table.jl) on the GPU: one row per construction method.
+
+    python tools/test_table.py [--matrix Boeing/ct20stif] [--dtype f64] [--fit-time-model] [--json out.json]
+
+For each matrix (mdopen from $VBC_MATRIX_DIR, else the synthetic stand-in with the same n and nnz,
+synthetic.STANDINS) it builds A = permutedims(A) (test_table.jl:27) and reports, per method:
+setup time (host partition + layout build), memory (the reference's `mem` formula, Int64 indices),
+the GPU time of mul!(y, B', x, true, false) (median of HIP-event-timed launches), the oracle's CPU
+time of the same product (all host cores, as the reference's @threads loop), and the normwise error
+against scipy's A'x.  Row 'reference' is TrSpMV!(y, A, x) on the CSC matrix (test_table.jl:29-41).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def gpu_time(B, x, y, reps):
+    import torch
+    import sparsematrixvbcs_amd as V
+    op = V.adjoint(B)
+    for _ in range(3):
+        V.mul_(y, op, x, True, False)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        V.mul_(y, op, x, True, False)
+        b.record()
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e-3
+
+
+def cpu_time(R, x, n, reps=5, trsp=None):
+    from oracle import oracle as O
+    th = max(1, min(16, os.cpu_count() or 1))
+    y = np.zeros(n, dtype=x.dtype)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        if trsp is not None:
+            O.trspmv(trsp, x, y, nthreads=th)
+        else:
+            O.mul(R, x, y, trans=True, nthreads=th)
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), th
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--matrix", default="Boeing/ct20stif")
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--W", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--fit-time-model", action="store_true", help="add the 'min time' row (fits the GPU model)")
+    ap.add_argument("--no-2d", action="store_true")
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    import torch
+    import sparsematrixvbcs_amd as V
+    from oracle import oracle as O
+
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    try:
+        A = V.io.mdopen(args.matrix).A
+        source = "SuiteSparse file"
+    except FileNotFoundError:
+        A = V.synthetic.standin(args.matrix)
+        source = "synthetic stand-in (synthetic.STANDINS: same n, nnz)"
+    A = A.T.tocsc().astype(dtype)  # permutedims(sparse(mdopen(mtx).A)), test_table.jl:27
+    A.sort_indices()
+    m, n = A.shape
+    rng = np.random.default_rng(0xC0FFEE)
+    xh = rng.random(m).astype(dtype)
+    ref = (A.T @ xh.astype(np.float64))
+    x = torch.from_numpy(xh).cuda()
+    y = torch.empty(n, dtype=x.dtype, device="cuda")
+    W = args.W
+    lim = lambda mdl: V.ConstrainedCost(mdl, V.VertexCount(), W)
+    rows = []
+
+    def record(name, setup, mem, B=None, R=None, trsp=None):
+        t_gpu = gpu_time(B, x, y, args.reps)
+        err = float(np.linalg.norm(y.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref))
+        t_cpu, th = cpu_time(R, xh, n, trsp=trsp)
+        bytes_ = B.info()["bytes_t"] if hasattr(B, "info") else None
+        row = dict(method=name, setup_s=round(setup, 4), memory=int(mem), gpu_us=round(t_gpu * 1e6, 2),
+                   cpu_us=round(t_cpu * 1e6, 1), cpu_threads=th, speedup=round(t_cpu / t_gpu, 1),
+                   gpu_GBs=round(bytes_ / t_gpu / 1e9, 1) if bytes_ else None, rel_err=err)
+        rows.append(row)
+        print(f"{name:22s} setup {setup:8.3f}s  mem {mem:12d}  gpu {t_gpu * 1e6:9.2f} us  cpu {t_cpu * 1e6:10.1f} us"
+              f"  x{t_cpu / t_gpu:7.1f}  err {err:.1e}", flush=True)
+        if hasattr(B, "release"):
+            B.release()
+
+    # reference row: TrSpMV!(y, A, x) on the CSC matrix
+    C = V.SparseMatrixCSC(A)
+    mem_csc = 8 * (len(A.indptr) + len(A.indices)) + A.data.nbytes
+    record("reference (TrSpMV!)", 0.0, mem_csc, C, trsp=A)
+
+    methods = [("strict", V.StrictChunker(W)), ("overlap", V.OverlapChunker(0.9, W)),
+               ("min blocks", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks()))),
+               ("min memory", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_memory(dtype, np.int64))))]
+    if args.fit_time_model:
+        mdl = V.model_SparseMatrix1DVBC_TrSpMV_time(W, dtype, np.int64, dtype)
+        methods.append(("min time (GPU model)", V.DynamicTotalChunker(lim(mdl))))
+    for name, method in methods:
+        t0 = time.perf_counter()
+        B = V.SparseMatrix1DVBC[W](A, method)
+        setup = time.perf_counter() - t0
+        R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+        record(name, setup, V.io.memory_bytes(B), B, R)
+    if not args.no_2d:
+        for name, method in [
+                ("1D 2D", V.AlternatingPacker(V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks())), V.EquiChunker(1))),
+                ("strict 2D", V.AlternatingPacker(V.StrictChunker(W), V.StrictChunker(W))),
+                ("overlap 2D 0.9", V.AlternatingPacker(V.OverlapChunker(0.9, W), V.OverlapChunker(0.9, W))),
+                ("overlap 2D 0.8", V.AlternatingPacker(V.OverlapChunker(0.8, W), V.OverlapChunker(0.8, W))),
+                ("overlap 2D 0.7", V.AlternatingPacker(V.OverlapChunker(0.7, W), V.OverlapChunker(0.7, W)))]:
+            t0 = time.perf_counter()
+            B = V.SparseMatrixVBC[W, W](A, method)
+            setup = time.perf_counter() - t0
+            R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+            record(name, setup, V.io.memory_bytes(B), B, R)
+    out = dict(matrix=args.matrix, source=source, m=m, n=n, nnz=int(A.nnz), dtype=args.dtype, W=W,
+               device=torch.cuda.get_device_name(0), rows=rows)
+    if args.json:
+        Path(args.json).write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
