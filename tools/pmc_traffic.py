@@ -17,10 +17,10 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-KERNEL = "spmv_ranges"
+KERNEL = "spmv_ranges"  # --kernel overrides
 
 
-def run_pass(counters, outdir, bench_args):
+def run_pass(counters, outdir, bench_args, kernel=KERNEL):
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", str(outdir),
            "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), *bench_args]
     print("pass:", " ".join(counters), flush=True)
@@ -30,7 +30,7 @@ def run_pass(counters, outdir, bench_args):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if KERNEL not in row.get("Kernel_Name", ""):
+                if kernel not in row.get("Kernel_Name", ""):
                     continue
                 name = row["Counter_Name"]
                 vals.setdefault(name, []).append(float(row["Counter_Value"]))
@@ -44,6 +44,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--extra", default="")
     ap.add_argument("--counters", default="", help="extra counter passes, ';'-separated groups")
+    ap.add_argument("--kernel", default=KERNEL, help="kernel name substring to attribute counters to")
+    ap.add_argument("--read-factor", type=float, default=2.0,
+                    help="FETCH_SIZE correction: 2 for 16-B/lane streaming reads (gfx950 half-count), 1 for "
+                         "dword loads and gathers")
     args = ap.parse_args()
     out = ROOT / "gpurun_out" / "pmc"
     bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--workload", args.workload,
@@ -52,7 +56,7 @@ def main():
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"]] + [g.split(",") for g in args.counters.split(";") if g]
     for i, counters in enumerate(passes):
         try:
-            vals = run_pass(counters, out / f"pass{i}", bench_args)
+            vals = run_pass(counters, out / f"pass{i}", bench_args, args.kernel)
         except subprocess.SubprocessError as e:  # a counter set the profiler cannot serve
             print("pass failed:", counters, e, flush=True)
             if i < 2:
@@ -63,11 +67,12 @@ def main():
     fetch_kb = res["FETCH_SIZE"]["mean"]
     write_kb = res["WRITE_SIZE"]["mean"]
     summary = {
-        "workload": args.workload, "dtype": args.dtype, "kernel": KERNEL,
+        "workload": args.workload, "dtype": args.dtype, "kernel": args.kernel,
         "method": "rocprofv3 --kernel-trace --pmc, FETCH_SIZE and WRITE_SIZE in separate passes; "
-                  "read bytes = 2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md §HBM)",
+                  f"read bytes = {args.read_factor:g} x FETCH_SIZE (gfx950 counts 16-B/lane streaming reads "
+                  "at half, MI355X_MICROARCH.md §HBM; dword loads and gathers are counted in full)",
         "fetch_size_kb_per_launch": fetch_kb, "write_size_kb_per_launch": write_kb,
-        "hbm_bytes_per_launch": int(2 * fetch_kb * 1024 + write_kb * 1024),
+        "hbm_bytes_per_launch": int(args.read_factor * fetch_kb * 1024 + write_kb * 1024),
         "raw_bytes_per_launch": int(fetch_kb * 1024 + write_kb * 1024),
         "counters": res,
     }
