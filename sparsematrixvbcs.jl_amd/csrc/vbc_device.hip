@@ -147,8 +147,10 @@ struct Entry {
 // Lay out one bucket's entry stream (segment-ordered) as tiles, ranges and fix-up slots.
 static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry> &ents,
                         const std::vector<int32_t> &out, int64_t total_entries, const char *val,
-                        Arena &ar, int &range0, PendingBin &pb)
+                        Arena &ar, int &range0, PendingBin &pb, int wsrc = 0)
 {
+    // wsrc < w: the entries carry wsrc values each, stored w wide with zero padding columns
+    if (wsrc <= 0) wsrc = w;
     const int esz = h->esz;
     const int V = w <= 8 ? vec_elems(esz, w) : 1;
     const int LPR = w / V;
@@ -168,6 +170,7 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     pb.b.kind = kind;
     pb.b.wkey = w <= 8 ? w : 0;
     pb.b.w = w;
+    pb.b.wst = wsrc;
     pb.b.rpi = RPI;
     pb.b.range0 = range0;
     pb.b.nranges = (int32_t)nr;
@@ -195,21 +198,47 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     int32_t *rseg = ar.at<int32_t>(pb.o_rseg);
     std::memcpy(ar.at<int32_t>(pb.o_out), out.data(), out.size() * 4);
     int64_t heads = 0;
+    const int GV = val_group(esz, w);  // grouped tile layout (vbc_kernels.h key_pos / val_pos)
     for (int64_t t = 0; t < Rp; t++) {
         const int64_t tile = t / tile_rows, within = t - tile * tile_rows;
-        const int64_t slot = within / K, k = within - slot * K;
-        const int64_t phys = tile * tile_rows + k * RPI + slot;
+        const int slot = (int)(within / K), k = (int)(within - (int64_t)slot * K);
+        const size_t pk = key_pos((size_t)(tile * tile_rows), k, slot, RPI);
+        const size_t pv = val_pos((size_t)(tile * tile_rows), k, slot, RPI, GV);
         if (within == 0 && tile % tpr == 0) rseg[tile / tpr] = (int32_t)heads;
         if (t < R) {
-            key[phys] = ents[t].key;
+            key[pk] = ents[t].key;
             heads += (ents[t].key >> 31);
-            std::memcpy(vv + phys * w * esz, val + ents[t].voff * esz, (size_t)w * esz);
+            std::memcpy(vv + pv * w * esz, val + ents[t].voff * esz, (size_t)wsrc * esz);
+            if (wsrc < w) std::memset(vv + (pv * w + wsrc) * esz, 0, (size_t)(w - wsrc) * esz);
         } else {
-            key[phys] = 0;  // padding extends the last segment by zeros
-            std::memset(vv + phys * w * esz, 0, (size_t)w * esz);
+            key[pk] = 0;  // padding extends the last segment by zeros
+            std::memset(vv + pv * w * esz, 0, (size_t)w * esz);
         }
     }
     return VBC_OK;
+}
+
+// Stored width of a transposed bucket.  Widths whose rows do not split into 16-B lane vectors
+// with a power-of-two slot count (w = 3, 5, 6, 7) run the shuffle-scan path with 4-8-B loads; padding
+// them with zero columns buys 16-B loads and the DPP scan for 14-60 % more value bytes.  The padding
+// columns multiply x[row] by 0 into outputs that are never written (the forward product, which would
+// gather x beyond the stripe, is never padded).  VBC_PAD="w:wp,..." overrides (A/B).
+static int padded_width(const vbc_handle *h, int w)
+{
+    static const int def64[9] = {0, 1, 2, 4, 4, 5, 6, 8, 8};
+    static const int def32[9] = {0, 1, 2, 4, 4, 5, 8, 8, 8};
+    int wp = w <= 8 ? (h->esz == 8 ? def64[w] : def32[w]) : w;
+    if (const char *e = getenv("VBC_PAD")) {
+        wp = w;
+        for (const char *p = e; *p;) {
+            int a = 0, b = 0, n = 0;
+            if (sscanf(p, "%d:%d%n", &a, &b, &n) != 2) break;
+            if (a == w && b >= w && b <= 64) wp = b;
+            p += n;
+            if (*p == ',') p++;
+        }
+    }
+    return wp;
 }
 
 // Transposed layout: segments = non-empty stripes of each width, entries = their stored rows.
@@ -234,8 +263,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                                 s.voff[l] + (r - s.rbeg[l]) * w});
         }
         PendingBin pb;
-        if (int st = build_bucket(h, 0, w, ents, out, total, val, ar, range0, pb)) return st;
-        h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)w * h->esz) + (int64_t)out.size() * 4;
+        const int wp = padded_width(h, w);
+        if (int st = build_bucket(h, 0, wp, ents, out, total, val, ar, range0, pb, w)) return st;
+        h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)wp * h->esz) + (int64_t)out.size() * 4;
         pbs.push_back(pb);
     }
     L.total_ranges = range0;

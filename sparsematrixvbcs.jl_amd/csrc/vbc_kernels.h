@@ -48,7 +48,8 @@ __device__ __forceinline__ double fmadd(double a, double b, double c) { return _
 struct Bin {
     int32_t kind;     // 0: B'x, 1: Bx
     int32_t wkey;     // dispatch width: 1..8, or 0 = runtime width (w > 8)
-    int32_t w;        // entry width
+    int32_t w;        // entry width as laid out (padded: a w = 3 bucket may be stored 4 wide)
+    int32_t wst;      // columns actually written (the stripes' width, <= w)
     int32_t rpi;      // slots per tile (64 / lanes-per-entry)
     int32_t range0;   // first range (wave) of this bucket in the launch
     int32_t nranges;  // ranges of this bucket
@@ -71,6 +72,25 @@ struct Bin {
 __host__ __device__ constexpr int vec_elems(int esz, int w)
 {
     return esz == 8 ? (w % 2 == 0 ? 2 : 1) : (w % 4 == 0 ? 4 : (w % 2 == 0 ? 2 : 1));
+}
+
+// Grouped tile layout.  Keys: each lane's 4 consecutive entries (k = 4g .. 4g+3) are contiguous, one
+// 16-B load: entry (slot s, k) of a tile at (k/4)*RPI*4 + s*4 + k%4.  Values: when one lane holds a
+// whole row (LPR = 1) narrower than 16 B, G = 16 / (V*esz) consecutive entries of the lane are
+// contiguous (entry at (k/G)*RPI*G + s*G + k%G) so those loads are 16 B too; otherwise G = 1.
+constexpr int kKeyGroup = 4;
+__host__ __device__ constexpr int val_group(int esz, int w)
+{
+    return (w >= 1 && w <= 8 && w / vec_elems(esz, w) == 1 && vec_elems(esz, w) * esz < 16)
+               ? 16 / (vec_elems(esz, w) * esz) : 1;
+}
+__host__ __device__ constexpr size_t key_pos(size_t tile_base, int k, int s, int RPI)
+{
+    return tile_base + (size_t)(k / kKeyGroup) * RPI * kKeyGroup + (size_t)s * kKeyGroup + (k % kKeyGroup);
+}
+__host__ __device__ constexpr size_t val_pos(size_t tile_base, int k, int s, int RPI, int G)
+{
+    return tile_base + (size_t)(k / G) * RPI * G + (size_t)s * G + (k % G);
 }
 
 template <typename T, int V>
@@ -163,8 +183,10 @@ __device__ __forceinline__ void emit(const Bin &b, int seg, const T (&v)[V], int
     const int o = FASTE ? b.out_base + seg * b.out_stride : out_of(b, seg);
     if constexpr (KIND == 0) {
         gptr<T> yo = G(y) + o + sub * V;
+        const int lim = b.wst - sub * V;  // padding columns (w > wst) are never written
 #pragma unroll
         for (int e = 0; e < V; e++) {
+            if (e >= lim) break;
             T r = alpha * v[e];
             if (!FASTE && rd) r = fmadd(beta, yo[e], r);
             yo[e] = r;
@@ -237,12 +259,30 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     // and drop it -- so no branch hides them from the waitcnt pass (which would otherwise wait for
     // the whole in-flight stream at the merge).
     const int lslot = active ? slot : 0, lsub = active ? sub : 0;
+    constexpr int GV = kGeneric ? 1 : val_group((int)sizeof(T), W_);
     auto load_stream = [&](int t, uint32_t (&kk)[K], T (&v)[K][V]) {
-        const size_t base = (size_t)min(t, t1 - 1) * tile_rows + lslot;
+        const size_t tb = (size_t)min(t, t1 - 1) * tile_rows;
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int k = 0; k < K; k++) kk[k] = __builtin_nontemporal_load(key + base + (size_t)k * RPI);
+        for (int g = 0; g < K / kKeyGroup; g++) {
+            const u4 q = __builtin_nontemporal_load((gptr<const u4>)(key + key_pos(tb, g * kKeyGroup, lslot, RPI)));
 #pragma unroll
-        for (int k = 0; k < K; k++) ld_stream<T, V>(val + (base + (size_t)k * RPI) * w + lsub * V, v[k]);
+            for (int i = 0; i < kKeyGroup; i++) kk[g * kKeyGroup + i] = q[i];
+        }
+        if constexpr (GV == 1) {
+#pragma unroll
+            for (int k = 0; k < K; k++) ld_stream<T, V>(val + val_pos(tb, k, lslot, RPI, 1) * w + lsub * V, v[k]);
+        } else {  // one row per lane, GV entries per 16-B load
+            typedef T vt __attribute__((ext_vector_type(GV * V)));
+#pragma unroll
+            for (int g = 0; g < K / GV; g++) {
+                const vt q = __builtin_nontemporal_load((gptr<const vt>)(val + val_pos(tb, g * GV, lslot, RPI, GV) * w));
+#pragma unroll
+                for (int i = 0; i < GV; i++)
+#pragma unroll
+                    for (int e = 0; e < V; e++) v[g * GV + i][e] = q[i * V + e];
+            }
+        }
         if constexpr (!kDpp) {
 #pragma unroll
             for (int k = 0; k < K; k++) {
@@ -560,6 +600,7 @@ __device__ __forceinline__ void run_range_mm(const Bin &b, int r, int lane, cons
         const int o = out_of(b, seg);
 #pragma unroll
         for (int c = 0; c < W_; c++) {
+            if (c >= b.wst) break;
             gptr<T> yo = yg + (int64_t)(o + c) * ldy + j;
             T q = alpha * v[c];
             if (rd) q = fmadd(beta, *yo, q);
@@ -583,10 +624,9 @@ __device__ __forceinline__ void run_range_mm(const Bin &b, int r, int lane, cons
             T vv[K][W_], xv[K];
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                const size_t e = base + (size_t)k * RPI + s;
                 if (sv) {
-                    kk[k] = __builtin_nontemporal_load(key + e);
-                    load_row<T, W_>(val + e * W_, vv[k]);
+                    kk[k] = __builtin_nontemporal_load(key + key_pos(base, k, s, RPI));
+                    load_row<T, W_>(val + val_pos(base, k, s, RPI, val_group((int)sizeof(T), W_)) * W_, vv[k]);
                 } else {
                     kk[k] = 0u;
 #pragma unroll
@@ -741,7 +781,7 @@ __global__ __launch_bounds__(kBlockThreads) void fixup_mm(const Bin *__restrict_
         if (seg < 0 || (r > 0 && b.carry_seg[r - 1] == seg)) return;
         const T *cm = carry_mm + (size_t)bi * carry_stride;
         const int o = out_of(b, seg);
-        for (int c = 0; c < b.w; c++) {
+        for (int c = 0; c < b.wst; c++) {
             T s = T(0);
             for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++) s += cm[((size_t)q * b.w + c) * NR + j];
             T *yo = y + (int64_t)(o + c) * ldy + j;
@@ -768,9 +808,10 @@ __global__ __launch_bounds__(kBlockThreads) void fixup(const Bin *__restrict__ b
         const int r = i - b.range0;
         const int seg = b.carry_seg[r];
         if (seg < 0 || (r > 0 && b.carry_seg[r - 1] == seg)) return;
-        const int wc = KIND == 0 ? b.w : 1;
+        const int wc = KIND == 0 ? b.w : 1;            // carry stride (layout width)
+        const int wout = KIND == 0 ? b.wst : 1;        // columns written
         T *__restrict__ yo = y + out_of(b, seg);
-        for (int c = 0; c < wc; c++) {
+        for (int c = 0; c < wout; c++) {
             T s = T(0);
             for (int q = r; q < b.nranges && b.carry_seg[q] == seg; q++)
                 s += static_cast<const T *>(b.carry)[(size_t)q * wc + c];

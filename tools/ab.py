@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="fe")
+    ap.add_argument("--workload", default="fe", help="fe | ns | ns-mixed | c5 | ct20stif | ldoor | ldoor-csc")
     ap.add_argument("--variants", default="VBC_TILE_K=4;VBC_TILE_K=8")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
@@ -35,7 +35,9 @@ def main():
     from sparsematrixvbcs_amd import _lib as L
 
     dtype = np.float64 if args.dtype == "f64" else np.float32
-    if args.workload in ("ct20stif", "ldoor"):
+    if args.workload == "ldoor-csc":
+        B = V.SparseMatrixCSC(V.synthetic.standin("GHS_psdef/ldoor").T.tocsc().astype(dtype))
+    elif args.workload in ("ct20stif", "ldoor"):
         name = {"ct20stif": "Boeing/ct20stif", "ldoor": "GHS_psdef/ldoor"}[args.workload]
         A = V.synthetic.standin(name).T.tocsc().astype(dtype)
         B = V.SparseMatrix1DVBC[8](A, V.StrictChunker(8))
@@ -49,7 +51,8 @@ def main():
     trans = bool(args.trans)
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
     k = max(args.nrhs, 1)
-    nbytes = bench.algorithmic_bytes(B, esz) + (k - 1) * esz * (B.m + B.n) if args.workload not in ("c5",) else \
+    nbytes = (B.info(0, trans)["bytes_t" if trans else "bytes_f"] if args.workload == "ldoor-csc" else
+              bench.algorithmic_bytes(B, esz) + (k - 1) * esz * (B.m + B.n)) if args.workload not in ("c5",) else \
         (len(B.val) * esz + 4 * len(B.idx) + (k * esz) * (B.m + B.n))
     x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, (nx, k) if args.nrhs else nx).astype(dtype)).cuda()
     variants = [v for v in args.variants.split(";")]
