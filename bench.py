@@ -162,6 +162,12 @@ def measure(args, workload, dtype, world, rank, local, device, with_cpu):
     y = torch.empty((B.n, k) if k > 1 else B.n, dtype=x.dtype, device=device)
     Bt = B.T
     B.handle(local, True, multi=k > 1)  # build the HBM layout outside the timed region
+    if k > 1:
+        kernel_name = "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
+    elif B.info(local, True)["slot_bins"] > 0:
+        kernel_name = "vbc::spmv_slots<T, 0, U, FASTE> (slotted segments, csrc/vbc_slots.h)"
+    else:
+        kernel_name = "vbc::spmv_ranges<T, 0, K, P> (+ vbc::fixup)"
     stream = torch.cuda.current_stream(device)
 
     for _ in range(args.warmup):
@@ -233,8 +239,7 @@ def measure(args, workload, dtype, world, rank, local, device, with_cpu):
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": ("vbc::spmv_ranges<T, 0, K, P> (+ vbc::fixup)" if k == 1 else
-                       "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"),
+            "kernel": kernel_name,
             "bytes_per_launch": bytes_rank,
             "avg_launch_ms": round(kernel_ms, 5),
             "traffic_source": traffic_src,

@@ -136,7 +136,7 @@ typedef struct vbc_info {
     int64_t bytes_t;        /* HBM bytes one transposed product moves in this layout */
     int64_t bytes_f;        /* same for the forward product */
     int32_t bins_m;         /* width buckets of the multi-RHS panel layout (0 = absent) */
-    int32_t reserved_;
+    int32_t slot_bins;      /* buckets laid out slotted (vbc_slots.h), both directions */
     int64_t bytes_m;        /* matrix bytes (keys + values, panel-padded) one panel pass streams */
 } vbc_info;
 

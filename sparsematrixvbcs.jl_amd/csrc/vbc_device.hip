@@ -61,6 +61,9 @@ struct Launch {
     int nfill = 0;
     size_t o_fill = 0;             // arena offset of the fill list (y indices)
     const int32_t *d_fill = nullptr;
+    std::vector<SlotBin> sbins;    // slotted buckets (vbc_slots.h), launched before the merge kernel
+    SlotBin *d_sbins = nullptr;
+    int slot_ranges = 0;
 };
 
 // The panel layout of the MFMA multi-RHS transposed product (vbc_panel.h): one launch.
@@ -107,6 +110,14 @@ struct vbc_handle {
     int tile_k = vbc::kTileKDefault;  // entries per slot per tile
     int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
     int diag = 0;                     // ablation variant (VBC_DIAG; tools/ab.py only)
+    int target_ranges_s[2] = {4096, 4096};  // resident waves of the slotted kernels
+    int slots_mode = -1;              // VBC_SLOTS: -1 auto, 0 never, 1 always (when representable)
+    double slots_pad = 1.10;          // auto: largest padded/real row ratio of a slotted bucket
+    int xcd = 0;                      // VBC_XCD=1: XCD-contiguous range order in the slotted kernel (measured slower)
+    int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)
+    int64_t slot_rows_padded_last = 0;
+    int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
+    int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
 };
 
 namespace vbc {
@@ -218,6 +229,138 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     return VBC_OK;
 }
 
+// ---- slotted layout (vbc_slots.h) ----------------------------------------------------------------
+
+struct PendingSlot {
+    SlotBin b;
+    size_t o_key, o_val, o_out, o_rrow, o_rchunk;
+};
+
+// Slots per chunk of a bucket stored w wide (lane-vector width as in the kernel).
+static int slot_rpi(int esz, int w)
+{
+    const int V = w <= 8 ? vec_elems(esz, w) : 1;
+    return 64 / (w / V);
+}
+
+// Rows of each chunk: the longest segment of its RPI (>= 1, so every chunk closes).
+static std::vector<int32_t> chunk_rows(const std::vector<int64_t> &sbeg, int RPI)
+{
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    std::vector<int32_t> cr((nseg + RPI - 1) / RPI, 1);
+    for (int64_t q = 0; q < nseg; q++)
+        cr[q / RPI] = (int32_t)std::max<int64_t>(cr[q / RPI], sbeg[q + 1] - sbeg[q]);
+    return cr;
+}
+
+// Whether a bucket (segments sbeg over `real` entries) runs slotted: auto mode asks for a padded row
+// count within slots_pad of the real one and chunks short enough to balance over the ranges.
+static bool want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
+                       int64_t total_entries, int64_t gather_limit)
+{
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    const int64_t real = nseg > 0 ? sbeg[nseg] - sbeg[0] : 0;
+    if (h->slots_mode == 0 || real == 0 || gather_limit >= (int64_t)kSlotIdxLimit) return false;
+    if (nseg >= (int64_t(1) << 31)) return false;
+    const int RPI = slot_rpi(h->esz, w);
+    const std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
+    int64_t rows = 0, longest = 0;
+    for (int32_t c : cr) { rows += c; longest = std::max<int64_t>(longest, c); }
+    if (rows * RPI >= (int64_t(1) << 31)) return false;
+    if (h->slots_mode == 1) return true;
+    const double ratio = (double)(rows * RPI) / (double)real;
+    const double share = (double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    const double rows_per_range = (double)rows / std::max(1.0, share);
+    return ratio <= h->slots_pad && (double)longest <= std::max(32.0, 0.5 * rows_per_range);
+}
+
+// Lay out a slotted bucket: chunk rows row-major over the slots, PAD / LAST keys, ranges of whole
+// chunks balanced by rows.  ents[sbeg[q] ...] are segment q's entries (keys = gather index only).
+static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vector<Entry> &ents,
+                       const std::vector<int64_t> &sbeg, const std::vector<int32_t> &out, int64_t total_entries,
+                       const char *val, Arena &ar, int &range0, PendingSlot &ps)
+{
+    const int esz = h->esz;
+    const int RPI = slot_rpi(esz, w);
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    const int64_t real = sbeg[nseg] - sbeg[0];
+    const std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
+    const int64_t nch = (int64_t)cr.size();
+    int64_t rows = 0;
+    for (int32_t c : cr) rows += c;
+    int64_t nr = (int64_t)std::llround((double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1));
+    nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
+    std::vector<int32_t> rrow{0}, rchunk{0};
+    int64_t acc = 0;
+    for (int64_t c = 0; c < nch; c++) {
+        acc += cr[c];
+        if (c + 1 < nch && (int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows) {
+            rrow.push_back((int32_t)acc);
+            rchunk.push_back((int32_t)(c + 1));
+        }
+    }
+    rrow.push_back((int32_t)rows);
+    nr = (int64_t)rchunk.size();
+    ps = PendingSlot{};
+    SlotBin &b = ps.b;
+    b.kind = kind;
+    b.wkey = w <= 8 ? w : 0;
+    b.w = w;
+    b.wst = wsrc;
+    b.rpi = RPI;
+    b.range0 = range0;
+    b.nranges = (int32_t)nr;
+    b.nseg = (int32_t)nseg;
+    b.u = h->slot_u;
+    b.diag = h->diag;
+    b.out_affine = 1;
+    b.out_base = out.empty() ? 0 : out[0];
+    b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
+    for (size_t q = 1; q < out.size() && b.out_affine; q++)
+        b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * b.out_stride;
+    if (getenv("VBC_NO_AFFINE")) b.out_affine = 0;  // A/B knob
+    {
+        const int V = w <= 8 ? vec_elems(esz, w) : 1;
+        const bool full = RPI * (w / V) == 64 && V * esz <= 16;
+        b.contig = b.out_affine && (kind == 0 ? (full && wsrc == w && (nseg <= 1 || b.out_stride == w))
+                                              : (nseg <= 1 || b.out_stride == 1));
+    }
+    range0 += (int)nr;
+    const int64_t E = rows * RPI;
+    ps.o_key = ar.reserve(E * 4);
+    ps.o_val = ar.reserve(E * w * esz);
+    ps.o_out = ar.reserve(std::max<size_t>(out.size(), 1) * 4);
+    ps.o_rrow = ar.reserve(rrow.size() * 4);
+    ps.o_rchunk = ar.reserve(rchunk.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_out), out.data(), out.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_rrow), rrow.data(), rrow.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_rchunk), rchunk.data(), rchunk.size() * 4);
+    uint32_t *key = ar.at<uint32_t>(ps.o_key);
+    char *vv = ar.at<char>(ps.o_val);
+    int64_t row = 0;
+    for (int64_t c = 0; c < nch; c++) {
+        for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
+            const uint32_t last = qr + 1 == cr[c] ? kLast : 0u;
+            for (int sl = 0; sl < RPI; sl++) {
+                const int64_t seg = c * RPI + sl, e = row * RPI + sl;
+                if (seg < nseg && sbeg[seg] + qr < sbeg[seg + 1]) {
+                    const Entry &en = ents[sbeg[seg] + qr];
+                    key[e] = en.key | last;
+                    std::memcpy(vv + e * w * esz, val + en.voff * esz, (size_t)wsrc * esz);
+                    if (wsrc < w) std::memset(vv + (e * w + wsrc) * esz, 0, (size_t)(w - wsrc) * esz);
+                } else {
+                    key[e] = kPad | last;  // gathers x[0] (m >= 1: the bucket has entries), taken as 0
+                    std::memset(vv + e * w * esz, 0, (size_t)w * esz);
+                }
+            }
+        }
+    }
+    h->slot_rows_padded += E;
+    h->slot_rows_real += real;
+    h->slot_rows_padded_last = E;
+    return VBC_OK;
+}
+
 // Stored width of a transposed bucket.  Widths whose rows do not split into 16-B lane vectors
 // with a power-of-two slot count (w = 3, 5, 6, 7) run the shuffle-scan path with 4-8-B loads; padding
 // them with zero columns buys 16-B loads and the DPP scan for 14-60 % more value bytes.  The padding
@@ -241,43 +384,67 @@ static int padded_width(const vbc_handle *h, int w)
     return wp;
 }
 
-// Transposed layout: segments = non-empty stripes of each width, entries = their stored rows.
+// Transposed layout: segments = stripes of each width, entries = their stored rows.  A bucket runs
+// slotted (vbc_slots.h, every stripe of the width a segment, empty ones included) when its row counts
+// are near-uniform, else merged (non-empty stripes; empty ones go to the fill list).
 static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                            std::vector<PendingBin> &pbs, Launch &L, std::vector<int32_t> &fill)
+                            std::vector<PendingBin> &pbs, std::vector<PendingSlot> &pss, Launch &L,
+                            std::vector<int32_t> &fill)
 {
     std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
-    for (int64_t l = 0; l < s.L; l++) {
-        if (s.rbeg[l + 1] > s.rbeg[l]) buckets[s.w[l]].push_back(l);
-        else for (int c = 0; c < s.w[l]; c++) fill.push_back((int32_t)(s.col0[l] + c));
-    }
+    for (int64_t l = 0; l < s.L; l++) buckets[s.w[l]].push_back(l);
     const int64_t total = (int64_t)s.rows.size();
-    int range0 = 0;
+    int range0 = 0, srange0 = 0;
     for (auto &kv : buckets) {
         const int w = kv.first;
+        const int wp = padded_width(h, w);
+        std::vector<int64_t> sbeg{0};
+        for (int64_t l : kv.second) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
+        if (want_slots(h, 0, wp, sbeg, total, s.m)) {
+            std::vector<Entry> ents;
+            std::vector<int32_t> out;
+            ents.reserve(sbeg.back());
+            for (int64_t l : kv.second) {
+                out.push_back((int32_t)s.col0[l]);
+                for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
+                    ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+            }
+            PendingSlot ps;
+            if (int st = build_slots(h, 0, wp, w, ents, sbeg, out, total, val, ar, srange0, ps)) return st;
+            h->bytes_t += ps.b.nranges > 0 ? (int64_t)(h->slot_rows_padded_last) * (4 + (int64_t)wp * h->esz) : 0;
+            pss.push_back(ps);
+            continue;
+        }
         std::vector<Entry> ents;
         std::vector<int32_t> out;
         for (int64_t l : kv.second) {
+            if (s.rbeg[l + 1] == s.rbeg[l]) {
+                for (int c = 0; c < s.w[l]; c++) fill.push_back((int32_t)(s.col0[l] + c));
+                continue;
+            }
             out.push_back((int32_t)s.col0[l]);
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
                 ents.push_back({(uint32_t)s.rows[r] | (r == s.rbeg[l] ? kHead : 0u),
                                 s.voff[l] + (r - s.rbeg[l]) * w});
         }
+        if (ents.empty()) continue;
         PendingBin pb;
-        const int wp = padded_width(h, w);
         if (int st = build_bucket(h, 0, wp, ents, out, total, val, ar, range0, pb, w)) return st;
         h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)wp * h->esz) + (int64_t)out.size() * 4;
         pbs.push_back(pb);
     }
     L.total_ranges = range0;
+    L.slot_ranges = srange0;
     h->bytes_t += (s.m + s.n) * h->esz;  // x read once, y written once
     return VBC_OK;
 }
 
 // Forward layout: per width bucket, segments = output rows with entries of that width (ascending),
-// entries = (row, stripe) blocks ordered by stripe within the row.
+// entries = (row, stripe) blocks ordered by stripe within the row.  With a single bucket, a slotted
+// layout takes every row as a segment (affine, no fill list).
 static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                         std::vector<std::vector<PendingBin>> &pbs, std::vector<Launch> &Ls,
-                         std::vector<int32_t> &fill)
+                         std::vector<std::vector<PendingBin>> &pbs, std::vector<std::vector<PendingSlot>> &pss,
+                         std::vector<Launch> &Ls, std::vector<int32_t> &fill)
 {
     std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
     for (int64_t l = 0; l < s.L; l++)
@@ -290,14 +457,32 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
         for (int64_t l : kv.second)
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) cnt[s.rows[r] + 1]++;
         for (int64_t i = 0; i < s.m; i++) cnt[i + 1] += cnt[i];
+        const bool single = buckets.size() == 1;
+        std::vector<int64_t> sbeg{0};
+        std::vector<int32_t> sout;
+        for (int64_t i = 0; i < s.m; i++)
+            if (single || cnt[i + 1] > cnt[i]) { sbeg.push_back(cnt[i + 1]); sout.push_back((int32_t)i); }
+        const bool slotted = want_slots(h, 1, w, sbeg, (int64_t)cnt[s.m], s.n);
         std::vector<Entry> ents(cnt[s.m]);
         for (int64_t i = 0; i < s.m; i++) cur[i] = cnt[i];
         for (int64_t l : kv.second)
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) {
                 const int64_t i = s.rows[r];
                 const int64_t e = cur[i]++;
-                ents[e] = {(uint32_t)s.col0[l] | (e == cnt[i] ? kHead : 0u), s.voff[l] + (r - s.rbeg[l]) * w};
+                ents[e] = {(uint32_t)s.col0[l] | (!slotted && e == cnt[i] ? kHead : 0u), s.voff[l] + (r - s.rbeg[l]) * w};
             }
+        Ls.emplace_back();
+        if (slotted) {
+            PendingSlot ps;
+            int srange0 = 0;
+            if (int st = build_slots(h, 1, w, w, ents, sbeg, sout, (int64_t)ents.size(), val, ar, srange0, ps)) return st;
+            h->bytes_f += (int64_t)h->slot_rows_padded_last * (4 + (int64_t)w * h->esz) + (int64_t)sout.size() * h->esz;
+            for (int32_t i : sout) any[i] = 1;
+            pbs.push_back({});
+            pss.push_back({ps});
+            Ls.back().slot_ranges = srange0;
+            continue;
+        }
         std::vector<int32_t> out;
         for (int64_t i = 0; i < s.m; i++)
             if (cnt[i + 1] > cnt[i]) { out.push_back((int32_t)i); any[i] = 1; }
@@ -306,7 +491,7 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
         if (int st = build_bucket(h, 1, w, ents, out, (int64_t)ents.size(), val, ar, range0, pb)) return st;
         h->bytes_f += (int64_t)ents.size() * (4 + (int64_t)w * h->esz) + (int64_t)out.size() * (4 + h->esz);
         pbs.push_back({pb});
-        Ls.emplace_back();
+        pss.push_back({});
         Ls.back().total_ranges = range0;
     }
     h->f_scale = buckets.size() > 1;
@@ -456,9 +641,11 @@ static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, P
     return VBC_OK;
 }
 
-static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, Launch &L)
+static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, const std::vector<PendingSlot> &pss,
+                           Launch &L)
 {
     L.bins.clear();
+    L.sbins.clear();
     char *base = static_cast<char *>(h->d_arena);
     for (const PendingBin &pb : pbs) {
         Bin b = pb.b;
@@ -470,10 +657,23 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, La
         b.carry_seg = reinterpret_cast<int32_t *>(base + pb.o_cseg);
         L.bins.push_back(b);
     }
+    for (const PendingSlot &ps : pss) {
+        SlotBin b = ps.b;
+        b.key = reinterpret_cast<const uint32_t *>(base + ps.o_key);
+        b.val = base + ps.o_val;
+        b.out = reinterpret_cast<const int32_t *>(base + ps.o_out);
+        b.rrow = reinterpret_cast<const int32_t *>(base + ps.o_rrow);
+        b.rchunk = reinterpret_cast<const int32_t *>(base + ps.o_rchunk);
+        L.sbins.push_back(b);
+    }
     L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
     if (!L.bins.empty()) {
         VBC_HIP(hipMalloc(&L.d_bins, L.bins.size() * sizeof(Bin)));
         VBC_HIP(hipMemcpy(L.d_bins, L.bins.data(), L.bins.size() * sizeof(Bin), hipMemcpyHostToDevice));
+    }
+    if (!L.sbins.empty()) {
+        VBC_HIP(hipMalloc(&L.d_sbins, L.sbins.size() * sizeof(SlotBin)));
+        VBC_HIP(hipMemcpy(L.d_sbins, L.sbins.data(), L.sbins.size() * sizeof(SlotBin), hipMemcpyHostToDevice));
     }
     return VBC_OK;
 }
@@ -483,9 +683,12 @@ static void release(vbc_handle *h)
     if (!h) return;
     DeviceGuard g(h->device);
     if (h->lt.d_bins) (void)hipFree(h->lt.d_bins);
+    if (h->lt.d_sbins) (void)hipFree(h->lt.d_sbins);
     if (h->lm.d_bins) (void)hipFree(h->lm.d_bins);
-    for (auto &l : h->lf)
+    for (auto &l : h->lf) {
         if (l.d_bins) (void)hipFree(l.d_bins);
+        if (l.d_sbins) (void)hipFree(l.d_sbins);
+    }
     if (h->d_arena) (void)hipFree(h->d_arena);
     if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
     delete h;
@@ -554,6 +757,15 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     for (int kd = 0; kd < 2; kd++)
         h->target_ranges_k[kd] = prop.multiProcessorCount * std::max(1, std::min(occ[kd], 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
+    for (int kd = 0; kd < 2; kd++)
+        h->target_ranges_s[kd] = prop.multiProcessorCount * std::max(1, std::min(occupancy_slots(h->esz, kd), 8)) * kWavesPerBlock;
+    if (const char *e = getenv("VBC_TARGET_RANGES_S")) h->target_ranges_s[0] = h->target_ranges_s[1] = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
+    if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
+    h->slot_u = h->esz == 8 ? 8 : 16;  // measured (tools/ab.py, FE): 4 / 8 rows are 4-8 % slower
+    if (const char *e = getenv("VBC_SLOT_U")) h->slot_u = h->esz == 8 ? (atoi(e) == 4 ? 4 : 8) : (atoi(e) == 8 ? 8 : 16);
     if (flags & VBC_CREATE_MULTI) {
         int om = 0;
         if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1, true, true>, kBlockThreads, 0);
@@ -567,7 +779,9 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
 
     Arena ar;
     std::vector<PendingBin> pt;
+    std::vector<PendingSlot> st_t;
     std::vector<std::vector<PendingBin>> pf;
+    std::vector<std::vector<PendingSlot>> sf;
     std::vector<PendingPanel> pm;
     std::vector<int32_t> fill_t, fill_f, fill_m;
     int st = VBC_OK;
@@ -581,7 +795,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         }
     }
     if (st == VBC_OK && (flags & VBC_CREATE_TRANSPOSED)) {
-        st = build_transposed(h, s, v, ar, pt, h->lt, fill_t);
+        st = build_transposed(h, s, v, ar, pt, st_t, h->lt, fill_t);
         h->has_t = st == VBC_OK;
         if (st == VBC_OK) {
             h->lt.nfill = (int)fill_t.size();
@@ -590,7 +804,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         }
     }
     if (st == VBC_OK && (flags & VBC_CREATE_FORWARD)) {
-        st = build_forward(h, s, v, ar, pf, h->lf, fill_f);
+        st = build_forward(h, s, v, ar, pf, sf, h->lf, fill_f);
         h->has_f = st == VBC_OK;
         if (st == VBC_OK) {
             if (h->lf.empty()) h->lf.emplace_back();  // no entries: the fill list alone writes y
@@ -610,21 +824,46 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         release(h);
         return fail(VBC_HIP_ERROR, "hipMemcpy of the matrix arena failed");
     }
-    if (h->has_t && (st = finalize_launch(h, pt, h->lt))) { release(h); return st; }
+    if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt))) { release(h); return st; }
     if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)
-        if ((st = finalize_launch(h, pf[b], h->lf[b]))) { release(h); return st; }
-    if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, h->lf[0]))) { release(h); return st; }
+        if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b]))) { release(h); return st; }
+    if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
     *out = h;
     return VBC_OK;
 }
 
 template <typename T>
 static int launch(const Launch &L, int kind, const void *x, void *y, double alpha, double beta, bool rd,
-                  hipStream_t stream)
+                  hipStream_t stream, int xcd, int slot_stage)
 {
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
+    if (L.slot_ranges > 0) {
+        bool faste = !rd, contig = true;
+        for (const SlotBin &sb : L.sbins) {
+            faste = faste && sb.out_affine;
+            contig = contig && sb.contig;
+        }
+        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
+        // auto (-1): stage when the per-lane store is narrower than 16 B (kind 0: V * esz < 16, kind 1:
+        // fp32) -- measured: fp32 FE B'x 134 -> 118 us, fp64 (16-B lane stores already) slower staged
+        int stage = slot_stage;
+        if (stage < 0) {
+            stage = 8;
+            for (const SlotBin &sb : L.sbins) {
+                const int V = sb.w <= 8 ? vec_elems((int)sizeof(T), sb.w) : 1;
+                if (kind == 0 ? V * (int)sizeof(T) >= 16 : sizeof(T) == 8) stage = 0;
+            }
+        }
+        if (!(faste && contig)) stage = 0;
+        const hipError_t e = (hipError_t)launch_slots((int)sizeof(T), kind, L.d_sbins, (int)L.sbins.size(), L.slot_ranges,
+                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, x, y, alpha, beta, rd, stream);
+        if (e != hipSuccess) {
+            set_error("spmv_slots launch failed: %s", hipGetErrorString(e));
+            return VBC_HIP_ERROR;
+        }
+    }
     if (L.total_ranges > 0) {
         const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
         const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;
@@ -686,7 +925,7 @@ static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, do
 {
     if (trans) {
         if (h->n == 0) return VBC_OK;
-        return launch<T>(h->lt, 0, x, y, alpha, beta, beta != 0.0, stream);
+        return launch<T>(h->lt, 0, x, y, alpha, beta, beta != 0.0, stream, h->xcd, h->slot_stage);
     }
     if (h->m == 0) return VBC_OK;
     if (h->f_scale) {
@@ -697,7 +936,7 @@ static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, do
     for (size_t b = 0; b < h->lf.size(); b++) {
         const bool own_beta = !h->f_scale;
         if (int st = launch<T>(h->lf[b], 1, x, y, alpha, own_beta ? beta : 1.0, own_beta ? beta != 0.0 : true,
-                               stream))
+                               stream, h->xcd, h->slot_stage))
             return st;
     }
     return VBC_OK;
@@ -974,6 +1213,9 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
     info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : 0;
+    int32_t sl = h->has_t ? (int32_t)h->lt.sbins.size() : 0;
+    for (auto &l : h->lf) sl += h->has_f ? (int32_t)l.sbins.size() : 0;
+    info->slot_bins = sl;
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }
@@ -1064,6 +1306,7 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
     }
     bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t;
     for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
+    fused = fused && h->lt.sbins.empty();  // the fused vector kernel reads the merge layout only
     if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
         const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
         const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;

@@ -69,6 +69,44 @@ struct Bin {
     int32_t *carry_seg;   // per range: continued segment, or -1
 };
 
+// One width bucket in the slotted layout (vbc_slots.h): chunks of RPI segments, one slot each.
+struct SlotBin {
+    int32_t kind;        // 0: B'x, 1: Bx
+    int32_t wkey;        // dispatch width: 1..8, or 0 = runtime width (w > 8)
+    int32_t w;           // entry width as laid out
+    int32_t wst;         // columns actually written (<= w)
+    int32_t rpi;         // slots per chunk
+    int32_t range0;      // first range (wave) of this bucket in the launch
+    int32_t nranges;
+    int32_t nseg;        // segments (the last chunk may be partial)
+    int32_t out_affine;  // 1: out[s] == out_base + s * out_stride
+    int32_t out_base;
+    int32_t out_stride;
+    int32_t u;           // rows per pipeline step of the launch (4 / 8 fp64, 8 / 16 fp32)
+    int32_t diag;        // ablation variant (0 = production)
+    int32_t contig;      // affine and chunk outputs contiguous in y (LDS-staged writes allowed)
+    const uint32_t *key;   // rows * rpi: PAD | LAST | gather index
+    const void *val;       // rows * rpi * w values
+    const int32_t *out;    // per segment (when not affine)
+    const int32_t *rrow;   // per range: first row, nranges + 1 entries
+    const int32_t *rchunk; // per range: first chunk
+};
+
+__device__ __forceinline__ int out_of_slots(const SlotBin &b, int seg)
+{
+    return b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
+}
+
+constexpr uint32_t kPad = 0x80000000u;   // slotted layout: padding row (x taken as 0)
+constexpr uint32_t kLast = 0x40000000u;  // slotted layout: last row of a chunk
+constexpr uint32_t kSlotIdx = 0x3FFFFFFFu;
+constexpr int64_t kSlotIdxLimit = int64_t(1) << 30;  // gather indices of the slotted layout (30 bits)
+
+// Launches spmv_slots (vbc_slots.hip): returns the hipError_t of the launch.
+int launch_slots(int esz, int kind, const SlotBin *d_bins, int nbins, int total_ranges, bool faste, int xcd, int u, int diag, int stage,
+                 const void *x, void *y, double alpha, double beta, bool rd, hipStream_t stream);
+int occupancy_slots(int esz, int kind);
+
 __host__ __device__ constexpr int vec_elems(int esz, int w)
 {
     return esz == 8 ? (w % 2 == 0 ? 2 : 1) : (w % 4 == 0 ? 4 : (w % 2 == 0 ? 2 : 1));
