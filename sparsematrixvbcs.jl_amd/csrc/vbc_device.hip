@@ -11,9 +11,7 @@
 #include <type_traits>
 #include <vector>
 
-#include "vbc_internal.h"
-#include "vbc_kernels.h"
-#include "vbc_panel.h"
+#include "vbc_handle.h"
 
 namespace vbc {
 
@@ -29,15 +27,6 @@ void set_error(const char *fmt, ...)
     g_err = buf;
 }
 
-#define VBC_HIP(call)                                                                             \
-    do {                                                                                          \
-        hipError_t e_ = (call);                                                                   \
-        if (e_ != hipSuccess) {                                                                   \
-            set_error("%s failed: %s", #call, hipGetErrorString(e_));                             \
-            return VBC_HIP_ERROR;                                                                 \
-        }                                                                                         \
-    } while (0)
-
 // Restores the caller's current device on scope exit.
 struct DeviceGuard {
     int prev = -1;
@@ -52,75 +41,6 @@ struct DeviceGuard {
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
-
-// One fused launch of spmv_ranges (+ its fix-up pass).
-struct Launch {
-    std::vector<Bin> bins;
-    Bin *d_bins = nullptr;
-    int total_ranges = 0;
-    int nfill = 0;
-    size_t o_fill = 0;             // arena offset of the fill list (y indices)
-    const int32_t *d_fill = nullptr;
-    std::vector<SlotBin> sbins;    // slotted buckets (vbc_slots.h), launched before the merge kernel
-    SlotBin *d_sbins = nullptr;
-    int slot_ranges = 0;
-};
-
-// The panel layout of the MFMA multi-RHS transposed product (vbc_panel.h): one launch.
-struct PanelLaunch {
-    std::vector<PanelBin> bins;
-    PanelBin *d_bins = nullptr;
-    int total_ranges = 0;
-    int nfill = 0;
-    size_t o_fill = 0;
-    const int32_t *d_fill = nullptr;
-};
-
-// Host description of the input stripes, common to 1D, 2D (expanded) and CSC inputs.
-struct Stripes {
-    int64_t m = 0, n = 0, L = 0;
-    std::vector<int64_t> col0;  // 0-based first column of stripe l
-    std::vector<int32_t> w;     // width
-    std::vector<int64_t> rbeg;  // L+1 prefix into rows
-    std::vector<int32_t> rows;  // 0-based x row of each stored w-wide row
-    std::vector<int64_t> voff;  // element offset of the stripe's first value in the input val
-};
-
-}  // namespace vbc
-
-struct vbc_handle {
-    int64_t m = 0, n = 0, L = 0, K = 0, nblocks = 0, nrows = 0, nval = 0, nnz = 0;
-    int dtype = 0, esz = 8, device = 0;
-    void *d_arena = nullptr;
-    size_t arena_bytes = 0;
-    bool has_t = false, has_f = false, has_m = false;
-    vbc::PanelLaunch lm;          // multi-RHS transposed product on matrix cores (VBC_CREATE_MULTI)
-    int64_t bytes_m = 0;          // matrix bytes one panel product streams
-    int target_ranges_m = 4096;
-    int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
-    int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
-    int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
-    vbc::Launch lt;               // transposed product: all buckets in one launch
-    std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
-    bool f_scale = false;         // forward with several buckets: scale y by beta first
-    int64_t bytes_t = 0, bytes_f = 0;
-    void *d_carry_mm = nullptr;   // multi-RHS carry slots (allocated on first use)
-    size_t carry_mm_bytes = 0;
-    int target_ranges_k[2] = {4096, 4096};  // resident waves of the B'x / Bx kernels (one range each)
-    int tile_k = vbc::kTileKDefault;  // entries per slot per tile
-    int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
-    int diag = 0;                     // ablation variant (VBC_DIAG; tools/ab.py only)
-    int target_ranges_s[2] = {4096, 4096};  // resident waves of the slotted kernels
-    int slots_mode = -1;              // VBC_SLOTS: -1 auto, 0 never, 1 always (when representable)
-    double slots_pad = 1.10;          // auto: largest padded/real row ratio of a slotted bucket
-    int xcd = 0;                      // VBC_XCD=1: XCD-contiguous range order in the slotted kernel (measured slower)
-    int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)
-    int64_t slot_rows_padded_last = 0;
-    int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
-    int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
-};
-
-namespace vbc {
 
 // Arena builder: reserves aligned regions, fills a host image, uploads once.
 struct Arena {
@@ -743,17 +663,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_DIAG")) h->diag = atoi(e);
     // one range per resident wave: occupancy of the kernel variant this handle will launch
     int occ[2] = {0, 0};
-#define VBC_OCC(TT, KK, PP)                                                                           \
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], spmv_ranges<TT, 0, KK, PP>, kBlockThreads, 0); \
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], spmv_ranges<TT, 1, KK, PP>, kBlockThreads, 0)
-    if (dtype == VBC_F64) {
-        if (h->tile_k == 4) { if (h->pipe == 2) { VBC_OCC(double, 4, 2); } else { VBC_OCC(double, 4, 3); } }
-        else { if (h->pipe == 2) { VBC_OCC(double, 8, 2); } else { VBC_OCC(double, 8, 3); } }
-    } else {
-        if (h->tile_k == 4) { if (h->pipe == 2) { VBC_OCC(float, 4, 2); } else { VBC_OCC(float, 4, 3); } }
-        else { if (h->pipe == 2) { VBC_OCC(float, 8, 2); } else { VBC_OCC(float, 8, 3); } }
-    }
-#undef VBC_OCC
+    occupancy_ranges(h->esz, h->tile_k, h->pipe, occ);
     for (int kd = 0; kd < 2; kd++)
         h->target_ranges_k[kd] = prop.multiProcessorCount * std::max(1, std::min(occ[kd], 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
@@ -767,9 +677,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     h->slot_u = h->esz == 8 ? 8 : 16;  // measured (tools/ab.py, FE): 4 / 8 rows are 4-8 % slower
     if (const char *e = getenv("VBC_SLOT_U")) h->slot_u = h->esz == 8 ? (atoi(e) == 4 ? 4 : 8) : (atoi(e) == 8 ? 8 : 16);
     if (flags & VBC_CREATE_MULTI) {
-        int om = 0;
-        if (dtype == VBC_F64) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<double, 1, true, true>, kBlockThreads, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&om, spmm_panel<float, 1, true, true>, kBlockThreads, 0);
+        const int om = occupancy_panel(h->esz);
         h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
         if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
         if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
@@ -830,224 +738,6 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b]))) { release(h); return st; }
     if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
     *out = h;
-    return VBC_OK;
-}
-
-template <typename T>
-static int launch(const Launch &L, int kind, const void *x, void *y, double alpha, double beta, bool rd,
-                  hipStream_t stream, int xcd, int slot_stage)
-{
-    const T *xs = static_cast<const T *>(x);
-    T *ys = static_cast<T *>(y);
-    if (L.slot_ranges > 0) {
-        bool faste = !rd, contig = true;
-        for (const SlotBin &sb : L.sbins) {
-            faste = faste && sb.out_affine;
-            contig = contig && sb.contig;
-        }
-        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
-        // auto (-1): stage when the per-lane store is narrower than 16 B (kind 0: V * esz < 16, kind 1:
-        // fp32) -- measured: fp32 FE B'x 134 -> 118 us, fp64 (16-B lane stores already) slower staged
-        int stage = slot_stage;
-        if (stage < 0) {
-            stage = 8;
-            for (const SlotBin &sb : L.sbins) {
-                const int V = sb.w <= 8 ? vec_elems((int)sizeof(T), sb.w) : 1;
-                if (kind == 0 ? V * (int)sizeof(T) >= 16 : sizeof(T) == 8) stage = 0;
-            }
-        }
-        if (!(faste && contig)) stage = 0;
-        const hipError_t e = (hipError_t)launch_slots((int)sizeof(T), kind, L.d_sbins, (int)L.sbins.size(), L.slot_ranges,
-                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, x, y, alpha, beta, rd, stream);
-        if (e != hipSuccess) {
-            set_error("spmv_slots launch failed: %s", hipGetErrorString(e));
-            return VBC_HIP_ERROR;
-        }
-    }
-    if (L.total_ranges > 0) {
-        const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
-        const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;
-        // load-free owner writes when every bucket maps segments affinely and beta = 0
-        bool faste = !rd;
-        for (const Bin &bb : L.bins) faste = faste && bb.out_affine;
-        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
-#define VBC_LAUNCH(KIND, KK, PP)                                                                         \
-    do {                                                                                                 \
-        if (faste)                                                                                       \
-            hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP, 0, true>), dim3(grid), dim3(kBlockThreads), 0, stream, \
-                               L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
-        else                                                                                             \
-            hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP>), dim3(grid), dim3(kBlockThreads), 0, stream, \
-                               L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
-    } while (0)
-        const int P = L.bins.empty() ? kPipeDefault : L.bins[0].pipe;
-        const int D = L.bins.empty() ? 0 : L.bins[0].diag;
-        if constexpr (std::is_same<T, double>::value) {
-            if (kind == 0 && K == 4 && P == 2 && D == 1) {
-                hipLaunchKernelGGL((spmv_ranges<T, 0, 4, 2, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                                   (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
-                return VBC_OK;
-            }
-            if (kind == 0 && K == 4 && P == 2 && D == 2) {
-                hipLaunchKernelGGL((spmv_ranges<T, 0, 4, 2, 2>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                                   (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
-                return VBC_OK;
-            }
-        }
-        if (kind == 0) {
-            if (P == 2) { if (K == 4) VBC_LAUNCH(0, 4, 2); else VBC_LAUNCH(0, 8, 2); }
-            else { if (K == 4) VBC_LAUNCH(0, 4, 3); else VBC_LAUNCH(0, 8, 3); }
-        } else {
-            if (P == 2) { if (K == 4) VBC_LAUNCH(1, 4, 2); else VBC_LAUNCH(1, 8, 2); }
-            else { if (K == 4) VBC_LAUNCH(1, 4, 3); else VBC_LAUNCH(1, 8, 3); }
-        }
-#undef VBC_LAUNCH
-        VBC_HIP(hipGetLastError());
-    }
-    const int work = (L.total_ranges > 1 ? L.total_ranges : 0) + L.nfill;
-    if (work > 0) {
-        const int nr = L.total_ranges > 1 ? L.total_ranges : 0;
-        const int grid = (work + kBlockThreads - 1) / kBlockThreads;
-        if (kind == 0)
-            hipLaunchKernelGGL((fixup<T, 0>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                               (int)L.bins.size(), nr, L.d_fill, L.nfill, ys, (T)alpha, (T)beta, (int)rd);
-        else
-            hipLaunchKernelGGL((fixup<T, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
-                               (int)L.bins.size(), nr, L.d_fill, L.nfill, ys, (T)alpha, (T)beta, (int)rd);
-        VBC_HIP(hipGetLastError());
-    }
-    return VBC_OK;
-}
-
-template <typename T>
-static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
-                      hipStream_t stream)
-{
-    if (trans) {
-        if (h->n == 0) return VBC_OK;
-        return launch<T>(h->lt, 0, x, y, alpha, beta, beta != 0.0, stream, h->xcd, h->slot_stage);
-    }
-    if (h->m == 0) return VBC_OK;
-    if (h->f_scale) {
-        hipLaunchKernelGGL((scale<T>), dim3(std::min<int64_t>((h->m + kBlockThreads - 1) / kBlockThreads, 4096)),
-                           dim3(kBlockThreads), 0, stream, static_cast<T *>(y), h->m, (T)beta, (int)(beta != 0.0));
-        VBC_HIP(hipGetLastError());
-    }
-    for (size_t b = 0; b < h->lf.size(); b++) {
-        const bool own_beta = !h->f_scale;
-        if (int st = launch<T>(h->lf[b], 1, x, y, alpha, own_beta ? beta : 1.0, own_beta ? beta != 0.0 : true,
-                               stream, h->xcd, h->slot_stage))
-            return st;
-    }
-    return VBC_OK;
-}
-
-static int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, double alpha,
-                        double beta, hipStream_t stream)
-{
-    return h->dtype == VBC_F64 ? mul_device<double>(h, trans, x, y, alpha, beta, stream)
-                               : mul_device<float>(h, trans, x, y, alpha, beta, stream);
-}
-
-// Multi-RHS transposed product on the tiled stream (row-major X / Y), in chunks of <= 64 columns.
-template <typename T>
-static int mulmat_t_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy,
-                             double alpha, double beta, hipStream_t s)
-{
-    const Launch &L = h->lt;
-    const int NRmax = 64;
-    int64_t stride = 1;
-    for (const Bin &b : L.bins) stride = std::max<int64_t>(stride, (int64_t)b.nranges * b.w * NRmax);
-    const size_t need = (size_t)std::max<size_t>(L.bins.size(), 1) * stride * sizeof(T);
-    if (h->carry_mm_bytes < need) {
-        if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
-        h->d_carry_mm = nullptr;
-        h->carry_mm_bytes = 0;
-        VBC_HIP(hipMalloc(&h->d_carry_mm, need));
-        h->carry_mm_bytes = need;
-    }
-    T *cm = static_cast<T *>(h->d_carry_mm);
-    const bool rd = beta != 0.0;
-    for (int64_t c0 = 0; c0 < nrhs; c0 += NRmax) {
-        const int nr = (int)std::min<int64_t>(NRmax, nrhs - c0);
-        const T *xs = reinterpret_cast<const T *>(X) + c0;
-        T *ys = reinterpret_cast<T *>(Y) + c0;
-        const int NR = nr <= 16 ? 16 : 64;
-        const int64_t cs = nr <= 16 ? stride / 4 : stride;  // carry slots are sized per NR
-        if (L.total_ranges > 0) {
-            const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
-            const int K = L.bins[0].tile_k;
-#define VBC_MM(NRR, KK)                                                                                  \
-    hipLaunchKernelGGL((spmm_ranges<T, NRR, KK>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins,       \
-                       (int)L.bins.size(), L.total_ranges, xs, ldx, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd)
-            if (NR == 16) { if (K == 4) VBC_MM(16, 4); else VBC_MM(16, 8); }
-            else { if (K == 4) VBC_MM(64, 4); else VBC_MM(64, 8); }
-#undef VBC_MM
-            VBC_HIP(hipGetLastError());
-        }
-        const int nrng = L.total_ranges > 1 ? L.total_ranges : 0;
-        const int64_t work = (int64_t)(nrng + L.nfill) * NR;
-        if (work > 0) {
-            const int grid = (int)((work + kBlockThreads - 1) / kBlockThreads);
-            if (NR == 16)
-                hipLaunchKernelGGL((fixup_mm<T, 16>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
-                                   nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
-            else
-                hipLaunchKernelGGL((fixup_mm<T, 64>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
-                                   nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
-            VBC_HIP(hipGetLastError());
-        }
-    }
-    return VBC_OK;
-}
-
-// Multi-RHS transposed product on the panel layout (MFMA), X / Y addressed by (row, column) strides,
-// in chunks of <= 64 right-hand sides (four 16-column accumulators).
-template <typename T>
-static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
-                        int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s)
-{
-    const PanelLaunch &L = h->lm;
-    const bool rd = beta != 0.0;
-    for (int64_t c0 = 0; c0 < nrhs; c0 += 64) {
-        const int nr = (int)std::min<int64_t>(64, nrhs - c0);
-        const T *xs = reinterpret_cast<const T *>(X) + c0 * sxc;
-        T *ys = reinterpret_cast<T *>(Y) + c0 * syc;
-        if (L.total_ranges > 0) {
-            const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
-            // byte extents of X and Y as addressed by this chunk (rows 0..m-1 / 0..n-1, columns 0..nr-1)
-            const int64_t span = ((h->m - 1) * sxr + (int64_t)(nr - 1) * sxc + 1) * (int64_t)sizeof(T);
-            const int64_t yspan = ((h->n - 1) * syr + (int64_t)(nr - 1) * syc + 1) * (int64_t)sizeof(T);
-            const int64_t lim = int64_t(1) << 31;
-            const bool buf = span + 64 * sxc * (int64_t)sizeof(T) < lim && h->panel_val_bytes < lim && !h->panel_nobuf;
-            bool affine = true;
-            for (const PanelBin &pb : L.bins) affine = affine && pb.out_affine;
-            const bool fast = buf && affine && !rd && yspan < lim;
-            const uint32_t xb = (uint32_t)span, yb = (uint32_t)std::min<int64_t>(yspan, lim - 1);
-#define VBC_PANEL(NB, BUF, FAST)                                                                              \
-    hipLaunchKernelGGL((spmm_panel<T, NB, BUF, FAST>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins,        \
-                       (int)L.bins.size(), L.total_ranges, xs, sxr, sxc, xb, ys, syr, syc, yb, nr, (T)alpha, (T)beta, \
-                       (int)rd, h->panel_valu)
-#define VBC_PANEL_NB(BUF, FAST)                                                                               \
-    do {                                                                                                      \
-        if (nr <= 16) VBC_PANEL(1, BUF, FAST);                                                                \
-        else if (nr <= 32) VBC_PANEL(2, BUF, FAST);                                                           \
-        else VBC_PANEL(4, BUF, FAST);                                                                         \
-    } while (0)
-            if (fast) VBC_PANEL_NB(true, true);
-            else if (buf) VBC_PANEL_NB(true, false);
-            else VBC_PANEL_NB(false, false);
-#undef VBC_PANEL_NB
-#undef VBC_PANEL
-            VBC_HIP(hipGetLastError());
-        }
-        if (L.nfill > 0) {
-            const int64_t work = (int64_t)L.nfill * nr;
-            hipLaunchKernelGGL((fill_rows_mm<T>), dim3((int)((work + kBlockThreads - 1) / kBlockThreads)), dim3(kBlockThreads),
-                               0, s, L.d_fill, L.nfill, ys, syr, syc, nr, (T)beta, (int)rd);
-            VBC_HIP(hipGetLastError());
-        }
-    }
     return VBC_OK;
 }
 
@@ -1310,11 +1000,9 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
     if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
         const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
         const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;
-        st = h->dtype == VBC_F64 ? mulmat_panel<double>(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s)
-                                 : mulmat_panel<float>(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
+        st = mulmat_panel_any(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
     } else if (fused) {
-        st = h->dtype == VBC_F64 ? mulmat_t_rowmajor<double>(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s)
-                                 : mulmat_t_rowmajor<float>(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
+        st = mulmat_rowmajor(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
     } else if (!rowmajor) {
         for (int64_t r = 0; r < nrhs && st == VBC_OK; r++)
             st = mul_dispatch(h, trans, dX + r * ldx * esz, dY + r * ldy * esz, alpha, beta, s);

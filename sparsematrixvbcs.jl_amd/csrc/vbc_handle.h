@@ -1,0 +1,105 @@
+// Host-side handle and launch descriptors shared by libvbc's translation units (vbc_device.hip:
+// creation and the C ABI; vbc_launch.hip / vbc_panel_launch.hip: the kernel launches).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "vbc_internal.h"
+#include "vbc_kernels.h"
+#include "vbc_panel.h"
+
+namespace vbc {
+
+#define VBC_HIP(call)                                                                             \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            set_error("%s failed: %s", #call, hipGetErrorString(e_));                             \
+            return VBC_HIP_ERROR;                                                                 \
+        }                                                                                         \
+    } while (0)
+
+// One fused launch of spmv_ranges (+ its fix-up pass).
+struct Launch {
+    std::vector<Bin> bins;
+    Bin *d_bins = nullptr;
+    int total_ranges = 0;
+    int nfill = 0;
+    size_t o_fill = 0;             // arena offset of the fill list (y indices)
+    const int32_t *d_fill = nullptr;
+    std::vector<SlotBin> sbins;    // slotted buckets (vbc_slots.h), launched before the merge kernel
+    SlotBin *d_sbins = nullptr;
+    int slot_ranges = 0;
+};
+
+// The panel layout of the MFMA multi-RHS transposed product (vbc_panel.h): one launch.
+struct PanelLaunch {
+    std::vector<PanelBin> bins;
+    PanelBin *d_bins = nullptr;
+    int total_ranges = 0;
+    int nfill = 0;
+    size_t o_fill = 0;
+    const int32_t *d_fill = nullptr;
+};
+
+// Host description of the input stripes, common to 1D, 2D (expanded) and CSC inputs.
+struct Stripes {
+    int64_t m = 0, n = 0, L = 0;
+    std::vector<int64_t> col0;  // 0-based first column of stripe l
+    std::vector<int32_t> w;     // width
+    std::vector<int64_t> rbeg;  // L+1 prefix into rows
+    std::vector<int32_t> rows;  // 0-based x row of each stored w-wide row
+    std::vector<int64_t> voff;  // element offset of the stripe's first value in the input val
+};
+
+}  // namespace vbc
+
+struct vbc_handle {
+    int64_t m = 0, n = 0, L = 0, K = 0, nblocks = 0, nrows = 0, nval = 0, nnz = 0;
+    int dtype = 0, esz = 8, device = 0;
+    void *d_arena = nullptr;
+    size_t arena_bytes = 0;
+    bool has_t = false, has_f = false, has_m = false;
+    vbc::PanelLaunch lm;          // multi-RHS transposed product on matrix cores (VBC_CREATE_MULTI)
+    int64_t bytes_m = 0;          // matrix bytes one panel product streams
+    int target_ranges_m = 4096;
+    int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
+    int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
+    int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
+    vbc::Launch lt;               // transposed product: all buckets in one launch
+    std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
+    bool f_scale = false;         // forward with several buckets: scale y by beta first
+    int64_t bytes_t = 0, bytes_f = 0;
+    void *d_carry_mm = nullptr;   // multi-RHS carry slots (allocated on first use)
+    size_t carry_mm_bytes = 0;
+    int target_ranges_k[2] = {4096, 4096};  // resident waves of the B'x / Bx kernels (one range each)
+    int tile_k = vbc::kTileKDefault;  // entries per slot per tile
+    int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
+    int diag = 0;                     // ablation variant (VBC_DIAG; tools/ab.py only)
+    int target_ranges_s[2] = {4096, 4096};  // resident waves of the slotted kernels
+    int slots_mode = -1;              // VBC_SLOTS: -1 auto, 0 never, 1 always (when representable)
+    double slots_pad = 1.10;          // auto: largest padded/real row ratio of a slotted bucket
+    int xcd = 0;                      // VBC_XCD=1: XCD-contiguous range order in the slotted kernel (measured slower)
+    int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)
+    int64_t slot_rows_padded_last = 0;
+    int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
+    int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
+};
+
+
+namespace vbc {
+
+// vbc_launch.hip
+int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
+                 hipStream_t stream);
+int mulmat_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy, double alpha,
+                    double beta, hipStream_t s);
+void occupancy_ranges(int esz, int K, int P, int occ[2]);
+// vbc_panel_launch.hip
+int mulmat_panel_any(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
+                     int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s);
+int occupancy_panel(int esz);
+
+}  // namespace vbc

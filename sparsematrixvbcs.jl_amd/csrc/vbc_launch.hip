@@ -1,0 +1,203 @@
+// libvbc kernel launches of the vector products: merge kernel (vbc_kernels.h) + slotted kernel
+// (vbc_slots.hip), their fix-up passes, and the fused vector multi-RHS kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "vbc_handle.h"
+
+namespace vbc {
+
+template <typename T>
+static int launch(const Launch &L, int kind, const void *x, void *y, double alpha, double beta, bool rd,
+                  hipStream_t stream, int xcd, int slot_stage)
+{
+    const T *xs = static_cast<const T *>(x);
+    T *ys = static_cast<T *>(y);
+    if (L.slot_ranges > 0) {
+        bool faste = !rd, contig = true;
+        for (const SlotBin &sb : L.sbins) {
+            faste = faste && sb.out_affine;
+            contig = contig && sb.contig;
+        }
+        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
+        // auto (-1): stage when the per-lane store is narrower than 16 B (kind 0: V * esz < 16, kind 1:
+        // fp32) -- measured: fp32 FE B'x 134 -> 118 us, fp64 (16-B lane stores already) slower staged
+        int stage = slot_stage;
+        if (stage < 0) {
+            stage = 8;
+            for (const SlotBin &sb : L.sbins) {
+                const int V = sb.w <= 8 ? vec_elems((int)sizeof(T), sb.w) : 1;
+                if (kind == 0 ? V * (int)sizeof(T) >= 16 : sizeof(T) == 8) stage = 0;
+            }
+        }
+        if (!(faste && contig)) stage = 0;
+        const hipError_t e = (hipError_t)launch_slots((int)sizeof(T), kind, L.d_sbins, (int)L.sbins.size(), L.slot_ranges,
+                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, x, y, alpha, beta, rd, stream);
+        if (e != hipSuccess) {
+            set_error("spmv_slots launch failed: %s", hipGetErrorString(e));
+            return VBC_HIP_ERROR;
+        }
+    }
+    if (L.total_ranges > 0) {
+        const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
+        const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;
+        // load-free owner writes when every bucket maps segments affinely and beta = 0
+        bool faste = !rd;
+        for (const Bin &bb : L.bins) faste = faste && bb.out_affine;
+        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
+#define VBC_LAUNCH(KIND, KK, PP)                                                                         \
+    do {                                                                                                 \
+        if (faste)                                                                                       \
+            hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP, 0, true>), dim3(grid), dim3(kBlockThreads), 0, stream, \
+                               L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
+        else                                                                                             \
+            hipLaunchKernelGGL((spmv_ranges<T, KIND, KK, PP>), dim3(grid), dim3(kBlockThreads), 0, stream, \
+                               L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
+    } while (0)
+        const int P = L.bins.empty() ? kPipeDefault : L.bins[0].pipe;
+        const int D = L.bins.empty() ? 0 : L.bins[0].diag;
+        if constexpr (std::is_same<T, double>::value) {
+            if (kind == 0 && K == 4 && P == 2 && D == 1) {
+                hipLaunchKernelGGL((spmv_ranges<T, 0, 4, 2, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                                   (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+                return VBC_OK;
+            }
+            if (kind == 0 && K == 4 && P == 2 && D == 2) {
+                hipLaunchKernelGGL((spmv_ranges<T, 0, 4, 2, 2>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                                   (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd);
+                return VBC_OK;
+            }
+        }
+        if (kind == 0) {
+            if (P == 2) { if (K == 4) VBC_LAUNCH(0, 4, 2); else VBC_LAUNCH(0, 8, 2); }
+            else { if (K == 4) VBC_LAUNCH(0, 4, 3); else VBC_LAUNCH(0, 8, 3); }
+        } else {
+            if (P == 2) { if (K == 4) VBC_LAUNCH(1, 4, 2); else VBC_LAUNCH(1, 8, 2); }
+            else { if (K == 4) VBC_LAUNCH(1, 4, 3); else VBC_LAUNCH(1, 8, 3); }
+        }
+#undef VBC_LAUNCH
+        VBC_HIP(hipGetLastError());
+    }
+    const int work = (L.total_ranges > 1 ? L.total_ranges : 0) + L.nfill;
+    if (work > 0) {
+        const int nr = L.total_ranges > 1 ? L.total_ranges : 0;
+        const int grid = (work + kBlockThreads - 1) / kBlockThreads;
+        if (kind == 0)
+            hipLaunchKernelGGL((fixup<T, 0>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                               (int)L.bins.size(), nr, L.d_fill, L.nfill, ys, (T)alpha, (T)beta, (int)rd);
+        else
+            hipLaunchKernelGGL((fixup<T, 1>), dim3(grid), dim3(kBlockThreads), 0, stream, L.d_bins,
+                               (int)L.bins.size(), nr, L.d_fill, L.nfill, ys, (T)alpha, (T)beta, (int)rd);
+        VBC_HIP(hipGetLastError());
+    }
+    return VBC_OK;
+}
+
+template <typename T>
+static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
+                      hipStream_t stream)
+{
+    if (trans) {
+        if (h->n == 0) return VBC_OK;
+        return launch<T>(h->lt, 0, x, y, alpha, beta, beta != 0.0, stream, h->xcd, h->slot_stage);
+    }
+    if (h->m == 0) return VBC_OK;
+    if (h->f_scale) {
+        hipLaunchKernelGGL((scale<T>), dim3(std::min<int64_t>((h->m + kBlockThreads - 1) / kBlockThreads, 4096)),
+                           dim3(kBlockThreads), 0, stream, static_cast<T *>(y), h->m, (T)beta, (int)(beta != 0.0));
+        VBC_HIP(hipGetLastError());
+    }
+    for (size_t b = 0; b < h->lf.size(); b++) {
+        const bool own_beta = !h->f_scale;
+        if (int st = launch<T>(h->lf[b], 1, x, y, alpha, own_beta ? beta : 1.0, own_beta ? beta != 0.0 : true,
+                               stream, h->xcd, h->slot_stage))
+            return st;
+    }
+    return VBC_OK;
+}
+
+int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
+                 hipStream_t stream)
+{
+    return h->dtype == VBC_F64 ? mul_device<double>(h, trans, x, y, alpha, beta, stream)
+                               : mul_device<float>(h, trans, x, y, alpha, beta, stream);
+}
+
+// Multi-RHS transposed product on the tiled stream (row-major X / Y), in chunks of <= 64 columns.
+template <typename T>
+static int mulmat_t_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy,
+                             double alpha, double beta, hipStream_t s)
+{
+    const Launch &L = h->lt;
+    const int NRmax = 64;
+    int64_t stride = 1;
+    for (const Bin &b : L.bins) stride = std::max<int64_t>(stride, (int64_t)b.nranges * b.w * NRmax);
+    const size_t need = (size_t)std::max<size_t>(L.bins.size(), 1) * stride * sizeof(T);
+    if (h->carry_mm_bytes < need) {
+        if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
+        h->d_carry_mm = nullptr;
+        h->carry_mm_bytes = 0;
+        VBC_HIP(hipMalloc(&h->d_carry_mm, need));
+        h->carry_mm_bytes = need;
+    }
+    T *cm = static_cast<T *>(h->d_carry_mm);
+    const bool rd = beta != 0.0;
+    for (int64_t c0 = 0; c0 < nrhs; c0 += NRmax) {
+        const int nr = (int)std::min<int64_t>(NRmax, nrhs - c0);
+        const T *xs = reinterpret_cast<const T *>(X) + c0;
+        T *ys = reinterpret_cast<T *>(Y) + c0;
+        const int NR = nr <= 16 ? 16 : 64;
+        const int64_t cs = nr <= 16 ? stride / 4 : stride;  // carry slots are sized per NR
+        if (L.total_ranges > 0) {
+            const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
+            const int K = L.bins[0].tile_k;
+#define VBC_MM(NRR, KK)                                                                                  \
+    hipLaunchKernelGGL((spmm_ranges<T, NRR, KK>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins,       \
+                       (int)L.bins.size(), L.total_ranges, xs, ldx, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd)
+            if (NR == 16) { if (K == 4) VBC_MM(16, 4); else VBC_MM(16, 8); }
+            else { if (K == 4) VBC_MM(64, 4); else VBC_MM(64, 8); }
+#undef VBC_MM
+            VBC_HIP(hipGetLastError());
+        }
+        const int nrng = L.total_ranges > 1 ? L.total_ranges : 0;
+        const int64_t work = (int64_t)(nrng + L.nfill) * NR;
+        if (work > 0) {
+            const int grid = (int)((work + kBlockThreads - 1) / kBlockThreads);
+            if (NR == 16)
+                hipLaunchKernelGGL((fixup_mm<T, 16>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
+                                   nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
+            else
+                hipLaunchKernelGGL((fixup_mm<T, 64>), dim3(grid), dim3(kBlockThreads), 0, s, L.d_bins, (int)L.bins.size(),
+                                   nrng, L.d_fill, L.nfill, ys, ldy, nr, cm, cs, (T)alpha, (T)beta, (int)rd);
+            VBC_HIP(hipGetLastError());
+        }
+    }
+    return VBC_OK;
+}
+
+int mulmat_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy, double alpha,
+                    double beta, hipStream_t s)
+{
+    return h->dtype == VBC_F64 ? mulmat_t_rowmajor<double>(h, nrhs, X, ldx, Y, ldy, alpha, beta, s)
+                               : mulmat_t_rowmajor<float>(h, nrhs, X, ldx, Y, ldy, alpha, beta, s);
+}
+
+void occupancy_ranges(int esz, int K, int P, int occ[2])
+{
+#define VBC_OCC(TT, KK, PP)                                                                           \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], spmv_ranges<TT, 0, KK, PP>, kBlockThreads, 0); \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], spmv_ranges<TT, 1, KK, PP>, kBlockThreads, 0)
+    if (esz == 8) {
+        if (K == 4) { if (P == 2) { VBC_OCC(double, 4, 2); } else { VBC_OCC(double, 4, 3); } }
+        else { if (P == 2) { VBC_OCC(double, 8, 2); } else { VBC_OCC(double, 8, 3); } }
+    } else {
+        if (K == 4) { if (P == 2) { VBC_OCC(float, 4, 2); } else { VBC_OCC(float, 4, 3); } }
+        else { if (P == 2) { VBC_OCC(float, 8, 2); } else { VBC_OCC(float, 8, 3); } }
+    }
+#undef VBC_OCC
+}
+
+}  // namespace vbc
