@@ -153,8 +153,54 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
 
 struct PendingSlot {
     SlotBin b;
-    size_t o_key, o_val, o_out, o_rrow, o_rchunk;
+    size_t o_key, o_val, o_out, o_rrow, o_rchunk, o_base = 0;
+    std::vector<uint32_t> keys;  // full keys until commit_slot_keys picks the stored form
+    int64_t rows = 0;
+    bool kc_ok = false;          // every row's keys fit base + int16 deltas
 };
+
+// Per-row base of the compressed form: the first non-padding key of the row (0 if none).
+static bool slot_keys_compressible(const std::vector<uint32_t> &keys, int64_t rows, int RPI)
+{
+    for (int64_t r = 0; r < rows; r++) {
+        const uint32_t *k = keys.data() + r * RPI;
+        int64_t base = -1;
+        for (int s = 0; s < RPI; s++) {
+            if (k[s] & kPad) continue;
+            const int64_t g = k[s] & kSlotIdx;
+            if (base < 0) base = g;
+            if (g - base < -32767 || g - base > 32767) return false;
+        }
+    }
+    return true;
+}
+
+// Store a slotted bin's keys: full 32-bit keys, or (kc) per-row bases + int16 deltas.
+static void commit_slot_keys(PendingSlot &ps, bool kc, Arena &ar)
+{
+    const int RPI = ps.b.rpi;
+    const int64_t E = ps.rows * RPI;
+    ps.b.kc = kc ? 1 : 0;
+    if (!kc) {
+        ps.o_key = ar.reserve(E * 4);
+        std::memcpy(ar.at<uint32_t>(ps.o_key), ps.keys.data(), E * 4);
+    } else {
+        ps.o_key = ar.reserve(E * 2);
+        ps.o_base = ar.reserve(ps.rows * 4);
+        int16_t *d = ar.at<int16_t>(ps.o_key);
+        uint32_t *bs = ar.at<uint32_t>(ps.o_base);
+        for (int64_t r = 0; r < ps.rows; r++) {
+            const uint32_t *k = ps.keys.data() + r * RPI;
+            uint32_t base = 0;
+            for (int s = 0; s < RPI; s++)
+                if (!(k[s] & kPad)) { base = k[s] & kSlotIdx; break; }
+            bs[r] = base | (k[0] & kLast);
+            for (int s = 0; s < RPI; s++)
+                d[r * RPI + s] = (k[s] & kPad) ? INT16_MIN : (int16_t)((int64_t)(k[s] & kSlotIdx) - (int64_t)base);
+        }
+    }
+    std::vector<uint32_t>().swap(ps.keys);
+}
 
 // Slots per chunk of a bucket stored w wide (lane-vector width as in the kernel).
 static int slot_rpi(int esz, int w)
@@ -247,7 +293,8 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     }
     range0 += (int)nr;
     const int64_t E = rows * RPI;
-    ps.o_key = ar.reserve(E * 4);
+    ps.rows = rows;
+    ps.keys.resize(E);
     ps.o_val = ar.reserve(E * w * esz);
     ps.o_out = ar.reserve(std::max<size_t>(out.size(), 1) * 4);
     ps.o_rrow = ar.reserve(rrow.size() * 4);
@@ -255,7 +302,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     std::memcpy(ar.at<int32_t>(ps.o_out), out.data(), out.size() * 4);
     std::memcpy(ar.at<int32_t>(ps.o_rrow), rrow.data(), rrow.size() * 4);
     std::memcpy(ar.at<int32_t>(ps.o_rchunk), rchunk.data(), rchunk.size() * 4);
-    uint32_t *key = ar.at<uint32_t>(ps.o_key);
+    uint32_t *key = ps.keys.data();
     char *vv = ar.at<char>(ps.o_val);
     int64_t row = 0;
     for (int64_t c = 0; c < nch; c++) {
@@ -275,10 +322,19 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             }
         }
     }
+    ps.kc_ok = h->slot_keys16 && slot_keys_compressible(ps.keys, rows, RPI);
     h->slot_rows_padded += E;
     h->slot_rows_real += real;
     h->slot_rows_padded_last = E;
     return VBC_OK;
+}
+
+// One launch's slotted bins share one key form (the kernel is specialised on it).
+static void commit_launch_keys(std::vector<PendingSlot> &pss, Arena &ar)
+{
+    bool kc = !pss.empty();
+    for (const PendingSlot &ps : pss) kc = kc && ps.kc_ok;
+    for (PendingSlot &ps : pss) commit_slot_keys(ps, kc, ar);
 }
 
 // Stored width of a transposed bucket.  Widths whose rows do not split into 16-B lane vectors
@@ -331,8 +387,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             }
             PendingSlot ps;
             if (int st = build_slots(h, 0, wp, w, ents, sbeg, out, total, val, ar, srange0, ps)) return st;
-            h->bytes_t += ps.b.nranges > 0 ? (int64_t)(h->slot_rows_padded_last) * (4 + (int64_t)wp * h->esz) : 0;
-            pss.push_back(ps);
+            pss.push_back(std::move(ps));
             continue;
         }
         std::vector<Entry> ents;
@@ -353,6 +408,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)wp * h->esz) + (int64_t)out.size() * 4;
         pbs.push_back(pb);
     }
+    commit_launch_keys(pss, ar);
+    for (const PendingSlot &ps : pss)  // slotted bins: padded rows x (index bytes + values)
+        h->bytes_t += ps.rows * ps.b.rpi * ((ps.b.kc ? 2 : 4) + (int64_t)ps.b.w * h->esz) + (ps.b.kc ? ps.rows * 4 : 0);
     L.total_ranges = range0;
     L.slot_ranges = srange0;
     h->bytes_t += (s.m + s.n) * h->esz;  // x read once, y written once
@@ -396,10 +454,15 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
             PendingSlot ps;
             int srange0 = 0;
             if (int st = build_slots(h, 1, w, w, ents, sbeg, sout, (int64_t)ents.size(), val, ar, srange0, ps)) return st;
-            h->bytes_f += (int64_t)h->slot_rows_padded_last * (4 + (int64_t)w * h->esz) + (int64_t)sout.size() * h->esz;
+            std::vector<PendingSlot> one;
+            one.push_back(std::move(ps));
+            commit_launch_keys(one, ar);
+            const PendingSlot &p1 = one[0];
+            h->bytes_f += p1.rows * p1.b.rpi * ((p1.b.kc ? 2 : 4) + (int64_t)w * h->esz) + (p1.b.kc ? p1.rows * 4 : 0) +
+                          (int64_t)sout.size() * h->esz;
             for (int32_t i : sout) any[i] = 1;
             pbs.push_back({});
-            pss.push_back({ps});
+            pss.push_back(std::move(one));
             Ls.back().slot_ranges = srange0;
             continue;
         }
@@ -584,6 +647,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.out = reinterpret_cast<const int32_t *>(base + ps.o_out);
         b.rrow = reinterpret_cast<const int32_t *>(base + ps.o_rrow);
         b.rchunk = reinterpret_cast<const int32_t *>(base + ps.o_rchunk);
+        b.base = reinterpret_cast<const uint32_t *>(base + ps.o_base);
         L.sbins.push_back(b);
     }
     L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
@@ -673,6 +737,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     h->slot_u = h->esz == 8 ? 8 : 16;  // measured (tools/ab.py, FE): 4 / 8 rows are 4-8 % slower
     if (const char *e = getenv("VBC_SLOT_U")) h->slot_u = h->esz == 8 ? (atoi(e) == 4 ? 4 : 8) : (atoi(e) == 8 ? 8 : 16);

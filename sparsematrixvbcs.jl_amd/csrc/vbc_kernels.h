@@ -85,7 +85,10 @@ struct SlotBin {
     int32_t u;           // rows per pipeline step of the launch (4 / 8 fp64, 8 / 16 fp32)
     int32_t diag;        // ablation variant (0 = production)
     int32_t contig;      // affine and chunk outputs contiguous in y (LDS-staged writes allowed)
-    const uint32_t *key;   // rows * rpi: PAD | LAST | gather index
+    int32_t kc;          // compressed keys: per-row base + int16 per-slot deltas
+    int32_t pad2_;
+    const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
+    const uint32_t *base;  // kc: per row, LAST | base gather index
     const void *val;       // rows * rpi * w values
     const int32_t *out;    // per segment (when not affine)
     const int32_t *rrow;   // per range: first row, nranges + 1 entries
@@ -103,7 +106,7 @@ constexpr uint32_t kSlotIdx = 0x3FFFFFFFu;
 constexpr int64_t kSlotIdxLimit = int64_t(1) << 30;  // gather indices of the slotted layout (30 bits)
 
 // Launches spmv_slots (vbc_slots.hip): returns the hipError_t of the launch.
-int launch_slots(int esz, int kind, const SlotBin *d_bins, int nbins, int total_ranges, bool faste, int xcd, int u, int diag, int stage,
+int launch_slots(int esz, int kind, const SlotBin *d_bins, int nbins, int total_ranges, bool faste, int xcd, int u, int diag, int stage, bool kc,
                  const void *x, void *y, double alpha, double beta, bool rd, hipStream_t stream);
 int occupancy_slots(int esz, int kind);
 

@@ -35,7 +35,7 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
         }
         if (!(faste && contig)) stage = 0;
         const hipError_t e = (hipError_t)launch_slots((int)sizeof(T), kind, L.d_sbins, (int)L.sbins.size(), L.slot_ranges,
-                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, x, y, alpha, beta, rd, stream);
+                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, L.sbins[0].kc != 0, x, y, alpha, beta, rd, stream);
         if (e != hipSuccess) {
             set_error("spmv_slots launch failed: %s", hipGetErrorString(e));
             return VBC_HIP_ERROR;

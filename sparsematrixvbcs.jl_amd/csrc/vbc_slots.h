@@ -40,7 +40,9 @@ __device__ __forceinline__ T slot_reduce(const T (&v)[V], int lane, int sub, int
 // NB > 0 (FASTE launches whose bins are all `contig`): finished chunks are staged in LDS, NB at a
 // time, and written as one contiguous run of y with 16-B stores -- longer write bursts, NB times
 // fewer write events interleaved with the load stream.
-template <typename T, int KIND, int W_, int U, bool FASTE, int DIAG = 0, int NB = 0>
+// KC: compressed keys -- a scalar per-row base (LAST in bit 30) plus an int16 delta per slot
+// (INT16_MIN marks padding): 2 index bytes per entry instead of 4.
+template <typename T, int KIND, int W_, int U, bool FASTE, int DIAG = 0, int NB = 0, bool KC = false>
 __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, const T *__restrict__ x,
                                           T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave)
 {
@@ -62,18 +64,28 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
 
     // Loads are unconditional (rows past the range re-read its last row and are never folded) so
     // the waitcnt pass can count them exactly through the pipeline.
-    auto load = [&](int R, uint32_t (&kk)[U], T (&v)[U][V]) {
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;  // scalar (constant) loads
+    const cptr bases = (cptr)b.base;
+    auto load = [&](int R, uint32_t (&kk)[U], uint32_t (&bs)[U], T (&v)[U][V]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const size_t p = (size_t)min(R + u, R1 - 1) * RPI + lslot;
-            kk[u] = __builtin_nontemporal_load(key + p);
+            const int Rc = min(R + u, R1 - 1);
+            const size_t p = (size_t)Rc * RPI + lslot;
+            if constexpr (KC) {
+                kk[u] = (uint32_t)(int32_t)__builtin_nontemporal_load((gptr<const int16_t>)key + p);
+                bs[u] = bases[Rc];
+            } else {
+                kk[u] = __builtin_nontemporal_load(key + p);
+                bs[u] = 0;
+            }
             ld_stream<T, V>(val + p * w + lsub * V, v[u]);
         }
     };
-    auto gather = [&](const uint32_t (&kk)[U], T (&xv)[U][XV]) {
+    constexpr uint32_t kPad16 = 0xFFFF8000u;  // INT16_MIN sign-extended
+    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&bs)[U], T (&xv)[U][XV]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t gi = kk[u] & kSlotIdx;
+            const uint32_t gi = KC ? (bs[u] & kSlotIdx) + (kk[u] == kPad16 ? 0u : kk[u]) : kk[u] & kSlotIdx;
 #pragma unroll
             for (int e = 0; e < XV; e++) xv[u][e] = DIAG == 2 ? T(1) : xg[gi + (KIND == 0 ? 0 : lsub * V + e)];
         }
@@ -175,37 +187,39 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
     // scalar branch around the fold.
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
-    auto compute = [&](int R, const uint32_t (&kk)[U], const T (&v)[U][V], const T (&xv)[U][XV]) {
+    auto compute = [&](int R, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const T (&v)[U][V],
+                       const T (&xv)[U][XV]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const bool live = R + u < R1v;
-            const bool pad = (kk[u] & kPad) != 0;
+            const bool pad = KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0;
 #pragma unroll
             for (int e = 0; e < V; e++) {
                 const T xe = pad ? T(0) : xv[u][KIND == 0 ? 0 : e];
                 const T nv = fmadd(v[u][e], xe, acc[e]);
                 acc[e] = live ? nv : acc[e];
             }
-            if (R + u < R1 && (__builtin_amdgcn_readfirstlane((int)kk[u]) & (int)kLast)) flush();
+            const uint32_t lastw = KC ? bs[u] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[u]);
+            if (R + u < R1 && (lastw & kLast)) flush();
         }
     };
 
     // Two-stage ping-pong: the gathers of step i are issued before the stream loads of step i+1.
     // Every path to the loop header has consumed every load it issued, so the header's wait for the
     // keys of the next step is counted (vmcnt(n)), never a drain.
-    uint32_t kA[U], kB[U];
+    uint32_t kA[U], kB[U], bA[U], bB[U];
     T vA[U][V], vB[U][V], xv[U][XV];
-    load(R0, kA, vA);
+    load(R0, kA, bA, vA);
     __builtin_amdgcn_s_waitcnt(0);  // prologue drained: the loop header merges the back-edge state only
     for (int R = R0; R < R1; R += 2 * U) {
-        gather(kA, xv);
-        load(R + U, kB, vB);
-        compute(R, kA, vA, xv);
+        gather(kA, bA, xv);
+        load(R + U, kB, bB, vB);
+        compute(R, kA, bA, vA, xv);
         // no early exit: a half step past the range folds nothing (live = false) and re-reads
         // cached rows, while a break here would leave loads pending on a path to the loop header
-        gather(kB, xv);
-        load(R + 2 * U, kA, vA);
-        compute(R + U, kB, vB, xv);
+        gather(kB, bB, xv);
+        load(R + 2 * U, kA, bA, vA);
+        compute(R + U, kB, bB, vB, xv);
     }
     if constexpr (NB > 0) {
         if (nbuf > 0) write_out();
@@ -216,7 +230,7 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
     }
 }
 
-template <typename T, int KIND, int U, bool FASTE, int DIAG = 0, int NB = 0>
+template <typename T, int KIND, int U, bool FASTE, int DIAG = 0, int NB = 0, bool KC = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__restrict__ bins, int nbins,
                                                             int total_ranges, int xcd_chunk, const T *__restrict__ x,
                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
@@ -242,15 +256,15 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__res
     __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * NB * 1024 : 16];
     char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * NB * 1024 : 0);
     switch (b.wkey) {
-    case 0: run_slots<T, KIND, 0, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 1: run_slots<T, KIND, 1, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 2: run_slots<T, KIND, 2, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 3: run_slots<T, KIND, 3, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 4: run_slots<T, KIND, 4, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 5: run_slots<T, KIND, 5, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 6: run_slots<T, KIND, 6, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 7: run_slots<T, KIND, 7, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 8: run_slots<T, KIND, 8, U, FASTE, DIAG, NB>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 0: run_slots<T, KIND, 0, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 1: run_slots<T, KIND, 1, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 2: run_slots<T, KIND, 2, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 3: run_slots<T, KIND, 3, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 4: run_slots<T, KIND, 4, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 5: run_slots<T, KIND, 5, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 6: run_slots<T, KIND, 6, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 7: run_slots<T, KIND, 7, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 8: run_slots<T, KIND, 8, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
     default: break;
     }
 }
