@@ -322,7 +322,9 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             }
         }
     }
-    ps.kc_ok = h->slot_keys16 && slot_keys_compressible(ps.keys, rows, RPI);
+    // compressed keys: measured faster on FE except the fp32 forward product (145 -> 158 us)
+    const bool kc_wanted = h->slot_keys16 == 1 ? !(kind == 1 && esz == 4) : h->slot_keys16 == 2;
+    ps.kc_ok = kc_wanted && slot_keys_compressible(ps.keys, rows, RPI);
     h->slot_rows_padded += E;
     h->slot_rows_real += real;
     h->slot_rows_padded_last = E;
@@ -737,7 +739,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
-    if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     h->slot_u = h->esz == 8 ? 8 : 16;  // measured (tools/ab.py, FE): 4 / 8 rows are 4-8 % slower
     if (const char *e = getenv("VBC_SLOT_U")) h->slot_u = h->esz == 8 ? (atoi(e) == 4 ? 4 : 8) : (atoi(e) == 8 ? 8 : 16);

@@ -23,16 +23,11 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
             contig = contig && sb.contig;
         }
         if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
-        // auto (-1): stage when the per-lane store is narrower than 16 B (kind 0: V * esz < 16, kind 1:
-        // fp32) -- measured: fp32 FE B'x 134 -> 118 us, fp64 (16-B lane stores already) slower staged
+        // auto (-1): B'x stages 8 chunks per write, Bx writes directly -- measured on FE with every
+        // variant built twice (tools/ab.py --copies 2): fp64 B'x 192/177 -> 184/172 us staged,
+        // fp64 Bx 186 -> 198 and fp32 Bx 142 -> 157 us staged
         int stage = slot_stage;
-        if (stage < 0) {
-            stage = 8;
-            for (const SlotBin &sb : L.sbins) {
-                const int V = sb.w <= 8 ? vec_elems((int)sizeof(T), sb.w) : 1;
-                if (kind == 0 ? V * (int)sizeof(T) >= 16 : sizeof(T) == 8) stage = 0;
-            }
-        }
+        if (stage < 0) stage = kind == 0 ? 8 : 0;
         if (!(faste && contig)) stage = 0;
         const hipError_t e = (hipError_t)launch_slots((int)sizeof(T), kind, L.d_sbins, (int)L.sbins.size(), L.slot_ranges,
                                                       faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, L.sbins[0].kc != 0, x, y, alpha, beta, rd, stream);

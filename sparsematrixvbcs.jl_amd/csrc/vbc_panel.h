@@ -83,23 +83,23 @@ __device__ __forceinline__ int panel_out(const PanelBin &b, int seg)
 #define VBC_PANEL_BATCH 16
 #endif
 constexpr int kPanelBatch = VBC_PANEL_BATCH;
+#ifndef VBC_PANEL_VAL_AUX
+#define VBC_PANEL_VAL_AUX 2  // val is streamed once: nt
+#endif
 constexpr int kPanelTail = 8 * kPanelBatch;
 // Offset of a masked buffer access: at least every num_records used (operands < 2 GiB) and, plus any
 // soffset below 2 GiB, still inside 32 bits -- the access is dropped (store) or reads 0 (load).
 constexpr uint32_t kOobOff = 0x80000000u;  // padding rows after each bin (batch over-read + key prefetch)
 
 // Raw buffer loads (32-bit offsets, hardware bounds check) for operands below 4 GiB.
-template <typename T>
-__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff);
-template <>
-__device__ __forceinline__ float buf_load<float>(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
+// AUX = cache policy bits of the buffer instruction (2 = nt: streamed once, keep the caches for X).
+template <typename T, int AUX = 0>
+__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
 {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
-}
-template <>
-__device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
-{
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+    if constexpr (sizeof(T) == 4)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, AUX));
+    else
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, AUX));
 }
 
 template <typename T>
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
             rsv[q] = xch[wv][4 * q + kr][1];
             if constexpr (BUF) {
                 const uint32_t vo = (!kOobMask || (int)rsv[q] == sa) ? voff_lane + (uint32_t)(q * 4 * w * esz) : kOobOff;
-                av[q] = buf_load<T>(vrs, vo, (diag & 8) ? 0u : (uint32_t)((size_t)gb * 4 * w * esz));
+                av[q] = buf_load<T, VBC_PANEL_VAL_AUX>(vrs, vo, (diag & 8) ? 0u : (uint32_t)((size_t)gb * 4 * w * esz));
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) xv[q][nb] = buf_load<T>(xrs, xo + jofs[nb], 0u);
             } else {

@@ -44,6 +44,27 @@ def test_forced_golden_one_hot(golden, forced):
             one_hot_probes(V.SparseMatrixVBC[4, 4](g["A"], meth()), g["A"])
 
 
+def test_forced_golden_one_hot_full_keys(golden, forced, monkeypatch):
+    """The 32-bit key form of the slotted layout (compression off) under the one-hot protocol."""
+    monkeypatch.setenv("VBC_SLOT_KEYS16", "0")
+    for key, g in golden.items():
+        one_hot_probes(V.SparseMatrix1DVBC[4](g["A"], METHODS_1D[1]()), g["A"])
+
+
+def test_keys16_falls_back_on_wide_deltas(monkeypatch):
+    """Rows whose keys span more than int16 keep 32-bit keys (and stay exact)."""
+    monkeypatch.setenv("VBC_SLOTS", "1")
+    monkeypatch.setenv("VBC_SLOT_KEYS16", "2")
+    rng = np.random.default_rng(5)
+    m, n = 200000, 64
+    D = sp.random(m, n, density=4e-5, random_state=5, format="csc")
+    B = V.SparseMatrix1DVBC[1](D, V.EquiChunker(1))
+    x = rng.uniform(-1, 1, m)
+    y = torch.zeros(n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert rel(y.cpu().numpy(), D.T @ x) <= TOL64
+
+
 def test_forced_sprand_grid_one_hot(forced):
     for name, A in sprand_family(trials=1):
         one_hot_probes(V.SparseMatrix1DVBC[4](A, METHODS_1D[1]()), A)
@@ -214,13 +235,16 @@ def test_slots_deterministic_and_matches_merge(monkeypatch):
     assert (torch.linalg.norm(ya - y0) / torch.linalg.norm(y0)).item() <= 1e-14
 
 
+@pytest.mark.parametrize("keys16", ["0", "2"])
 @pytest.mark.parametrize("stage", ["0", "8"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_staged_writes(monkeypatch, stage, dtype):
-    """LDS-staged y writes (VBC_SLOT_STAGE): single-width matrices of every width (contiguous chunk
-    outputs), a partial last chunk, and a y that is not 16-B aligned (element-wise write path)."""
+def test_staged_writes(monkeypatch, stage, dtype, keys16):
+    """LDS-staged y writes (VBC_SLOT_STAGE) and both key forms (32-bit keys / per-row base + int16
+    deltas): single-width matrices of every width (contiguous chunk outputs), a partial last chunk,
+    and a y that is not 16-B aligned (element-wise write path)."""
     monkeypatch.setenv("VBC_SLOTS", "1")
     monkeypatch.setenv("VBC_SLOT_STAGE", stage)
+    monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
     tol = TOL64 if dtype == np.float64 else TOL32
     rng = np.random.default_rng(int(stage) + np.dtype(dtype).itemsize)
     cases = [V.synthetic.fe_grid_2d(37, dof=2, dtype=dtype)]

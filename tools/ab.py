@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--trans", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--nrhs", type=int, default=0, help=">0: time the multi-RHS product (row-major X / Y)")
+    ap.add_argument("--copies", type=int, default=1,
+                    help="build every variant this many times (A B .. A B ..): placement effects show as spread")
     args = ap.parse_args()
     import torch
 
@@ -55,7 +57,7 @@ def main():
               bench.algorithmic_bytes(B, esz) + (k - 1) * esz * (B.m + B.n)) if args.workload not in ("c5",) else \
         (len(B.val) * esz + 4 * len(B.idx) + (k * esz) * (B.m + B.n))
     x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, (nx, k) if args.nrhs else nx).astype(dtype)).cuda()
-    variants = [v for v in args.variants.split(";")]
+    variants = [v for v in args.variants.split(";")] * max(1, args.copies)
     handles, libs = [], []
     main_lib = L.lib()
     for v in variants:
