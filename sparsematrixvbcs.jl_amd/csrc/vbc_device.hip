@@ -219,35 +219,81 @@ static std::vector<int32_t> chunk_rows(const std::vector<int64_t> &sbeg, int RPI
     return cr;
 }
 
+// Segment order of a sorted slotted bucket: by decreasing length inside windows of kSortWindow
+// chunks (neighbouring segments stay near each other, so x locality survives the sort).
+constexpr int kSortWindow = 32;
+static std::vector<int64_t> sorted_order(const std::vector<int64_t> &sbeg, int RPI)
+{
+    const int64_t nseg = (int64_t)sbeg.size() - 1, win = (int64_t)kSortWindow * RPI;
+    std::vector<int64_t> ord(nseg);
+    for (int64_t i = 0; i < nseg; i++) ord[i] = i;
+    for (int64_t a = 0; a < nseg; a += win) {
+        const int64_t e = std::min(nseg, a + win);
+        std::stable_sort(ord.begin() + a, ord.begin() + e, [&](int64_t p, int64_t q) {
+            return sbeg[p + 1] - sbeg[p] > sbeg[q + 1] - sbeg[q];
+        });
+    }
+    return ord;
+}
+
+static std::vector<int64_t> permuted_sbeg(const std::vector<int64_t> &sbeg, const std::vector<int64_t> &ord)
+{
+    std::vector<int64_t> p(sbeg.size());
+    p[0] = 0;
+    for (size_t i = 0; i < ord.size(); i++) p[i + 1] = p[i] + sbeg[ord[i] + 1] - sbeg[ord[i]];
+    return p;
+}
+
 // Whether a bucket (segments sbeg over `real` entries) runs slotted: auto mode asks for a padded row
-// count within slots_pad of the real one and chunks short enough to balance over the ranges.
-static bool want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
-                       int64_t total_entries, int64_t gather_limit)
+// count within slots_pad of the real one and chunks short enough to balance over the ranges, first
+// in the natural segment order (affine y map), then sorted by length (y offsets from the table).
+// Returns 0 (merge layout), 1 (slotted, natural order) or 2 (slotted, `order`).
+static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
+                      int64_t total_entries, int64_t gather_limit, std::vector<int64_t> &order)
 {
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     const int64_t real = nseg > 0 ? sbeg[nseg] - sbeg[0] : 0;
-    if (h->slots_mode == 0 || real == 0 || gather_limit >= (int64_t)kSlotIdxLimit) return false;
-    if (nseg >= (int64_t(1) << 31)) return false;
+    order.clear();
+    if (h->slots_mode == 0 || real == 0 || gather_limit >= (int64_t)kSlotIdxLimit) return 0;
+    if (nseg >= (int64_t(1) << 31)) return 0;
     const int RPI = slot_rpi(h->esz, w);
-    const std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
-    int64_t rows = 0, longest = 0;
-    for (int32_t c : cr) { rows += c; longest = std::max<int64_t>(longest, c); }
-    if (rows * RPI >= (int64_t(1) << 31)) return false;
-    if (h->slots_mode == 1) return true;
-    const double ratio = (double)(rows * RPI) / (double)real;
-    const double share = (double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1);
-    const double rows_per_range = (double)rows / std::max(1.0, share);
-    return ratio <= h->slots_pad && (double)longest <= std::max(32.0, 0.5 * rows_per_range);
+    auto fits = [&](const std::vector<int64_t> &sb, bool force) {
+        const std::vector<int32_t> cr = chunk_rows(sb, RPI);
+        int64_t rows = 0, longest = 0;
+        for (int32_t c : cr) { rows += c; longest = std::max<int64_t>(longest, c); }
+        if (rows * RPI >= (int64_t(1) << 31)) return false;
+        if (force) return true;
+        const double ratio = (double)(rows * RPI) / (double)real;
+        const double share = (double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1);
+        const double rows_per_range = (double)rows / std::max(1.0, share);
+        return ratio <= h->slots_pad && (double)longest <= std::max(64.0, 0.5 * rows_per_range);
+    };
+    if (h->slots_sort != 2 && fits(sbeg, h->slots_mode == 1)) return 1;
+    if (h->slots_sort == 0) return 0;
+    order = sorted_order(sbeg, RPI);
+    if (fits(permuted_sbeg(sbeg, order), h->slots_mode == 1)) return 2;
+    order.clear();
+    return 0;
 }
 
 // Lay out a slotted bucket: chunk rows row-major over the slots, PAD / LAST keys, ranges of whole
 // chunks balanced by rows.  ents[sbeg[q] ...] are segment q's entries (keys = gather index only).
 static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vector<Entry> &ents,
-                       const std::vector<int64_t> &sbeg, const std::vector<int32_t> &out, int64_t total_entries,
-                       const char *val, Arena &ar, int &range0, PendingSlot &ps)
+                       const std::vector<int64_t> &sbeg0, const std::vector<int32_t> &out0, int64_t total_entries,
+                       const char *val, Arena &ar, int &range0, PendingSlot &ps,
+                       const std::vector<int64_t> &order = {})
 {
     const int esz = h->esz;
     const int RPI = slot_rpi(esz, w);
+    // segment q of the layout is input segment order[q] (natural order when `order` is empty)
+    const std::vector<int64_t> sbeg = order.empty() ? sbeg0 : permuted_sbeg(sbeg0, order);
+    std::vector<int64_t> pstart(sbeg.size() - 1);
+    std::vector<int32_t> out(out0.size());
+    for (size_t q = 0; q < pstart.size(); q++) {
+        const int64_t o = order.empty() ? (int64_t)q : order[q];
+        pstart[q] = sbeg0[o];
+        out[q] = out0[o];
+    }
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     const int64_t real = sbeg[nseg] - sbeg[0];
     const std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
@@ -256,11 +302,16 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     for (int32_t c : cr) rows += c;
     int64_t nr = (int64_t)std::llround((double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1));
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
+    bool affine = true;
+    for (size_t q = 1; q < out.size() && affine; q++)
+        affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * (out[1] - out[0]);
     std::vector<int32_t> rrow{0}, rchunk{0};
     int64_t acc = 0;
     for (int64_t c = 0; c < nch; c++) {
         acc += cr[c];
-        if (c + 1 < nch && (int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows) {
+        // a table-mapped bin keeps <= kSlotOutChunks chunks per range (their y offsets sit in LDS)
+        const bool full = c + 1 - rchunk.back() >= (affine ? INT32_MAX : kSlotOutChunks);
+        if (c + 1 < nch && (full || ((int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows))) {
             rrow.push_back((int32_t)acc);
             rchunk.push_back((int32_t)(c + 1));
         }
@@ -311,7 +362,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             for (int sl = 0; sl < RPI; sl++) {
                 const int64_t seg = c * RPI + sl, e = row * RPI + sl;
                 if (seg < nseg && sbeg[seg] + qr < sbeg[seg + 1]) {
-                    const Entry &en = ents[sbeg[seg] + qr];
+                    const Entry &en = ents[pstart[seg] + qr];
                     key[e] = en.key | last;
                     std::memcpy(vv + e * w * esz, val + en.voff * esz, (size_t)wsrc * esz);
                     if (wsrc < w) std::memset(vv + (e * w + wsrc) * esz, 0, (size_t)(w - wsrc) * esz);
@@ -376,9 +427,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     for (auto &kv : buckets) {
         const int w = kv.first;
         const int wp = padded_width(h, w);
-        std::vector<int64_t> sbeg{0};
+        std::vector<int64_t> sbeg{0}, order;
         for (int64_t l : kv.second) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
-        if (want_slots(h, 0, wp, sbeg, total, s.m)) {
+        if (want_slots(h, 0, wp, sbeg, total, s.m, order)) {
             std::vector<Entry> ents;
             std::vector<int32_t> out;
             ents.reserve(sbeg.back());
@@ -388,7 +439,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                     ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
             }
             PendingSlot ps;
-            if (int st = build_slots(h, 0, wp, w, ents, sbeg, out, total, val, ar, srange0, ps)) return st;
+            if (int st = build_slots(h, 0, wp, w, ents, sbeg, out, total, val, ar, srange0, ps, order)) return st;
             pss.push_back(std::move(ps));
             continue;
         }
@@ -442,7 +493,8 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
         std::vector<int32_t> sout;
         for (int64_t i = 0; i < s.m; i++)
             if (single || cnt[i + 1] > cnt[i]) { sbeg.push_back(cnt[i + 1]); sout.push_back((int32_t)i); }
-        const bool slotted = want_slots(h, 1, w, sbeg, (int64_t)cnt[s.m], s.n);
+        std::vector<int64_t> order;
+        const bool slotted = want_slots(h, 1, w, sbeg, (int64_t)cnt[s.m], s.n, order) != 0;
         std::vector<Entry> ents(cnt[s.m]);
         for (int64_t i = 0; i < s.m; i++) cur[i] = cnt[i];
         for (int64_t l : kv.second)
@@ -455,7 +507,7 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
         if (slotted) {
             PendingSlot ps;
             int srange0 = 0;
-            if (int st = build_slots(h, 1, w, w, ents, sbeg, sout, (int64_t)ents.size(), val, ar, srange0, ps)) return st;
+            if (int st = build_slots(h, 1, w, w, ents, sbeg, sout, (int64_t)ents.size(), val, ar, srange0, ps, order)) return st;
             std::vector<PendingSlot> one;
             one.push_back(std::move(ps));
             commit_launch_keys(one, ar);
@@ -738,6 +790,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_TARGET_RANGES_S")) h->target_ranges_s[0] = h->target_ranges_s[1] = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
+    if (const char *e = getenv("VBC_SLOTS_SORT")) h->slots_sort = atoi(e);
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;

@@ -103,6 +103,7 @@ __device__ __forceinline__ int out_of_slots(const SlotBin &b, int seg)
 constexpr uint32_t kPad = 0x80000000u;   // slotted layout: padding row (x taken as 0)
 constexpr uint32_t kLast = 0x40000000u;  // slotted layout: last row of a chunk
 constexpr uint32_t kSlotIdx = 0x3FFFFFFFu;
+constexpr int kSlotOutChunks = 16;  // chunks per range of a non-affine slotted bin (LDS-staged y offsets)
 constexpr int64_t kSlotIdxLimit = int64_t(1) << 30;  // gather indices of the slotted layout (30 bits)
 
 // Launches spmv_slots (vbc_slots.hip): returns the hipError_t of the launch.

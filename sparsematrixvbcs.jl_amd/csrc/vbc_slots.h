@@ -44,7 +44,7 @@ __device__ __forceinline__ T slot_reduce(const T (&v)[V], int lane, int sub, int
 // (INT16_MIN marks padding): 2 index bytes per entry instead of 4.
 template <typename T, int KIND, int W_, int U, bool FASTE, int DIAG = 0, int NB = 0, bool KC = false>
 __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, const T *__restrict__ x,
-                                          T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave)
+                                          T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave, int *lds_out)
 {
     constexpr bool kGeneric = (W_ == 0);
     constexpr int V = kGeneric ? 1 : vec_elems(sizeof(T), W_);
@@ -94,6 +94,16 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
 #pragma unroll
     for (int e = 0; e < V; e++) acc[e] = dump[e] = T(0);
     int nbuf = 0, cfirst = c;  // staged chunks (NB > 0) and the first of them
+    // Without FASTE the y offset of a segment comes from the table (sorted or non-affine segment
+    // orders; bins are cut so a range holds <= kSlotOutChunks chunks): the range's entries are staged
+    // in LDS by the prologue, so a flush reads LDS (lgkmcnt) and never waits on the vector loads.
+    const int c0 = c;
+    if constexpr (!FASTE) {
+        if (!b.out_affine) {
+            const int n = min(kSlotOutChunks * RPI, b.nseg - c0 * RPI);
+            for (int i = lane; i < n; i += 64) lds_out[i] = G(b.out)[c0 * RPI + i];
+        }
+    }
 
     // Staged chunks [cfirst, cfirst + nbuf) -> y: one contiguous run (kind 0: RPI * w values per
     // chunk, kind 1: RPI), valid segments only.
@@ -141,7 +151,7 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
         }
         if constexpr (KIND == 0) {
             if (ok) {
-                const int o = FASTE ? b.out_base + seg * b.out_stride : out_of_slots(b, seg);
+                const int o = (FASTE || b.out_affine) ? b.out_base + seg * b.out_stride : lds_out[(c - c0) * RPI + slot];
                 gptr<T> yo = DIAG == 4 ? G(y) + ((size_t)r * 64 + lane) * V : G(y) + o + sub * V;
                 const int lim = b.wst - sub * V;  // padding columns (w > wst) are never written
                 T q[V];
@@ -169,7 +179,7 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
         } else {
             const T s = slot_reduce<T, V>(acc, lane, sub, LPR);
             if (ok && sub == 0) {
-                const int o = FASTE ? b.out_base + seg * b.out_stride : out_of_slots(b, seg);
+                const int o = (FASTE || b.out_affine) ? b.out_base + seg * b.out_stride : lds_out[(c - c0) * RPI + slot];
                 gptr<T> yo = G(y) + o;
                 T q = alpha * s;
                 if (!FASTE && rd) q = fmadd(beta, *yo, q);
@@ -255,16 +265,18 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__res
     const bool rd = rd_i != 0;
     __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * NB * 1024 : 16];
     char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * NB * 1024 : 0);
+    __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutChunks * 64];
+    int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutChunks * 64);
     switch (b.wkey) {
-    case 0: run_slots<T, KIND, 0, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 1: run_slots<T, KIND, 1, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 2: run_slots<T, KIND, 2, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 3: run_slots<T, KIND, 3, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 4: run_slots<T, KIND, 4, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 5: run_slots<T, KIND, 5, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 6: run_slots<T, KIND, 6, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 7: run_slots<T, KIND, 7, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
-    case 8: run_slots<T, KIND, 8, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds); break;
+    case 0: run_slots<T, KIND, 0, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 1: run_slots<T, KIND, 1, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 2: run_slots<T, KIND, 2, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 3: run_slots<T, KIND, 3, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 4: run_slots<T, KIND, 4, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 5: run_slots<T, KIND, 5, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 6: run_slots<T, KIND, 6, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 7: run_slots<T, KIND, 7, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 8: run_slots<T, KIND, 8, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
     default: break;
     }
 }

@@ -34,7 +34,7 @@ def slot_bins(B, trans=True):
     return B.info(trans=trans)["slot_bins"]
 
 
-def test_forced_golden_one_hot(golden, forced):
+def test_forced_golden_one_hot(golden, forced, order):
     for key, g in golden.items():
         for meth in METHODS_1D:
             B = V.SparseMatrix1DVBC[4](g["A"], meth())
@@ -71,7 +71,7 @@ def test_forced_sprand_grid_one_hot(forced):
 
 
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (2.5, 0.0), (1.0, 1.0), (-0.5, 2.0)])
-def test_forced_random_alpha_beta(golden, forced, alpha, beta):
+def test_forced_random_alpha_beta(golden, forced, order, alpha, beta):
     rng = np.random.default_rng(21)
     for key, g in golden.items():
         A = g["A"]
@@ -93,8 +93,16 @@ def test_forced_random_alpha_beta(golden, forced, alpha, beta):
             assert rel(yd.cpu().numpy(), oracle_ref(B, x, y0.copy(), alpha, beta, trans, quirks=True)) <= TOL64
 
 
+@pytest.fixture(params=["natural", "sorted"])
+def order(request, monkeypatch):
+    """Slotted segment order: natural (affine y map where possible) or sorted by length (y offsets
+    from the table, staged in LDS per range)."""
+    monkeypatch.setenv("VBC_SLOTS_SORT", "2" if request.param == "sorted" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("widths", [[1], [2], [3], [4], [2, 3], [5, 6, 7, 8], [9, 12, 16], [17, 31, 33, 64]])
-def test_forced_widths(forced, widths):
+def test_forced_widths(forced, order, widths):
     """Every width variant of the slotted kernel (compile-time 1..8, runtime w > 8), both dtypes,
     several buckets (non-affine segment maps, multi-bucket forward accumulation)."""
     rng = np.random.default_rng(sum(widths) + 5)
@@ -141,7 +149,7 @@ def test_forced_nonfinite_x_stays_in_place(forced):
     assert np.array_equal(np.isinf(got), np.isinf(ref))
 
 
-def test_forced_edge_cases(forced):
+def test_forced_edge_cases(forced, order):
     """Empty matrices, empty stripes, one 20000-row stripe in a chunk of short ones."""
     for (m, n) in ((0, 0), (0, 5), (5, 0), (1, 1)):
         A = sp.csc_matrix((m, n))
@@ -211,10 +219,40 @@ def test_auto_fe_grid_uses_slots(dtype):
         assert rel(yd.cpu().numpy(), yr) <= tol, trans
 
 
-def test_auto_keeps_merge_for_ragged():
-    """Uniform-random rows (Poisson stripe lengths) stay on the merge layout in auto mode."""
+def test_auto_sorted_slots_for_standin():
+    """A SuiteSparse-like stand-in (3D stiffness, ragged stripe lengths) is laid out slotted in sorted
+    order in auto mode (padding ~1 %) and matches the oracle in both directions and both dtypes."""
+    A = V.synthetic.fe_stiffness_3d(3000, 150000, 3, seed=4)
+    B = V.SparseMatrix1DVBC[8](A, V.StrictChunker(8))
+    assert slot_bins(B) == 1
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    rng = np.random.default_rng(6)
+    for trans, nx, ny in ((True, B.m, B.n), (False, B.n, B.m)):
+        x = rng.uniform(-1, 1, nx)
+        y0 = rng.uniform(-1, 1, ny)
+        for alpha, beta in ((1.0, 0.0), (2.0, -0.5)):
+            yd = dev(y0)
+            V.mul_(yd, V.adjoint(B) if trans else B, dev(x), alpha, beta)
+            assert rel(yd.cpu().numpy(), O.mul(R, x, y0.copy(), alpha, beta, trans=trans, ref_semantics=False)) <= TOL64, trans
+    C = V.SparseMatrixCSC(A.astype(np.float32))
+    y = torch.zeros(A.shape[1], dtype=torch.float32, device=DEV)
+    xs = rng.uniform(-1, 1, A.shape[0]).astype(np.float32)
+    V.TrSpMV_(y, C, dev(xs))
+    assert rel(y.cpu().numpy(), A.T @ xs.astype(np.float64)) <= TOL32
+
+
+def test_auto_ns_sorted_slots_vs_oracle():
+    """Uniform-random rows (Poisson stripe lengths, costs.jl:63-83): auto mode sorts the stripes by
+    length inside windows (padding ~3 %), y offsets come from the table; parity both directions."""
     B = V.synthetic.north_star(scale=0.01)
-    assert slot_bins(B) == 0
+    assert slot_bins(B) == 1
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    rng = np.random.default_rng(0xC0FFEE)
+    for trans, nx, ny in ((True, B.m, B.n), (False, B.n, B.m)):
+        x = rng.uniform(-1, 1, nx)
+        yd = torch.zeros(ny, dtype=torch.float64, device=DEV)
+        V.mul_(yd, V.adjoint(B) if trans else B, dev(x))
+        assert rel(yd.cpu().numpy(), O.mul(R, x, np.zeros(ny), trans=trans)) <= TOL64, trans
 
 
 def test_slots_deterministic_and_matches_merge(monkeypatch):
