@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for wl in ${WORKLOADS:-fe ns c5}; do
-  dt=f64; kern=spmv_ranges; rf=2
+  dt=f64; kern=spmv_slots; rf=2
   if [ "$wl" = c5 ]; then dt=f32; kern=spmm_panel; rf=1; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$wl -o run -- \
       python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary --workload $wl --dtype $dt > gpurun_out/prof_$wl.log 2>&1
