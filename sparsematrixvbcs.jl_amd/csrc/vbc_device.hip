@@ -202,10 +202,20 @@ static void commit_slot_keys(PendingSlot &ps, bool kc, Arena &ar)
     std::vector<uint32_t>().swap(ps.keys);
 }
 
-// Slots per chunk of a bucket stored w wide (lane-vector width as in the kernel).
-static int slot_rpi(int esz, int w)
+// Segments per lane of a B'x bucket whose rows are narrower than a 16-B lane vector: fp32 w = 2 folds
+// two segments side by side (run_slots_narrow); w = 1 (CSC) keeps one segment per lane (faster).
+static int slot_spl(const vbc_handle *h, int kind, int w)
 {
-    const int V = w <= 8 ? vec_elems(esz, w) : 1;
+    if (kind != 0 || !h->slot_narrow) return 1;
+    return (h->esz == 4 && w == 2) ? 2 : 1;  // the only narrow form that measured faster (vbc_slots.h)
+}
+
+// Slots per chunk of a bucket stored w wide (lane-vector width as in the kernel).
+static int slot_rpi(const vbc_handle *h, int kind, int w)
+{
+    const int spl = slot_spl(h, kind, w);
+    if (spl > 1) return 64 * spl;
+    const int V = w <= 8 ? vec_elems(h->esz, w) : 1;
     return 64 / (w / V);
 }
 
@@ -256,7 +266,7 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
     order.clear();
     if (h->slots_mode == 0 || real == 0 || gather_limit >= (int64_t)kSlotIdxLimit) return 0;
     if (nseg >= (int64_t(1) << 31)) return 0;
-    const int RPI = slot_rpi(h->esz, w);
+    const int RPI = slot_rpi(h, kind, w);
     auto fits = [&](const std::vector<int64_t> &sb, bool force) {
         const std::vector<int32_t> cr = chunk_rows(sb, RPI);
         int64_t rows = 0, longest = 0;
@@ -284,7 +294,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
                        const std::vector<int64_t> &order = {})
 {
     const int esz = h->esz;
-    const int RPI = slot_rpi(esz, w);
+    const int RPI = slot_rpi(h, kind, w);
     // segment q of the layout is input segment order[q] (natural order when `order` is empty)
     const std::vector<int64_t> sbeg = order.empty() ? sbeg0 : permuted_sbeg(sbeg0, order);
     std::vector<int64_t> pstart(sbeg.size() - 1);
@@ -309,8 +319,8 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     int64_t acc = 0;
     for (int64_t c = 0; c < nch; c++) {
         acc += cr[c];
-        // a table-mapped bin keeps <= kSlotOutChunks chunks per range (their y offsets sit in LDS)
-        const bool full = c + 1 - rchunk.back() >= (affine ? INT32_MAX : kSlotOutChunks);
+        // a table-mapped bin keeps <= kSlotOutEntries segments per range (their y offsets sit in LDS)
+        const bool full = !affine && (int64_t)(c + 2 - rchunk.back()) * RPI > kSlotOutEntries;
         if (c + 1 < nch && (full || ((int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows))) {
             rrow.push_back((int32_t)acc);
             rchunk.push_back((int32_t)(c + 1));
@@ -330,6 +340,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.nseg = (int32_t)nseg;
     b.u = h->slot_u;
     b.diag = h->diag;
+    b.spl = slot_spl(h, kind, w);
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -338,7 +349,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     if (getenv("VBC_NO_AFFINE")) b.out_affine = 0;  // A/B knob
     {
         const int V = w <= 8 ? vec_elems(esz, w) : 1;
-        const bool full = RPI * (w / V) == 64 && V * esz <= 16;
+        const bool full = b.spl > 1 || (RPI * (w / V) == 64 && V * esz <= 16);
         b.contig = b.out_affine && (kind == 0 ? (full && wsrc == w && (nseg <= 1 || b.out_stride == w))
                                               : (nseg <= 1 || b.out_stride == 1));
     }
@@ -794,11 +805,11 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
     if (const char *e = getenv("VBC_SLOTS_SORT")) h->slots_sort = atoi(e);
+    if (const char *e = getenv("VBC_SLOT_NARROW")) h->slot_narrow = atoi(e) != 0;
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
-    h->slot_u = h->esz == 8 ? 8 : 16;  // measured (tools/ab.py, FE): 4 / 8 rows are 4-8 % slower
-    if (const char *e = getenv("VBC_SLOT_U")) h->slot_u = h->esz == 8 ? (atoi(e) == 4 ? 4 : 8) : (atoi(e) == 8 ? 8 : 16);
+    h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
     if (flags & VBC_CREATE_MULTI) {
         const int om = occupancy_panel(h->esz);
         h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;

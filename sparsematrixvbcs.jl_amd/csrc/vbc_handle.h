@@ -81,6 +81,7 @@ struct vbc_handle {
     int target_ranges_s[2] = {4096, 4096};  // resident waves of the slotted kernels
     int slots_mode = -1;              // VBC_SLOTS: -1 auto, 0 never, 1 always (when representable)
     double slots_pad = 1.10;          // auto: largest padded/real row ratio of a slotted bucket
+    int slot_narrow = 1;              // VBC_SLOT_NARROW=0: one segment per lane slot for narrow B'x rows too
     int slots_sort = 1;               // VBC_SLOTS_SORT: 0 natural order only, 1 sort when needed, 2 always sort
     int xcd = 0;                      // VBC_XCD=1: XCD-contiguous range order in the slotted kernel (measured slower)
     int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)

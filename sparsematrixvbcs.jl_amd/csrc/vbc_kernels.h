@@ -86,7 +86,7 @@ struct SlotBin {
     int32_t diag;        // ablation variant (0 = production)
     int32_t contig;      // affine and chunk outputs contiguous in y (LDS-staged writes allowed)
     int32_t kc;          // compressed keys: per-row base + int16 per-slot deltas
-    int32_t pad2_;
+    int32_t spl;         // segments per lane (narrow B'x rows: 16 / (w * sizeof(T))), else 1
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const void *val;       // rows * rpi * w values
@@ -103,7 +103,7 @@ __device__ __forceinline__ int out_of_slots(const SlotBin &b, int seg)
 constexpr uint32_t kPad = 0x80000000u;   // slotted layout: padding row (x taken as 0)
 constexpr uint32_t kLast = 0x40000000u;  // slotted layout: last row of a chunk
 constexpr uint32_t kSlotIdx = 0x3FFFFFFFu;
-constexpr int kSlotOutChunks = 16;  // chunks per range of a non-affine slotted bin (LDS-staged y offsets)
+constexpr int kSlotOutEntries = 1024;  // y offsets per range of a table-mapped slotted bin (LDS-staged)
 constexpr int64_t kSlotIdxLimit = int64_t(1) << 30;  // gather indices of the slotted layout (30 bits)
 
 // Launches spmv_slots (vbc_slots.hip): returns the hipError_t of the launch.

@@ -95,12 +95,12 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
     for (int e = 0; e < V; e++) acc[e] = dump[e] = T(0);
     int nbuf = 0, cfirst = c;  // staged chunks (NB > 0) and the first of them
     // Without FASTE the y offset of a segment comes from the table (sorted or non-affine segment
-    // orders; bins are cut so a range holds <= kSlotOutChunks chunks): the range's entries are staged
+    // orders; bins are cut so a range holds <= kSlotOutEntries segments): the range's entries are staged
     // in LDS by the prologue, so a flush reads LDS (lgkmcnt) and never waits on the vector loads.
     const int c0 = c;
     if constexpr (!FASTE) {
         if (!b.out_affine) {
-            const int n = min(kSlotOutChunks * RPI, b.nseg - c0 * RPI);
+            const int n = min(kSlotOutEntries, b.nseg - c0 * RPI);
             for (int i = lane; i < n; i += 64) lds_out[i] = G(b.out)[c0 * RPI + i];
         }
     }
@@ -240,6 +240,176 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
     }
 }
 
+// Narrow rows of B'x (w * sizeof(T) < 16: CSC columns for TrSpMV!, fp32 w = 2): one lane holds SPL
+// consecutive segments (slots lane*SPL .. lane*SPL+SPL-1), so each row's values are one 16-B load
+// per lane and its keys one 4-16-B load; the lane folds SPL segments side by side.  Same pipeline,
+// padding, LAST / PAD, staging and y-offset rules as run_slots.
+template <typename T, int W_, int SPL, int U, bool FASTE, int NB, bool KC>
+__device__ __forceinline__ void run_slots_narrow(const SlotBin &b, int r, int lane, const T *__restrict__ x,
+                                                 T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave,
+                                                 int *lds_out)
+{
+    constexpr int NV = SPL * W_;  // values per lane per row (16 B)
+    const int RPI = b.rpi;        // = 64 * SPL
+    const int R0 = G(b.rrow)[r], R1 = G(b.rrow)[r + 1];
+    if (R0 >= R1) return;
+    int c = G(b.rchunk)[r];
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const T> xg = G(x);
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;
+    const cptr bases = (cptr)b.base;
+    typedef T vt __attribute__((ext_vector_type(NV)));
+    auto load = [&](int R, uint32_t (&kk)[U][SPL], uint32_t (&bs)[U], T (&v)[U][NV]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int Rc = min(R + u, R1 - 1);
+            const size_t p = (size_t)Rc * RPI + (size_t)lane * SPL;
+            if constexpr (KC) {
+                typedef int16_t hv __attribute__((ext_vector_type(SPL)));
+                const hv d = __builtin_nontemporal_load((gptr<const hv>)((gptr<const int16_t>)b.key + p));
+#pragma unroll
+                for (int k = 0; k < SPL; k++) kk[u][k] = (uint32_t)(int32_t)d[k];
+                bs[u] = bases[Rc];
+            } else {
+                typedef uint32_t kv __attribute__((ext_vector_type(SPL)));
+                const kv d = __builtin_nontemporal_load((gptr<const kv>)(G(b.key) + p));
+#pragma unroll
+                for (int k = 0; k < SPL; k++) kk[u][k] = d[k];
+                bs[u] = 0;
+            }
+            const vt t = __builtin_nontemporal_load((gptr<const vt>)(val + p * W_));
+#pragma unroll
+            for (int e = 0; e < NV; e++) v[u][e] = t[e];
+        }
+    };
+    constexpr uint32_t kPad16 = 0xFFFF8000u;
+    auto is_pad = [&](uint32_t k) { return KC ? k == kPad16 : (k & kPad) != 0; };
+    auto gather = [&](const uint32_t (&kk)[U][SPL], const uint32_t (&bs)[U], T (&xv)[U][SPL]) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int k = 0; k < SPL; k++) {
+                const uint32_t gi = KC ? (bs[u] & kSlotIdx) + (kk[u][k] == kPad16 ? 0u : kk[u][k]) : kk[u][k] & kSlotIdx;
+                xv[u][k] = xg[gi];
+            }
+    };
+    T acc[NV];
+#pragma unroll
+    for (int e = 0; e < NV; e++) acc[e] = T(0);
+    int nbuf = 0, cfirst = c;
+    const int c0 = c;
+    if constexpr (!FASTE) {
+        if (!b.out_affine) {
+            const int n = min(kSlotOutEntries, b.nseg - c0 * RPI);
+            for (int i = lane; i < n; i += 64) lds_out[i] = G(b.out)[c0 * RPI + i];
+        }
+    }
+    auto write_out = [&]() {  // staged chunks -> one contiguous run of y (RPI * w values per chunk)
+        const int64_t segs = min((int64_t)nbuf * RPI, (int64_t)b.nseg - (int64_t)cfirst * RPI);
+        const int64_t bytes = segs * W_ * (int64_t)sizeof(T);
+        char *dst = reinterpret_cast<char *>(y + b.out_base + (int64_t)cfirst * RPI * b.out_stride);
+        if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
+                if (off + 16 <= bytes) {
+                    *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                } else {
+                    for (int64_t q = off; q < bytes; q += sizeof(T))
+                        *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);
+                }
+            }
+        } else {
+            for (int64_t off = (int64_t)lane * sizeof(T); off < bytes; off += 64 * sizeof(T))
+                *(gptr<T>)(dst + off) = *reinterpret_cast<const T *>(lds_wave + off);
+        }
+        nbuf = 0;
+    };
+    auto flush = [&]() {
+        if constexpr (NB > 0) {
+            vt t;
+#pragma unroll
+            for (int e = 0; e < NV; e++) t[e] = alpha * acc[e];
+            *reinterpret_cast<vt *>(lds_wave + ((size_t)nbuf * 64 + lane) * 16) = t;
+            if (nbuf == 0) cfirst = c;
+        } else {
+            const int seg0 = c * RPI + lane * SPL;
+            if (FASTE && b.out_stride == W_ && seg0 + SPL <= b.nseg) {  // the lane's SPL segments are adjacent in y
+                vt t;
+#pragma unroll
+                for (int e = 0; e < NV; e++) t[e] = alpha * acc[e];
+                *(gptr<vt>)(G(y) + b.out_base + (int64_t)seg0 * W_) = t;
+            } else {
+#pragma unroll
+                for (int k = 0; k < SPL; k++) {
+                    const int seg = seg0 + k;
+                    if (seg < b.nseg) {
+                        const int o = (FASTE || b.out_affine) ? b.out_base + seg * b.out_stride
+                                                              : lds_out[(c - c0) * RPI + lane * SPL + k];
+                        const int lim = b.wst;
+#pragma unroll
+                        for (int e = 0; e < W_; e++) {
+                            if (e >= lim) break;
+                            T q = alpha * acc[k * W_ + e];
+                            if (!FASTE && rd) q = fmadd(beta, G(y)[o + e], q);
+                            G(y)[o + e] = q;
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < NV; e++) acc[e] = T(0);
+        c++;
+        if constexpr (NB > 0) {
+            if (++nbuf == NB) write_out();
+        }
+    };
+    int R1v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
+    auto compute = [&](int R, const uint32_t (&kk)[U][SPL], const uint32_t (&bs)[U], const T (&v)[U][NV],
+                       const T (&xv)[U][SPL]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool live = R + u < R1v;
+#pragma unroll
+            for (int k = 0; k < SPL; k++) {
+                const T xe = is_pad(kk[u][k]) ? T(0) : xv[u][k];
+#pragma unroll
+                for (int e = 0; e < W_; e++) {
+                    const T nv = fmadd(v[u][k * W_ + e], xe, acc[k * W_ + e]);
+                    acc[k * W_ + e] = live ? nv : acc[k * W_ + e];
+                }
+            }
+            const uint32_t lastw = KC ? bs[u] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[u][0]);
+            if (R + u < R1 && (lastw & kLast)) flush();
+        }
+    };
+    uint32_t kA[U][SPL], kB[U][SPL], bA[U], bB[U];
+    T vA[U][NV], vB[U][NV], xv[U][SPL];
+    load(R0, kA, bA, vA);
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int R = R0; R < R1; R += 2 * U) {
+        gather(kA, bA, xv);
+        load(R + U, kB, bB, vB);
+        compute(R, kA, bA, vA, xv);
+        gather(kB, bB, xv);
+        load(R + 2 * U, kA, bA, vA);
+        compute(R + U, kB, bB, vB, xv);
+    }
+    if constexpr (NB > 0) {
+        if (nbuf > 0) write_out();
+    }
+}
+
+// Rows per step of a width: fp32 rows of 16-B lane vectors (w % 4 == 0) take half the launch's U,
+// so every width keeps about the same bytes in flight and the kernel's register budget (the max over
+// its width cases) stays at the FE width's.
+template <typename T>
+__host__ __device__ constexpr int slot_step(int w, int U)
+{
+    return (sizeof(T) == 4 && w > 0 && vec_elems(4, w) == 4) ? U / 2 : U;
+}
+
 template <typename T, int KIND, int U, bool FASTE, int DIAG = 0, int NB = 0, bool KC = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__restrict__ bins, int nbins,
                                                             int total_ranges, int xcd_chunk, const T *__restrict__ x,
@@ -265,18 +435,26 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__res
     const bool rd = rd_i != 0;
     __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * NB * 1024 : 16];
     char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * NB * 1024 : 0);
-    __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutChunks * 64];
-    int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutChunks * 64);
+    __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutEntries];
+    int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutEntries);
+    // narrow B'x rows: fp32 w = 2 only (FE fp32 124 -> 115 us); the w = 1 forms (CSC columns,
+    // 2 / 4 segments per lane) measured slower than one segment per lane (C4: 90 -> 102 us)
+    if constexpr (KIND == 0 && DIAG == 0 && sizeof(T) == 4) {
+        if (b.spl == 2 && b.wkey == 2) {
+            run_slots_narrow<T, 2, 2, U / 2, FASTE, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out);
+            return;
+        }
+    }
     switch (b.wkey) {
-    case 0: run_slots<T, KIND, 0, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 1: run_slots<T, KIND, 1, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 2: run_slots<T, KIND, 2, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 3: run_slots<T, KIND, 3, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 4: run_slots<T, KIND, 4, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 5: run_slots<T, KIND, 5, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 6: run_slots<T, KIND, 6, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 7: run_slots<T, KIND, 7, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
-    case 8: run_slots<T, KIND, 8, U, FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 0: run_slots<T, KIND, 0, slot_step<T>(0, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 1: run_slots<T, KIND, 1, slot_step<T>(1, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 2: run_slots<T, KIND, 2, slot_step<T>(2, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 3: run_slots<T, KIND, 3, slot_step<T>(3, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 4: run_slots<T, KIND, 4, slot_step<T>(4, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 5: run_slots<T, KIND, 5, slot_step<T>(5, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 6: run_slots<T, KIND, 6, slot_step<T>(6, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 7: run_slots<T, KIND, 7, slot_step<T>(7, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
+    case 8: run_slots<T, KIND, 8, slot_step<T>(8, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;
     default: break;
     }
 }
