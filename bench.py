@@ -116,8 +116,10 @@ def main():
         out["secondary"] = {k: s[k] for k in ("value", "unit", "ms_per_step", "gflops")}
         out["secondary"]["workload"] = s["config"]["workload"]
         out["secondary"]["roofline_frac"] = s["roofline"]["frac"]
-        out["secondary"]["note"] = ("uniform-random rows (costs.jl:63-83 generator): every x gather misses L2; "
-                                    "bound by random-access throughput, see DESIGN.md §6")
+        out["secondary"]["kernel"] = s["roofline"]["kernel"]
+        out["secondary"]["note"] = ("uniform-random rows (costs.jl:63-83 generator): no x locality; the row-swept "
+                                    "layout keeps the grid's gathers in a moving window of x, bound by L2-miss "
+                                    "throughput, see DESIGN.md §6")
         if args.workload != "c5":
             c = measure(args, "c5", np.float32, world, rank, local, device, with_cpu=False)
             out["secondary_c5"] = {k: c[k] for k in ("value", "unit", "ms_per_step", "gflops", "dtype")}
@@ -164,6 +166,8 @@ def measure(args, workload, dtype, world, rank, local, device, with_cpu):
     B.handle(local, True, multi=k > 1)  # build the HBM layout outside the timed region
     if k > 1:
         kernel_name = "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
+    elif B.info(local, True)["sweep_bins"] > 0:
+        kernel_name = "vbc::spmv_sweep<T, TB> (row-swept tiles, csrc/vbc_sweep.hip)"
     elif B.info(local, True)["slot_bins"] > 0:
         kernel_name = "vbc::spmv_slots<T, 0, U, FASTE> (slotted segments, csrc/vbc_slots.h)"
     else:

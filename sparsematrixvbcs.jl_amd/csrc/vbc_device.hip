@@ -401,6 +401,133 @@ static void commit_launch_keys(std::vector<PendingSlot> &pss, Arena &ar)
     for (PendingSlot &ps : pss) commit_slot_keys(ps, kc, ar);
 }
 
+// ---- row-swept layout (vbc_sweep.hip) ------------------------------------------------------------
+
+struct PendingSweep {
+    SweepBin b;
+    size_t o_tstep, o_key, o_loc, o_val, o_out;
+};
+
+// Whether a B'x bucket lacks x locality: the rows stored by windows of 64 consecutive stripes (the
+// stripes one slotted chunk folds together) span most of an x too large for L2.  Mesh operators span a
+// few bandwidths (FE: ~10^4 rows of 10^7); the costs.jl:63-83 generator spans all of x.
+static bool want_sweep(const vbc_handle *h, int w, const Stripes &s, const std::vector<int64_t> &stripes)
+{
+    if (h->sweep_mode == 0 || w > 8 || s.m >= kSlotIdxLimit || stripes.empty()) return false;
+    if (h->sweep_mode == 1) return true;
+    const double xbytes = (double)s.m * h->esz;
+    if (xbytes < 16e6) return false;  // x stays in L2 / MALL anyway
+    std::vector<double> span;
+    for (size_t a = 0; a < stripes.size(); a += 64) {
+        int64_t lo = INT64_MAX, hi = -1;
+        for (size_t i = a; i < std::min(stripes.size(), a + 64); i++)
+            for (int64_t r = s.rbeg[stripes[i]]; r < s.rbeg[stripes[i] + 1]; r++) {
+                lo = std::min<int64_t>(lo, s.rows[r]);
+                hi = std::max<int64_t>(hi, s.rows[r]);
+            }
+        if (hi >= 0) span.push_back((double)(hi - lo + 1) * h->esz);
+    }
+    if (span.empty()) return false;
+    std::nth_element(span.begin(), span.begin() + span.size() / 2, span.end());
+    return span[span.size() / 2] >= 0.25 * xbytes;
+}
+
+// Lay out a swept bucket: tiles of S stripes; each tile's stored rows in 64-lane steps, taken in
+// ascending row order by a min-heap over the stripes' next rows (a stripe enters a step at most once,
+// and its rows keep their stored order).
+// Stripes per tile of a swept bucket: as many as the wave's LDS tile holds.  (Capping narrow buckets
+// so that every tile costs the same measured slower on the mixed-width NS workload, 379 -> 395 us.)
+static int sweep_stripes(const vbc_handle *h, int w) { return (int)std::max(1, std::min(65535, h->sweep_tile / (w * h->esz))); }
+
+static int build_sweep(vbc_handle *h, int w, const Stripes &s, const std::vector<int64_t> &stripes, const char *val,
+                       Arena &ar, int &tile0, PendingSweep &pw)
+{
+    const int esz = h->esz;
+    const int64_t nseg = (int64_t)stripes.size();
+    const int S = sweep_stripes(h, w);
+    const int64_t ntiles = (nseg + S - 1) / S;
+    if (nseg >= (int64_t(1) << 31) || tile0 + ntiles >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
+    std::vector<int32_t> tstep{0};
+    std::vector<uint32_t> keys;
+    std::vector<uint16_t> locs;
+    std::vector<int64_t> voffs;  // value offset of each lane slot, -1 = padding
+    keys.reserve(s.rows.size() + 64 * ntiles);
+    typedef std::pair<int32_t, int32_t> Head;  // (row, stripe within tile)
+    std::vector<Head> heap, picks;
+    std::vector<int64_t> cur(S);
+    for (int64_t t = 0; t < ntiles; t++) {
+        const int64_t s0 = t * S;
+        const int ns = (int)std::min<int64_t>(S, nseg - s0);
+        heap.clear();
+        for (int q = 0; q < ns; q++) {
+            const int64_t l = stripes[s0 + q];
+            cur[q] = s.rbeg[l];
+            if (cur[q] < s.rbeg[l + 1]) heap.push_back({s.rows[cur[q]], q});
+        }
+        std::make_heap(heap.begin(), heap.end(), std::greater<Head>());
+        while (!heap.empty()) {
+            picks.clear();
+            while (!heap.empty() && picks.size() < 64) {
+                std::pop_heap(heap.begin(), heap.end(), std::greater<Head>());
+                picks.push_back(heap.back());
+                heap.pop_back();
+            }
+            for (const Head &p : picks) {
+                const int64_t l = stripes[s0 + p.second];
+                keys.push_back((uint32_t)p.first);
+                locs.push_back((uint16_t)p.second);
+                voffs.push_back(s.voff[l] + (cur[p.second] - s.rbeg[l]) * w);
+            }
+            for (size_t k = picks.size(); k < 64; k++) {
+                keys.push_back(kPad);
+                locs.push_back(0);
+                voffs.push_back(-1);
+            }
+            for (const Head &p : picks) {
+                const int64_t l = stripes[s0 + p.second];
+                if (++cur[p.second] < s.rbeg[l + 1]) {
+                    heap.push_back({s.rows[cur[p.second]], p.second});
+                    std::push_heap(heap.begin(), heap.end(), std::greater<Head>());
+                }
+            }
+        }
+        if ((int64_t)keys.size() / 64 >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
+        tstep.push_back((int32_t)(keys.size() / 64));
+    }
+    std::vector<int32_t> out(nseg);
+    for (int64_t q = 0; q < nseg; q++) out[q] = (int32_t)s.col0[stripes[q]];
+    pw = PendingSweep{};
+    SweepBin &b = pw.b;
+    b.w = w;
+    b.tile0 = tile0;
+    b.ntiles = (int32_t)ntiles;
+    b.S = S;
+    b.nseg = (int32_t)nseg;
+    b.out_affine = 1;
+    b.out_base = out.empty() ? 0 : out[0];
+    b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
+    for (size_t q = 1; q < out.size() && b.out_affine; q++)
+        b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * b.out_stride;
+    tile0 += (int)ntiles;
+    const int64_t E = (int64_t)keys.size();
+    pw.o_tstep = ar.reserve(tstep.size() * 4);
+    pw.o_key = ar.reserve(E * 4);
+    pw.o_loc = ar.reserve(E * 2);
+    pw.o_val = ar.reserve(E * w * esz);
+    pw.o_out = ar.reserve(out.size() * 4);
+    std::memcpy(ar.at<int32_t>(pw.o_tstep), tstep.data(), tstep.size() * 4);
+    std::memcpy(ar.at<uint32_t>(pw.o_key), keys.data(), E * 4);
+    std::memcpy(ar.at<uint16_t>(pw.o_loc), locs.data(), E * 2);
+    std::memcpy(ar.at<int32_t>(pw.o_out), out.data(), out.size() * 4);
+    char *vv = ar.at<char>(pw.o_val);
+    for (int64_t e = 0; e < E; e++) {
+        if (voffs[e] >= 0) std::memcpy(vv + e * w * esz, val + voffs[e] * esz, (size_t)w * esz);
+        else std::memset(vv + e * w * esz, 0, (size_t)w * esz);
+    }
+    h->bytes_t += E * (6 + (int64_t)w * esz) + (int64_t)tstep.size() * 4 + (b.out_affine ? 0 : nseg * 4);
+    return VBC_OK;
+}
+
 // Stored width of a transposed bucket.  Widths whose rows do not split into 16-B lane vectors
 // with a power-of-two slot count (w = 3, 5, 6, 7) run the shuffle-scan path with 4-8-B loads; padding
 // them with zero columns buys 16-B loads and the DPP scan for 14-60 % more value bytes.  The padding
@@ -428,15 +555,21 @@ static int padded_width(const vbc_handle *h, int w)
 // slotted (vbc_slots.h, every stripe of the width a segment, empty ones included) when its row counts
 // are near-uniform, else merged (non-empty stripes; empty ones go to the fill list).
 static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                            std::vector<PendingBin> &pbs, std::vector<PendingSlot> &pss, Launch &L,
-                            std::vector<int32_t> &fill)
+                            std::vector<PendingBin> &pbs, std::vector<PendingSlot> &pss,
+                            std::vector<PendingSweep> &pws, Launch &L, std::vector<int32_t> &fill)
 {
     std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
     for (int64_t l = 0; l < s.L; l++) buckets[s.w[l]].push_back(l);
     const int64_t total = (int64_t)s.rows.size();
-    int range0 = 0, srange0 = 0;
+    int range0 = 0, srange0 = 0, tile0 = 0;
     for (auto &kv : buckets) {
         const int w = kv.first;
+        if (want_sweep(h, w, s, kv.second)) {
+            PendingSweep pw;
+            if (int st = build_sweep(h, w, s, kv.second, val, ar, tile0, pw)) return st;
+            pws.push_back(pw);
+            continue;
+        }
         const int wp = padded_width(h, w);
         // the slotted kernel has no scan to feed: fp64 w = 3 runs unpadded (8-B lanes), measured
         // 117 -> 106 us on the ldoor stand-in (fp32 keeps 3 -> 4: 73 vs 84 us unpadded)
@@ -480,6 +613,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         h->bytes_t += ps.rows * ps.b.rpi * ((ps.b.kc ? 2 : 4) + (int64_t)ps.b.w * h->esz) + (ps.b.kc ? ps.rows * 4 : 0);
     L.total_ranges = range0;
     L.slot_ranges = srange0;
+    L.sweep_tiles = tile0;
+    L.sweep_tile_bytes = h->sweep_tile;
+    if (const char *e = getenv("VBC_SWEEP_DIAG")) L.sweep_diag = atoi(e);
     h->bytes_t += (s.m + s.n) * h->esz;  // x read once, y written once
     return VBC_OK;
 }
@@ -693,11 +829,25 @@ static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, P
 }
 
 static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, const std::vector<PendingSlot> &pss,
-                           Launch &L)
+                           Launch &L, const std::vector<PendingSweep> &pws = {})
 {
     L.bins.clear();
     L.sbins.clear();
+    L.wbins.clear();
     char *base = static_cast<char *>(h->d_arena);
+    for (const PendingSweep &pw : pws) {
+        SweepBin b = pw.b;
+        b.tstep = reinterpret_cast<const int32_t *>(base + pw.o_tstep);
+        b.key = reinterpret_cast<const uint32_t *>(base + pw.o_key);
+        b.loc = reinterpret_cast<const uint16_t *>(base + pw.o_loc);
+        b.val = base + pw.o_val;
+        b.out = reinterpret_cast<const int32_t *>(base + pw.o_out);
+        L.wbins.push_back(b);
+    }
+    if (!L.wbins.empty()) {
+        VBC_HIP(hipMalloc(&L.d_wbins, L.wbins.size() * sizeof(SweepBin)));
+        VBC_HIP(hipMemcpy(L.d_wbins, L.wbins.data(), L.wbins.size() * sizeof(SweepBin), hipMemcpyHostToDevice));
+    }
     for (const PendingBin &pb : pbs) {
         Bin b = pb.b;
         b.key = reinterpret_cast<const uint32_t *>(base + pb.o_key);
@@ -736,6 +886,7 @@ static void release(vbc_handle *h)
     DeviceGuard g(h->device);
     if (h->lt.d_bins) (void)hipFree(h->lt.d_bins);
     if (h->lt.d_sbins) (void)hipFree(h->lt.d_sbins);
+    if (h->lt.d_wbins) (void)hipFree(h->lt.d_wbins);
     if (h->lm.d_bins) (void)hipFree(h->lm.d_bins);
     for (auto &l : h->lf) {
         if (l.d_bins) (void)hipFree(l.d_bins);
@@ -808,6 +959,9 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_NARROW")) h->slot_narrow = atoi(e) != 0;
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
+    if (const char *e = getenv("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    h->sweep_tile = (h->esz == 8 ? 4 : 2) * kSweepTileBytes;  // measured on NS: fp64 32 KB 473 us (16 KB 508), fp32 16 KB 313 us (32 KB 353)
+    if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
     if (flags & VBC_CREATE_MULTI) {
@@ -822,6 +976,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     Arena ar;
     std::vector<PendingBin> pt;
     std::vector<PendingSlot> st_t;
+    std::vector<PendingSweep> sw_t;
     std::vector<std::vector<PendingBin>> pf;
     std::vector<std::vector<PendingSlot>> sf;
     std::vector<PendingPanel> pm;
@@ -837,7 +992,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         }
     }
     if (st == VBC_OK && (flags & VBC_CREATE_TRANSPOSED)) {
-        st = build_transposed(h, s, v, ar, pt, st_t, h->lt, fill_t);
+        st = build_transposed(h, s, v, ar, pt, st_t, sw_t, h->lt, fill_t);
         h->has_t = st == VBC_OK;
         if (st == VBC_OK) {
             h->lt.nfill = (int)fill_t.size();
@@ -866,7 +1021,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         release(h);
         return fail(VBC_HIP_ERROR, "hipMemcpy of the matrix arena failed");
     }
-    if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt))) { release(h); return st; }
+    if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt, sw_t))) { release(h); return st; }
     if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)
         if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b]))) { release(h); return st; }
@@ -1040,6 +1195,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     int32_t sl = h->has_t ? (int32_t)h->lt.sbins.size() : 0;
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)l.sbins.size() : 0;
     info->slot_bins = sl;
+    info->sweep_bins = h->has_t ? (int32_t)h->lt.wbins.size() : 0;
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }
@@ -1130,7 +1286,7 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
     }
     bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t;
     for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
-    fused = fused && h->lt.sbins.empty();  // the fused vector kernel reads the merge layout only
+    fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty();  // the fused vector kernel reads the merge layout only
     if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
         const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
         const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;

@@ -32,6 +32,11 @@ struct Launch {
     std::vector<SlotBin> sbins;    // slotted buckets (vbc_slots.h), launched before the merge kernel
     SlotBin *d_sbins = nullptr;
     int slot_ranges = 0;
+    std::vector<SweepBin> wbins;   // row-swept buckets (vbc_sweep.hip, B'x only), launched first
+    SweepBin *d_wbins = nullptr;
+    int sweep_tiles = 0;
+    int sweep_tile_bytes = 0;      // LDS accumulator bytes per wave the layout was cut for
+    int sweep_diag = 0;            // VBC_SWEEP_DIAG ablation (tools/ab.py only)
 };
 
 // The panel layout of the MFMA multi-RHS transposed product (vbc_panel.h): one launch.
@@ -89,6 +94,8 @@ struct vbc_handle {
     int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
     int slot_keys16 = 1;              // VBC_SLOT_KEYS16: 0 keep 32-bit keys, 1 auto, 2 compress whenever possible
     int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
+    int sweep_mode = -1;              // VBC_SWEEP: -1 auto (no x locality), 0 never, 1 always (w <= 8)
+    int sweep_tile = vbc::kSweepTileBytes;  // VBC_SWEEP_TILE=16: 16 KB of LDS accumulators per wave
 };
 
 
