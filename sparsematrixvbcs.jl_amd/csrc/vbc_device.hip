@@ -408,23 +408,30 @@ struct PendingSweep {
     size_t o_tstep, o_key, o_loc, o_val, o_out;
 };
 
-// Whether a B'x bucket lacks x locality: the rows stored by windows of 64 consecutive stripes (the
-// stripes one slotted chunk folds together) span most of an x too large for L2.  Mesh operators span a
-// few bandwidths (FE: ~10^4 rows of 10^7); the costs.jl:63-83 generator spans all of x.
-static bool want_sweep(const vbc_handle *h, int w, const Stripes &s, const std::vector<int64_t> &stripes)
+// Whether a bucket lacks x locality: the gathers of windows of 64 consecutive segments (the segments
+// one slotted chunk folds together) span most of an x (length nx) too large for L2.  Mesh operators
+// span a few bandwidths (FE: ~10^4 rows of 10^7); the costs.jl:63-83 generator spans all of x.
+// Segment q's entries are ents[sbeg[q] .. sbeg[q+1]), keys = gather index.
+static bool sweep_possible(const vbc_handle *h, int w, int64_t nx)
 {
-    if (h->sweep_mode == 0 || w > 8 || s.m >= kSlotIdxLimit || stripes.empty()) return false;
+    return h->sweep_mode != 0 && w <= 8 && nx < kSlotIdxLimit && (h->sweep_mode == 1 || (double)nx * h->esz >= 16e6);
+}
+
+static bool want_sweep(const vbc_handle *h, int w, int64_t nx, const std::vector<int64_t> &sbeg,
+                       const std::vector<Entry> &ents)
+{
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    if (h->sweep_mode == 0 || w > 8 || nx >= kSlotIdxLimit || nseg <= 0 || nseg >= (int64_t(1) << 31)) return false;
     if (h->sweep_mode == 1) return true;
-    const double xbytes = (double)s.m * h->esz;
+    const double xbytes = (double)nx * h->esz;
     if (xbytes < 16e6) return false;  // x stays in L2 / MALL anyway
     std::vector<double> span;
-    for (size_t a = 0; a < stripes.size(); a += 64) {
+    for (int64_t a = 0; a < nseg; a += 64) {
         int64_t lo = INT64_MAX, hi = -1;
-        for (size_t i = a; i < std::min(stripes.size(), a + 64); i++)
-            for (int64_t r = s.rbeg[stripes[i]]; r < s.rbeg[stripes[i] + 1]; r++) {
-                lo = std::min<int64_t>(lo, s.rows[r]);
-                hi = std::max<int64_t>(hi, s.rows[r]);
-            }
+        for (int64_t e = sbeg[a]; e < sbeg[std::min(nseg, a + 64)]; e++) {
+            lo = std::min<int64_t>(lo, ents[e].key);
+            hi = std::max<int64_t>(hi, ents[e].key);
+        }
         if (hi >= 0) span.push_back((double)(hi - lo + 1) * h->esz);
     }
     if (span.empty()) return false;
@@ -432,27 +439,34 @@ static bool want_sweep(const vbc_handle *h, int w, const Stripes &s, const std::
     return span[span.size() / 2] >= 0.25 * xbytes;
 }
 
-// Lay out a swept bucket: tiles of S stripes; each tile's stored rows in 64-lane steps, taken in
-// ascending row order by a min-heap over the stripes' next rows (a stripe enters a step at most once,
-// and its rows keep their stored order).
-// Stripes per tile of a swept bucket: as many as the wave's LDS tile holds.  (Capping narrow buckets
-// so that every tile costs the same measured slower on the mixed-width NS workload, 379 -> 395 us.)
-static int sweep_stripes(const vbc_handle *h, int w) { return (int)std::max(1, std::min(65535, h->sweep_tile / (w * h->esz))); }
+// Segments per tile: as many as the wave's LDS tile holds (kind 0: w accumulators per stripe, kind 1:
+// one per output row).  Capping narrow buckets so that every tile costs the same measured slower on
+// the mixed-width NS workload (379 -> 395 us).
+static int sweep_segments(const vbc_handle *h, int kind, int w)
+{
+    return (int)std::max(1, std::min(65535, h->sweep_tile / ((kind == 0 ? w : 1) * h->esz)));
+}
 
-static int build_sweep(vbc_handle *h, int w, const Stripes &s, const std::vector<int64_t> &stripes, const char *val,
-                       Arena &ar, int &tile0, PendingSweep &pw)
+// Lay out a swept bucket: tiles of S segments; each tile's entries in 64-lane steps, taken in
+// ascending gather order by a min-heap over the segments' next entries (a segment enters a step at
+// most once, and its entries keep their stored order).  out[q] = y offset of segment q.
+static int build_sweep(vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
+                       const std::vector<Entry> &ents, const std::vector<int32_t> &out, const char *val, Arena &ar,
+                       int &tile0, PendingSweep &pw)
 {
     const int esz = h->esz;
-    const int64_t nseg = (int64_t)stripes.size();
-    const int S = sweep_stripes(h, w);
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    const int S = sweep_segments(h, kind, w);
     const int64_t ntiles = (nseg + S - 1) / S;
-    if (nseg >= (int64_t(1) << 31) || tile0 + ntiles >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
+    if (tile0 + ntiles >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
     std::vector<int32_t> tstep{0};
     std::vector<uint32_t> keys;
     std::vector<uint16_t> locs;
     std::vector<int64_t> voffs;  // value offset of each lane slot, -1 = padding
-    keys.reserve(s.rows.size() + 64 * ntiles);
-    typedef std::pair<int32_t, int32_t> Head;  // (row, stripe within tile)
+    keys.reserve(ents.size() + 64 * ntiles);
+    locs.reserve(ents.size() + 64 * ntiles);
+    voffs.reserve(ents.size() + 64 * ntiles);
+    typedef std::pair<uint32_t, int32_t> Head;  // (gather index, segment within tile)
     std::vector<Head> heap, picks;
     std::vector<int64_t> cur(S);
     for (int64_t t = 0; t < ntiles; t++) {
@@ -460,9 +474,8 @@ static int build_sweep(vbc_handle *h, int w, const Stripes &s, const std::vector
         const int ns = (int)std::min<int64_t>(S, nseg - s0);
         heap.clear();
         for (int q = 0; q < ns; q++) {
-            const int64_t l = stripes[s0 + q];
-            cur[q] = s.rbeg[l];
-            if (cur[q] < s.rbeg[l + 1]) heap.push_back({s.rows[cur[q]], q});
+            cur[q] = sbeg[s0 + q];
+            if (cur[q] < sbeg[s0 + q + 1]) heap.push_back({ents[cur[q]].key, q});
         }
         std::make_heap(heap.begin(), heap.end(), std::greater<Head>());
         while (!heap.empty()) {
@@ -473,31 +486,27 @@ static int build_sweep(vbc_handle *h, int w, const Stripes &s, const std::vector
                 heap.pop_back();
             }
             for (const Head &p : picks) {
-                const int64_t l = stripes[s0 + p.second];
-                keys.push_back((uint32_t)p.first);
+                keys.push_back(p.first);
                 locs.push_back((uint16_t)p.second);
-                voffs.push_back(s.voff[l] + (cur[p.second] - s.rbeg[l]) * w);
+                voffs.push_back(ents[cur[p.second]].voff);
             }
             for (size_t k = picks.size(); k < 64; k++) {
                 keys.push_back(kPad);
                 locs.push_back(0);
                 voffs.push_back(-1);
             }
-            for (const Head &p : picks) {
-                const int64_t l = stripes[s0 + p.second];
-                if (++cur[p.second] < s.rbeg[l + 1]) {
-                    heap.push_back({s.rows[cur[p.second]], p.second});
+            for (const Head &p : picks)
+                if (++cur[p.second] < sbeg[s0 + p.second + 1]) {
+                    heap.push_back({ents[cur[p.second]].key, p.second});
                     std::push_heap(heap.begin(), heap.end(), std::greater<Head>());
                 }
-            }
         }
         if ((int64_t)keys.size() / 64 >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
         tstep.push_back((int32_t)(keys.size() / 64));
     }
-    std::vector<int32_t> out(nseg);
-    for (int64_t q = 0; q < nseg; q++) out[q] = (int32_t)s.col0[stripes[q]];
     pw = PendingSweep{};
     SweepBin &b = pw.b;
+    b.kind = kind;
     b.w = w;
     b.tile0 = tile0;
     b.ntiles = (int32_t)ntiles;
@@ -524,7 +533,8 @@ static int build_sweep(vbc_handle *h, int w, const Stripes &s, const std::vector
         if (voffs[e] >= 0) std::memcpy(vv + e * w * esz, val + voffs[e] * esz, (size_t)w * esz);
         else std::memset(vv + e * w * esz, 0, (size_t)w * esz);
     }
-    h->bytes_t += E * (6 + (int64_t)w * esz) + (int64_t)tstep.size() * 4 + (b.out_affine ? 0 : nseg * 4);
+    (kind == 0 ? h->bytes_t : h->bytes_f) +=
+        E * (6 + (int64_t)w * esz) + (int64_t)tstep.size() * 4 + (b.out_affine ? 0 : nseg * 4);
     return VBC_OK;
 }
 
@@ -564,11 +574,23 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     int range0 = 0, srange0 = 0, tile0 = 0;
     for (auto &kv : buckets) {
         const int w = kv.first;
-        if (want_sweep(h, w, s, kv.second)) {
-            PendingSweep pw;
-            if (int st = build_sweep(h, w, s, kv.second, val, ar, tile0, pw)) return st;
-            pws.push_back(pw);
-            continue;
+        if (sweep_possible(h, w, s.m)) {
+            std::vector<int64_t> sb{0};
+            std::vector<Entry> ents;
+            std::vector<int32_t> out;
+            ents.reserve(s.rbeg[s.L] - s.rbeg[0]);
+            for (int64_t l : kv.second) {
+                sb.push_back(sb.back() + s.rbeg[l + 1] - s.rbeg[l]);
+                out.push_back((int32_t)s.col0[l]);
+                for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
+                    ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+            }
+            if (want_sweep(h, w, s.m, sb, ents)) {
+                PendingSweep pw;
+                if (int st = build_sweep(h, 0, w, sb, ents, out, val, ar, tile0, pw)) return st;
+                pws.push_back(pw);
+                continue;
+            }
         }
         const int wp = padded_width(h, w);
         // the slotted kernel has no scan to feed: fp64 w = 3 runs unpadded (8-B lanes), measured
@@ -625,7 +647,8 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
 // layout takes every row as a segment (affine, no fill list).
 static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
                          std::vector<std::vector<PendingBin>> &pbs, std::vector<std::vector<PendingSlot>> &pss,
-                         std::vector<Launch> &Ls, std::vector<int32_t> &fill)
+                         std::vector<std::vector<PendingSweep>> &pws, std::vector<Launch> &Ls,
+                         std::vector<int32_t> &fill)
 {
     std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
     for (int64_t l = 0; l < s.L; l++)
@@ -639,6 +662,34 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) cnt[s.rows[r] + 1]++;
         for (int64_t i = 0; i < s.m; i++) cnt[i + 1] += cnt[i];
         const bool single = buckets.size() == 1;
+        // swept only as the single bucket: with several, every bucket's launch would sweep x and all of
+        // y again (mixed-width NS fp64: 904 -> 1280 us measured)
+        if ((single || h->sweep_mode == 1) && sweep_possible(h, w, s.n)) {
+            // every output row a segment (rows without blocks in this bucket keep beta * y)
+            std::vector<Entry> ents(cnt[s.m]);
+            for (int64_t i = 0; i < s.m; i++) cur[i] = cnt[i];
+            for (int64_t l : kv.second)
+                for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
+                    ents[cur[s.rows[r]]++] = {(uint32_t)s.col0[l], s.voff[l] + (r - s.rbeg[l]) * w};
+            std::vector<int64_t> sb(cnt.begin(), cnt.end());
+            if (want_sweep(h, w, s.n, sb, ents)) {
+                std::vector<int32_t> out(s.m);
+                for (int64_t i = 0; i < s.m; i++) out[i] = (int32_t)i;
+                PendingSweep pw;
+                int tile0 = 0;
+                if (int st = build_sweep(h, 1, w, sb, ents, out, val, ar, tile0, pw)) return st;
+                h->bytes_f += s.m * h->esz;  // y written once per bucket
+                std::fill(any.begin(), any.end(), 1);
+                Ls.emplace_back();
+                Ls.back().sweep_tiles = tile0;
+                Ls.back().sweep_tile_bytes = h->sweep_tile;
+                if (const char *e = getenv("VBC_SWEEP_DIAG")) Ls.back().sweep_diag = atoi(e);
+                pbs.push_back({});
+                pss.push_back({});
+                pws.push_back({pw});
+                continue;
+            }
+        }
         std::vector<int64_t> sbeg{0};
         std::vector<int32_t> sout;
         for (int64_t i = 0; i < s.m; i++)
@@ -667,6 +718,7 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
             for (int32_t i : sout) any[i] = 1;
             pbs.push_back({});
             pss.push_back(std::move(one));
+            pws.push_back({});
             Ls.back().slot_ranges = srange0;
             continue;
         }
@@ -679,6 +731,7 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
         h->bytes_f += (int64_t)ents.size() * (4 + (int64_t)w * h->esz) + (int64_t)out.size() * (4 + h->esz);
         pbs.push_back({pb});
         pss.push_back({});
+        pws.push_back({});
         Ls.back().total_ranges = range0;
     }
     h->f_scale = buckets.size() > 1;
@@ -891,6 +944,7 @@ static void release(vbc_handle *h)
     for (auto &l : h->lf) {
         if (l.d_bins) (void)hipFree(l.d_bins);
         if (l.d_sbins) (void)hipFree(l.d_sbins);
+        if (l.d_wbins) (void)hipFree(l.d_wbins);
     }
     if (h->d_arena) (void)hipFree(h->d_arena);
     if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
@@ -979,6 +1033,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     std::vector<PendingSweep> sw_t;
     std::vector<std::vector<PendingBin>> pf;
     std::vector<std::vector<PendingSlot>> sf;
+    std::vector<std::vector<PendingSweep>> wf;
     std::vector<PendingPanel> pm;
     std::vector<int32_t> fill_t, fill_f, fill_m;
     int st = VBC_OK;
@@ -1001,7 +1056,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         }
     }
     if (st == VBC_OK && (flags & VBC_CREATE_FORWARD)) {
-        st = build_forward(h, s, v, ar, pf, sf, h->lf, fill_f);
+        st = build_forward(h, s, v, ar, pf, sf, wf, h->lf, fill_f);
         h->has_f = st == VBC_OK;
         if (st == VBC_OK) {
             if (h->lf.empty()) h->lf.emplace_back();  // no entries: the fill list alone writes y
@@ -1024,7 +1079,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt, sw_t))) { release(h); return st; }
     if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)
-        if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b]))) { release(h); return st; }
+        if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b], wf[b]))) { release(h); return st; }
     if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
     *out = h;
     return VBC_OK;
@@ -1195,7 +1250,9 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     int32_t sl = h->has_t ? (int32_t)h->lt.sbins.size() : 0;
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)l.sbins.size() : 0;
     info->slot_bins = sl;
-    info->sweep_bins = h->has_t ? (int32_t)h->lt.wbins.size() : 0;
+    int32_t sw = h->has_t ? (int32_t)h->lt.wbins.size() : 0;
+    for (auto &l : h->lf) sw += h->has_f ? (int32_t)l.wbins.size() : 0;
+    info->sweep_bins = sw;
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }

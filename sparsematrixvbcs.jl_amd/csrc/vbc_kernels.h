@@ -106,11 +106,13 @@ constexpr uint32_t kSlotIdx = 0x3FFFFFFFu;
 constexpr int kSlotOutEntries = 1024;  // y offsets per range of a table-mapped slotted bin (LDS-staged)
 constexpr int64_t kSlotIdxLimit = int64_t(1) << 30;  // gather indices of the slotted layout (30 bits)
 
-// One width bucket of B'x in the row-swept layout (vbc_sweep.h): tiles of S consecutive stripes whose
-// y accumulators live in LDS; a tile's stored rows are packed into 64-lane steps in ascending x-row
-// order (no stripe twice in a step), so the whole grid sweeps x front to back and the gathers of the
-// concurrently resident waves fall into an L2-sized window of x.
+// One width bucket in the row-swept layout (vbc_sweep.hip): tiles of S consecutive segments (B'x:
+// stripes; Bx: output rows) whose y accumulators live in LDS; a tile's entries are packed into 64-lane
+// steps in ascending gather order (no segment twice in a step), so the whole grid sweeps x front to
+// back and the gathers of the concurrently resident waves fall into a narrow window of x.
 struct SweepBin {
+    int32_t kind;        // 0: B'x (segment = stripe, w outputs), 1: Bx (segment = output row)
+    int32_t pad_;
     int32_t w;           // entry width (1..8)
     int32_t tile0;       // first tile (wave) of this bucket in the launch
     int32_t ntiles;
@@ -120,15 +122,15 @@ struct SweepBin {
     int32_t out_base;
     int32_t out_stride;
     const int32_t *tstep;  // ntiles + 1: first step of each tile
-    const uint32_t *key;   // steps * 64: PAD | gather index
-    const uint16_t *loc;   // steps * 64: stripe within the tile
+    const uint32_t *key;   // steps * 64: PAD | gather index (B'x: x row; Bx: first x column)
+    const uint16_t *loc;   // steps * 64: segment within the tile
     const void *val;       // steps * 64 * w values
     const int32_t *out;    // per stripe: first y column (when not affine)
 };
 constexpr int kSweepTileBytes = 8192;  // LDS accumulators per wave: VBC_SWEEP_TILE = 8 / 16 / 32 (KB)
 
 // Launches spmv_sweep (vbc_sweep.hip): returns the hipError_t of the launch.
-int launch_sweep(int esz, const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag, const void *x,
+int launch_sweep(int esz, int kind, const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag, const void *x,
                  void *y, double alpha, double beta, bool rd, hipStream_t stream);
 
 // Launches spmv_slots (vbc_slots.hip): returns the hipError_t of the launch.

@@ -17,7 +17,7 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
     if (L.sweep_tiles > 0) {
-        const hipError_t e = (hipError_t)launch_sweep((int)sizeof(T), L.d_wbins, (int)L.wbins.size(), L.sweep_tiles,
+        const hipError_t e = (hipError_t)launch_sweep((int)sizeof(T), kind, L.d_wbins, (int)L.wbins.size(), L.sweep_tiles,
                                                       L.sweep_tile_bytes, L.sweep_diag, x, y, alpha, beta, rd, stream);
         if (e != hipSuccess) {
             set_error("spmv_sweep launch failed: %s", hipGetErrorString(e));

@@ -52,13 +52,19 @@ __device__ __forceinline__ void ld_row(gptr<const T> p, T (&r)[W_])
 // U steps per pipeline stage; loads are unconditional (steps past the tile re-read its last step and
 // are never folded), as in the slotted kernel.  DIAG (ablations, tools/ab.py only): 1 = gathers
 // confined to a 1 MB window of x, 2 = no LDS fold (products summed in registers, one LDS store).
-template <typename T, int W_, int U, int DIAG>
+// KIND 0 (B'x): a lane gathers x[row] and folds its w products into its stripe's w accumulators.
+// KIND 1 (Bx): a lane gathers the w-wide slice x[j ...] of its block's stripe and adds the block's
+// dot product to its output row's accumulator -- per row the blocks come in stripe order, as in the
+// reference's serial stripe loop (multiply_1DVBC.jl:62-71).
+template <typename T, int KIND, int W_, int U, int DIAG>
 __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, const T *__restrict__ x,
                                           T *__restrict__ y, T alpha, T beta, bool rd, T *acc)
 {
+    constexpr int OW = KIND == 0 ? W_ : 1;  // accumulators per segment
+    constexpr int XV = KIND == 0 ? 1 : W_;  // x values per entry
     const int s0 = t * b.S;
     const int ns = min(b.S, b.nseg - s0);
-    const int nel = ns * W_;
+    const int nel = ns * OW;
     for (int i = lane; i < nel; i += 64) acc[i] = T(0);
     const int S0 = G(b.tstep)[t], S1 = G(b.tstep)[t + 1];
     const gptr<const T> val = G(static_cast<const T *>(b.val));
@@ -80,32 +86,39 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
 #pragma unroll
         for (int u = 0; u < U; u++) ld_row<T, W_>(val + ((size_t)min(s + u, S1 - 1) * 64 + lane) * W_, v[u]);
     };
-    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&ll)[U], T (&xv)[U], uint32_t (&fl)[U]) {
+    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&ll)[U], T (&xv)[U][XV], uint32_t (&fl)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            xv[u] = xg[(kk[u] & kSlotIdx) & (DIAG == 1 ? 0x1FFFFu : kSlotIdx)];
+            const uint32_t gi = (kk[u] & kSlotIdx) & (DIAG == 1 ? 0x1FFFFu : kSlotIdx);
+#pragma unroll
+            for (int e = 0; e < XV; e++) xv[u][e] = xg[gi + e];
             fl[u] = ll[u] | (kk[u] & kPad);
         }
     };
     T racc = T(0);
-    auto fold = [&](int s, const T (&v)[U][W_], const T (&xv)[U], const uint32_t (&fl)[U]) {
+    auto fold = [&](int s, const T (&v)[U][W_], const T (&xv)[U][XV], const uint32_t (&fl)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (s + u < S1 && !(fl[u] & kPad)) {
                 if constexpr (DIAG == 2) {
 #pragma unroll
-                    for (int e = 0; e < W_; e++) racc = fmadd(v[u][e], xv[u], racc + T(fl[u]));
-                } else {
+                    for (int e = 0; e < W_; e++) racc = fmadd(v[u][e], xv[u][KIND == 0 ? 0 : e], racc + T(fl[u]));
+                } else if constexpr (KIND == 0) {
                     T *a = acc + fl[u] * W_;
 #pragma unroll
-                    for (int e = 0; e < W_; e++) a[e] = fmadd(v[u][e], xv[u], a[e]);
+                    for (int e = 0; e < W_; e++) a[e] = fmadd(v[u][e], xv[u][0], a[e]);
+                } else {
+                    T d = v[u][0] * xv[u][0];
+#pragma unroll
+                    for (int e = 1; e < W_; e++) d = fmadd(v[u][e], xv[u][e], d);
+                    acc[fl[u]] += d;
                 }
             }
         }
     };
     if (S0 < S1) {
         uint32_t kA[U], lA[U], kB[U], lB[U], fA[U], fB[U];
-        T vA[U][W_], vB[U][W_], xA[U], xB[U];
+        T vA[U][W_], vB[U][W_], xA[U][XV], xB[U][XV];
         loadk(S0, kA, lA);
         loadv(S0, vA);
         gather(kA, lA, xA, fA);
@@ -122,9 +135,9 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
         }
     }
     if constexpr (DIAG == 2) acc[lane % max(nel, 1)] = racc;
-    // y for the tile's stripes, written once
-    if (b.out_affine && b.out_stride == W_) {
-        const gptr<T> yo = G(y) + b.out_base + (int64_t)s0 * W_;
+    // y for the tile's segments, written once
+    if (b.out_affine && b.out_stride == OW) {
+        const gptr<T> yo = G(y) + b.out_base + (int64_t)s0 * OW;
         for (int i = lane; i < nel; i += 64) {
             T q = alpha * acc[i];
             if (rd) q = fmadd(beta, yo[i], q);
@@ -132,7 +145,7 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
         }
     } else {
         for (int i = lane; i < nel; i += 64) {
-            const int sl = i / W_, e = i - sl * W_;
+            const int sl = i / OW, e = i - sl * OW;
             const int o = b.out_affine ? b.out_base + (s0 + sl) * b.out_stride : G(b.out)[s0 + sl];
             T q = alpha * acc[i];
             if (rd) q = fmadd(beta, G(y)[o + e], q);
@@ -143,7 +156,7 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
 
 // One wave per workgroup: the workgroup's LDS is exactly the wave's tile (TB bytes), so occupancy is
 // LDS / TB waves per CU with no idle partner waves.
-template <typename T, int TB, int DIAG = 0>
+template <typename T, int KIND, int TB, int DIAG = 0>
 __global__ __launch_bounds__(64) void spmv_sweep(const SweepBin *__restrict__ bins, int nbins, int total_tiles,
                                                  const T *__restrict__ x, T *__restrict__ y, T alpha, T beta, int rd_i)
 {
@@ -160,46 +173,48 @@ __global__ __launch_bounds__(64) void spmv_sweep(const SweepBin *__restrict__ bi
     // steps per stage: ~16 values per lane per buffer whatever the width (w = 4: 4 steps in flight)
 #define U(W) (16 / W < 2 ? 2 : 16 / W > 8 ? 8 : 16 / W)
     switch (b.w) {
-    case 1: run_sweep<T, 1, U(1), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 2: run_sweep<T, 2, U(2), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 3: run_sweep<T, 3, U(3), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 4: run_sweep<T, 4, U(4), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 5: run_sweep<T, 5, U(5), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 6: run_sweep<T, 6, U(6), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 7: run_sweep<T, 7, U(7), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 8: run_sweep<T, 8, U(8), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 1: run_sweep<T, KIND, 1, U(1), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 2: run_sweep<T, KIND, 2, U(2), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 3: run_sweep<T, KIND, 3, U(3), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 4: run_sweep<T, KIND, 4, U(4), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 5: run_sweep<T, KIND, 5, U(5), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 6: run_sweep<T, KIND, 6, U(6), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 7: run_sweep<T, KIND, 7, U(7), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 8: run_sweep<T, KIND, 8, U(8), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
     default: break;
     }
 #undef U
 }
 
-template <typename T, int TB, int DIAG = 0>
+template <typename T, int KIND, int TB, int DIAG = 0>
 static void launch_t(const SweepBin *d_bins, int nbins, int total_tiles, const void *x, void *y, double alpha,
                      double beta, bool rd, hipStream_t s)
 {
-    hipLaunchKernelGGL((spmv_sweep<T, TB, DIAG>), dim3(total_tiles), dim3(64), 0, s, d_bins, nbins, total_tiles,
+    hipLaunchKernelGGL((spmv_sweep<T, KIND, TB, DIAG>), dim3(total_tiles), dim3(64), 0, s, d_bins, nbins, total_tiles,
                        static_cast<const T *>(x), static_cast<T *>(y), (T)alpha, (T)beta, (int)rd);
 }
 
-template <typename T>
+template <typename T, int KIND>
 static void launch_any(const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag, const void *x,
                        void *y, double alpha, double beta, bool rd, hipStream_t s)
 {
-    if constexpr (sizeof(T) == 8) {  // ablations (tools/ab.py only)
-        if (diag == 1 && tile_bytes == 2 * kSweepTileBytes) return launch_t<T, 2 * kSweepTileBytes, 1>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
-        if (diag == 2 && tile_bytes == 2 * kSweepTileBytes) return launch_t<T, 2 * kSweepTileBytes, 2>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
+    if constexpr (sizeof(T) == 8 && KIND == 0) {  // ablations (tools/ab.py only)
+        if (diag == 1 && tile_bytes == 2 * kSweepTileBytes) return launch_t<T, KIND, 2 * kSweepTileBytes, 1>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
+        if (diag == 2 && tile_bytes == 2 * kSweepTileBytes) return launch_t<T, KIND, 2 * kSweepTileBytes, 2>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
     }
-    if (tile_bytes >= 4 * kSweepTileBytes) launch_t<T, 4 * kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
-    else if (tile_bytes >= 2 * kSweepTileBytes) launch_t<T, 2 * kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
-    else launch_t<T, kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
+    if (tile_bytes >= 4 * kSweepTileBytes) launch_t<T, KIND, 4 * kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
+    else if (tile_bytes >= 2 * kSweepTileBytes) launch_t<T, KIND, 2 * kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
+    else launch_t<T, KIND, kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
 }
 
-int launch_sweep(int esz, const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag, const void *x,
-                 void *y, double alpha, double beta, bool rd, hipStream_t stream)
+int launch_sweep(int esz, int kind, const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag,
+                 const void *x, void *y, double alpha, double beta, bool rd, hipStream_t stream)
 {
     if (total_tiles <= 0) return hipSuccess;
-    if (esz == 8) launch_any<double>(d_bins, nbins, total_tiles, tile_bytes, diag, x, y, alpha, beta, rd, stream);
-    else launch_any<float>(d_bins, nbins, total_tiles, tile_bytes, diag, x, y, alpha, beta, rd, stream);
+#define VBC_SWEEP_ARGS d_bins, nbins, total_tiles, tile_bytes, diag, x, y, alpha, beta, rd, stream
+    if (esz == 8) { if (kind == 0) launch_any<double, 0>(VBC_SWEEP_ARGS); else launch_any<double, 1>(VBC_SWEEP_ARGS); }
+    else { if (kind == 0) launch_any<float, 0>(VBC_SWEEP_ARGS); else launch_any<float, 1>(VBC_SWEEP_ARGS); }
+#undef VBC_SWEEP_ARGS
     return hipGetLastError();
 }
 

@@ -1,9 +1,10 @@
-"""GPU parity of the row-swept B'x layout (csrc/vbc_sweep.hip) against the oracle.
+"""GPU parity of the row-swept layout (csrc/vbc_sweep.hip) against the oracle, both directions.
 
-The library picks the swept layout for a B'x width bucket (w <= 8) whose neighbouring stripes store
-unrelated rows of a large x (the costs.jl:63-83 generator); VBC_SWEEP=1 forces it for every bucket of
-width <= 8, so the reference's own corpus (golden matrices, sprand grid, ragged / empty stripes) runs
-through it too.  Each stripe still folds its rows in stored (reference) order, so the one-hot probes
+The library picks the swept layout for a width bucket (w <= 8) whose neighbouring segments gather
+from unrelated places of a large x (the costs.jl:63-83 generator); VBC_SWEEP=1 forces it for every
+bucket of width <= 8, so the reference's own corpus (golden matrices, sprand grid, ragged / empty
+stripes) runs through it too.  Each segment still folds its entries in stored (reference) order --
+B'x: a stripe's rows in row order; Bx: an output row's blocks in stripe order -- so the one-hot probes
 are bit-exact; random x: tolerances of test_gpu_parity.py (1e-12 fp64, 1e-5 fp32).
 """
 import numpy as np
@@ -30,20 +31,22 @@ def forced(request, monkeypatch):
     return request.param
 
 
-def sweep_bins(B):
-    return B.info(trans=True)["sweep_bins"]
+def sweep_bins(B, trans=True):
+    return B.info(trans=trans)["sweep_bins"]
 
 
 def one_hot_t(B, A):
-    """Every e_i through mul!(y, B', x): the rows of A, exactly (runtests.jl:63-87)."""
+    """Every e_i through mul!(y, B', x) and every e_j through mul!(y, B, x): the rows / columns of A,
+    exactly (runtests.jl:29-53, 63-87)."""
     m, n = A.shape
     D = A.toarray()
-    E = torch.eye(m, dtype=torch.float64, device=DEV)
-    Y = torch.full((m, n), float("nan"), dtype=torch.float64, device=DEV)
-    for i in range(m):
-        V.mul_(Y[i], V.adjoint(B), E[i])
-    got = Y.cpu().numpy()
-    assert np.array_equal(got, D), np.argwhere(got != D)[:5]
+    for trans, nin, nout, ref in ((True, m, n, D), (False, n, m, D.T)):
+        E = torch.eye(nin, dtype=torch.float64, device=DEV)
+        Y = torch.full((nin, nout), float("nan"), dtype=torch.float64, device=DEV)
+        for i in range(nin):
+            V.mul_(Y[i], V.adjoint(B) if trans else B, E[i])
+        got = Y.cpu().numpy()
+        assert np.array_equal(got, ref), (trans, np.argwhere(got != ref)[:5])
 
 
 def test_forced_golden_one_hot(golden, forced):
@@ -51,7 +54,7 @@ def test_forced_golden_one_hot(golden, forced):
         for meth in METHODS_1D:
             B = V.SparseMatrix1DVBC[4](g["A"], meth())
             one_hot_t(B, g["A"])
-            assert sweep_bins(B) > 0, key
+            assert sweep_bins(B) > 0 and sweep_bins(B, trans=False) > 0, key
         B = V.SparseMatrixVBC[4, 4](g["A"], V.AlternatingPacker(V.StrictChunker(4), V.StrictChunker(4)))
         one_hot_t(B, g["A"])
 
@@ -64,7 +67,8 @@ def test_forced_sprand_grid_one_hot(forced):
 @pytest.mark.parametrize("widths", [[1], [2], [3], [4], [5, 6, 7, 8], [2, 9], [3, 17, 64]])
 def test_forced_widths_tiles(forced, widths):
     """Every compile-time width, buckets mixing swept (w <= 8) and merged / slotted (w > 8) stripes,
-    several tiles per bucket (L > S) with a partial last tile, alpha / beta, both dtypes."""
+    several tiles per bucket with a partial last tile, alpha / beta, both dtypes, both directions
+    (forward with several buckets: beta scaling first, then one accumulating launch per bucket)."""
     rng = np.random.default_rng(sum(widths) + 11)
     L = 2600
     w = np.array([widths[i % len(widths)] for i in range(L)])
@@ -72,14 +76,16 @@ def test_forced_widths_tiles(forced, widths):
     for dtype, tol in ((np.float64, TOL64), (np.float32, TOL32)):
         Bd = B if dtype == np.float64 else V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs,
                                                                B.val.astype(np.float32))
-        assert sweep_bins(Bd) == len([v for v in set(widths) if v <= 8])
-        x = rng.uniform(-1, 1, B.m).astype(dtype)
-        y0 = rng.uniform(-1, 1, B.n).astype(dtype)
-        for alpha, beta in ((1.0, 0.0), (0.5, -1.5)):
-            yd = dev(y0)
-            V.mul_(yd, V.adjoint(Bd), dev(x), alpha, beta)
-            yr = oracle_ref(B, x.astype(np.float64), y0.astype(np.float64), alpha, beta, True)
-            assert rel(yd.cpu().numpy(), yr) <= tol, (widths, dtype, alpha, beta)
+        nsw = len([v for v in set(widths) if v <= 8])
+        assert sweep_bins(Bd) == nsw and sweep_bins(Bd, trans=False) == nsw
+        for trans, nx, ny in ((True, B.m, B.n), (False, B.n, B.m)):
+            x = rng.uniform(-1, 1, nx).astype(dtype)
+            y0 = rng.uniform(-1, 1, ny).astype(dtype)
+            for alpha, beta in ((1.0, 0.0), (0.5, -1.5)):
+                yd = dev(y0)
+                V.mul_(yd, V.adjoint(Bd) if trans else Bd, dev(x), alpha, beta)
+                yr = oracle_ref(B, x.astype(np.float64), y0.astype(np.float64), alpha, beta, trans)
+                assert rel(yd.cpu().numpy(), yr) <= tol, (widths, dtype, trans, alpha, beta)
 
 
 def test_forced_summation_order_bitwise(forced):
@@ -93,6 +99,10 @@ def test_forced_summation_order_bitwise(forced):
     y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
     V.mul_(y, B.T, dev(x))
     assert np.array_equal(y.cpu().numpy(), O.mul(R, x, np.zeros(B.n), trans=True))
+    xf = rng.integers(-2**33, 2**33, B.n).astype(np.float64)
+    y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(y, B, dev(xf))
+    assert np.array_equal(y.cpu().numpy(), O.mul(R, xf, np.zeros(B.m), trans=False))
 
 
 def test_forced_nonfinite_x_stays_in_place(forced):
@@ -111,6 +121,14 @@ def test_forced_nonfinite_x_stays_in_place(forced):
     assert np.array_equal(np.isinf(got), np.isinf(ref))
     fin = np.isfinite(ref)
     assert rel(got[fin], ref[fin]) <= TOL64
+    xf = rng.uniform(-1, 1, B.n)
+    xf[0] = np.nan
+    xf[5] = np.inf
+    y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(y, B, dev(xf))
+    got, ref = y.cpu().numpy(), O.mul(R, xf, np.zeros(B.m), trans=False)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(np.isinf(got), np.isinf(ref))
 
 
 def test_forced_edge_cases(forced):
@@ -135,6 +153,11 @@ def test_forced_edge_cases(forced):
             y = dev(y0)
             V.mul_(y, B.T, dev(x), 1.0, beta)
             assert rel(y.cpu().numpy(), D.T @ x + beta * y0) <= TOL64
+            xf = rng.uniform(-1, 1, 12)
+            y0 = rng.uniform(-1, 1, 20000)
+            y = dev(y0)
+            V.mul_(y, B, dev(xf), 1.0, beta)
+            assert rel(y.cpu().numpy(), D @ xf + beta * y0) <= TOL64
 
 
 def test_forced_trspmv_and_multi_rhs(golden, forced):
@@ -159,7 +182,7 @@ def test_auto_uniform_rows_use_sweep(dtype):
     """Auto mode: the uniform-row generator at an x beyond L2 (m = 4e6) is laid out swept; the FE
     mesh operator of a similar size is not.  Parity against the oracle on the swept one."""
     B = V.synthetic.north_star(dtype=dtype, scale=0.4)
-    assert sweep_bins(B) == 1
+    assert sweep_bins(B) == 1 and sweep_bins(B, trans=False) == 1
     rng = np.random.default_rng(0xC0FFEE)
     x = rng.uniform(-1, 1, B.m).astype(dtype)
     y = torch.zeros(B.n, dtype=torch.from_numpy(x).dtype, device=DEV)
@@ -167,5 +190,10 @@ def test_auto_uniform_rows_use_sweep(dtype):
     R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
     yr = O.mul(R, x.astype(np.float64), np.zeros(B.n), trans=True)
     assert rel(y.cpu().numpy(), yr) <= (TOL64 if dtype == np.float64 else TOL32)
+    xf = rng.uniform(-1, 1, B.n).astype(dtype)
+    y = torch.zeros(B.m, dtype=torch.from_numpy(xf).dtype, device=DEV)
+    V.mul_(y, B, dev(xf))
+    yr = O.mul(R, xf.astype(np.float64), np.zeros(B.m), trans=False)
+    assert rel(y.cpu().numpy(), yr) <= (TOL64 if dtype == np.float64 else TOL32)
     F = V.synthetic.fe_grid_2d(1000, dof=2, dtype=dtype)
-    assert sweep_bins(F) == 0
+    assert sweep_bins(F) == 0 and sweep_bins(F, trans=False) == 0
