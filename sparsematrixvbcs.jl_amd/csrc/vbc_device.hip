@@ -9,6 +9,7 @@
 #include <map>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "vbc_handle.h"
@@ -153,7 +154,8 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
 
 struct PendingSlot {
     SlotBin b;
-    size_t o_key, o_val, o_out, o_rrow, o_rchunk, o_base = 0;
+    size_t o_key, o_val, o_out, o_rrow, o_rchunk, o_base = 0, o_doff = 0;
+    int64_t key_bytes = 0;       // index bytes as stored (keys, deltas, bases, delta offsets)
     std::vector<uint32_t> keys;  // full keys until commit_slot_keys picks the stored form
     int64_t rows = 0;
     bool kc_ok = false;          // every row's keys fit base + int16 deltas
@@ -175,8 +177,11 @@ static bool slot_keys_compressible(const std::vector<uint32_t> &keys, int64_t ro
     return true;
 }
 
-// Store a slotted bin's keys: full 32-bit keys, or (kc) per-row bases + int16 deltas.
-static void commit_slot_keys(PendingSlot &ps, bool kc, Arena &ar)
+// Store a slotted bin's keys: full 32-bit keys, or (kc) per-row bases + int16 deltas.  Compressed rows
+// with identical delta patterns are stored once (a mesh operator's interior chunks all share one --
+// FE: [0, 2, 4, ...] -- so its delta stream collapses to a few KB that stay in L2); each row carries
+// the offset of its pattern.  VBC_SLOT_DEDUP=0 keeps one pattern per row (A/B).
+static void commit_slot_keys(PendingSlot &ps, bool kc, Arena &ar, bool dedup)
 {
     const int RPI = ps.b.rpi;
     const int64_t E = ps.rows * RPI;
@@ -184,11 +189,10 @@ static void commit_slot_keys(PendingSlot &ps, bool kc, Arena &ar)
     if (!kc) {
         ps.o_key = ar.reserve(E * 4);
         std::memcpy(ar.at<uint32_t>(ps.o_key), ps.keys.data(), E * 4);
+        ps.key_bytes = E * 4;
     } else {
-        ps.o_key = ar.reserve(E * 2);
-        ps.o_base = ar.reserve(ps.rows * 4);
-        int16_t *d = ar.at<int16_t>(ps.o_key);
-        uint32_t *bs = ar.at<uint32_t>(ps.o_base);
+        std::vector<int16_t> d(E);
+        std::vector<uint32_t> bs(ps.rows), doff(ps.rows);
         for (int64_t r = 0; r < ps.rows; r++) {
             const uint32_t *k = ps.keys.data() + r * RPI;
             uint32_t base = 0;
@@ -198,6 +202,27 @@ static void commit_slot_keys(PendingSlot &ps, bool kc, Arena &ar)
             for (int s = 0; s < RPI; s++)
                 d[r * RPI + s] = (k[s] & kPad) ? INT16_MIN : (int16_t)((int64_t)(k[s] & kSlotIdx) - (int64_t)base);
         }
+        std::unordered_map<std::string, uint32_t> seen;
+        int64_t stored = 0;  // distinct patterns, in rows
+        for (int64_t r = 0; r < ps.rows; r++) {
+            const int16_t *row = d.data() + r * RPI;
+            if (dedup) {
+                std::string kbytes(reinterpret_cast<const char *>(row), (size_t)RPI * 2);
+                auto it = seen.find(kbytes);
+                if (it != seen.end()) { doff[r] = it->second; continue; }
+                seen.emplace(std::move(kbytes), (uint32_t)(stored * RPI));
+            }
+            if (stored != r) std::memmove(d.data() + stored * RPI, row, (size_t)RPI * 2);
+            doff[r] = (uint32_t)(stored * RPI);
+            stored++;
+        }
+        ps.o_key = ar.reserve(stored * RPI * 2);
+        ps.o_base = ar.reserve(ps.rows * 4);
+        ps.o_doff = ar.reserve(ps.rows * 4);
+        std::memcpy(ar.at<int16_t>(ps.o_key), d.data(), (size_t)stored * RPI * 2);
+        std::memcpy(ar.at<uint32_t>(ps.o_base), bs.data(), (size_t)ps.rows * 4);
+        std::memcpy(ar.at<uint32_t>(ps.o_doff), doff.data(), (size_t)ps.rows * 4);
+        ps.key_bytes = stored * RPI * 2 + ps.rows * 8;
     }
     std::vector<uint32_t>().swap(ps.keys);
 }
@@ -394,11 +419,11 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
 }
 
 // One launch's slotted bins share one key form (the kernel is specialised on it).
-static void commit_launch_keys(std::vector<PendingSlot> &pss, Arena &ar)
+static void commit_launch_keys(const vbc_handle *h, std::vector<PendingSlot> &pss, Arena &ar)
 {
     bool kc = !pss.empty();
     for (const PendingSlot &ps : pss) kc = kc && ps.kc_ok;
-    for (PendingSlot &ps : pss) commit_slot_keys(ps, kc, ar);
+    for (PendingSlot &ps : pss) commit_slot_keys(ps, kc, ar, h->slot_dedup);
 }
 
 // ---- row-swept layout (vbc_sweep.hip) ------------------------------------------------------------
@@ -630,9 +655,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)wp * h->esz) + (int64_t)out.size() * 4;
         pbs.push_back(pb);
     }
-    commit_launch_keys(pss, ar);
+    commit_launch_keys(h, pss, ar);
     for (const PendingSlot &ps : pss)  // slotted bins: padded rows x (index bytes + values)
-        h->bytes_t += ps.rows * ps.b.rpi * ((ps.b.kc ? 2 : 4) + (int64_t)ps.b.w * h->esz) + (ps.b.kc ? ps.rows * 4 : 0);
+        h->bytes_t += ps.rows * ps.b.rpi * (int64_t)ps.b.w * h->esz + ps.key_bytes;
     L.total_ranges = range0;
     L.slot_ranges = srange0;
     L.sweep_tiles = tile0;
@@ -711,9 +736,9 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
             if (int st = build_slots(h, 1, w, w, ents, sbeg, sout, (int64_t)ents.size(), val, ar, srange0, ps, order)) return st;
             std::vector<PendingSlot> one;
             one.push_back(std::move(ps));
-            commit_launch_keys(one, ar);
+            commit_launch_keys(h, one, ar);
             const PendingSlot &p1 = one[0];
-            h->bytes_f += p1.rows * p1.b.rpi * ((p1.b.kc ? 2 : 4) + (int64_t)w * h->esz) + (p1.b.kc ? p1.rows * 4 : 0) +
+            h->bytes_f += p1.rows * p1.b.rpi * (int64_t)w * h->esz + p1.key_bytes +
                           (int64_t)sout.size() * h->esz;
             for (int32_t i : sout) any[i] = 1;
             pbs.push_back({});
@@ -919,6 +944,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.rrow = reinterpret_cast<const int32_t *>(base + ps.o_rrow);
         b.rchunk = reinterpret_cast<const int32_t *>(base + ps.o_rchunk);
         b.base = reinterpret_cast<const uint32_t *>(base + ps.o_base);
+        b.kdoff = reinterpret_cast<const uint32_t *>(base + ps.o_doff);
         L.sbins.push_back(b);
     }
     L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
@@ -1013,6 +1039,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_NARROW")) h->slot_narrow = atoi(e) != 0;
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
+    if (const char *e = getenv("VBC_SLOT_DEDUP")) h->slot_dedup = atoi(e) != 0;
     if (const char *e = getenv("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     h->sweep_tile = (h->esz == 8 ? 4 : 2) * kSweepTileBytes;  // measured on NS: fp64 32 KB 473 us (16 KB 508), fp32 16 KB 313 us (32 KB 353)
     if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;

@@ -92,6 +92,7 @@ struct vbc_handle {
     int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)
     int64_t slot_rows_padded_last = 0;
     int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
+    bool slot_dedup = true;           // VBC_SLOT_DEDUP=0: one stored delta pattern per compressed row
     int slot_keys16 = 1;              // VBC_SLOT_KEYS16: 0 keep 32-bit keys, 1 auto, 2 compress whenever possible
     int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
     int sweep_mode = -1;              // VBC_SWEEP: -1 auto (no x locality), 0 never, 1 always (w <= 8)

@@ -89,6 +89,7 @@ struct SlotBin {
     int32_t spl;         // segments per lane (narrow B'x rows: 16 / (w * sizeof(T))), else 1
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
+    const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key
     const void *val;       // rows * rpi * w values
     const int32_t *out;    // per segment (when not affine)
     const int32_t *rrow;   // per range: first row, nranges + 1 entries

@@ -66,13 +66,14 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
     // the waitcnt pass can count them exactly through the pipeline.
     typedef __attribute__((address_space(4))) const uint32_t *cptr;  // scalar (constant) loads
     const cptr bases = (cptr)b.base;
+    const cptr doffs = (cptr)b.kdoff;
     auto load = [&](int R, uint32_t (&kk)[U], uint32_t (&bs)[U], T (&v)[U][V]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int Rc = min(R + u, R1 - 1);
             const size_t p = (size_t)Rc * RPI + lslot;
-            if constexpr (KC) {
-                kk[u] = (uint32_t)(int32_t)__builtin_nontemporal_load((gptr<const int16_t>)key + p);
+            if constexpr (KC) {  // shared delta patterns: cached loads
+                kk[u] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + lslot];
                 bs[u] = bases[Rc];
             } else {
                 kk[u] = __builtin_nontemporal_load(key + p);
@@ -258,6 +259,7 @@ __device__ __forceinline__ void run_slots_narrow(const SlotBin &b, int r, int la
     const gptr<const T> xg = G(x);
     typedef __attribute__((address_space(4))) const uint32_t *cptr;
     const cptr bases = (cptr)b.base;
+    const cptr doffs = (cptr)b.kdoff;
     typedef T vt __attribute__((ext_vector_type(NV)));
     auto load = [&](int R, uint32_t (&kk)[U][SPL], uint32_t (&bs)[U], T (&v)[U][NV]) {
 #pragma unroll
@@ -266,7 +268,7 @@ __device__ __forceinline__ void run_slots_narrow(const SlotBin &b, int r, int la
             const size_t p = (size_t)Rc * RPI + (size_t)lane * SPL;
             if constexpr (KC) {
                 typedef int16_t hv __attribute__((ext_vector_type(SPL)));
-                const hv d = __builtin_nontemporal_load((gptr<const hv>)((gptr<const int16_t>)b.key + p));
+                const hv d = *(gptr<const hv>)((gptr<const int16_t>)b.key + (size_t)doffs[Rc] + (size_t)lane * SPL);
 #pragma unroll
                 for (int k = 0; k < SPL; k++) kk[u][k] = (uint32_t)(int32_t)d[k];
                 bs[u] = bases[Rc];

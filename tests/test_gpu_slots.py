@@ -51,6 +51,28 @@ def test_forced_golden_one_hot_full_keys(golden, forced, monkeypatch):
         one_hot_probes(V.SparseMatrix1DVBC[4](g["A"], METHODS_1D[1]()), g["A"])
 
 
+@pytest.mark.parametrize("dedup", ["0", "1"])
+def test_shared_delta_patterns(monkeypatch, dedup):
+    """Compressed rows with identical delta patterns are stored once (VBC_SLOT_DEDUP=1, the default):
+    the FE operator's interior chunks share one pattern, its boundary chunks keep their own; results
+    are identical with and without sharing."""
+    monkeypatch.setenv("VBC_SLOT_DEDUP", dedup)
+    B = V.synthetic.fe_grid_2d(200, dof=2)
+    assert slot_bins(B) == 1
+    rng = np.random.default_rng(17)
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    for trans, nx, ny in ((True, B.m, B.n), (False, B.n, B.m)):
+        x = rng.uniform(-1, 1, nx)
+        yd = torch.zeros(ny, dtype=torch.float64, device=DEV)
+        V.mul_(yd, V.adjoint(B) if trans else B, dev(x))
+        assert rel(yd.cpu().numpy(), O.mul(R, x, np.zeros(ny), trans=trans)) <= TOL64, trans
+    shared = B.info(trans=True)["bytes_t"]
+    monkeypatch.setenv("VBC_SLOT_DEDUP", "0" if dedup == "1" else "1")
+    C = V.synthetic.fe_grid_2d(200, dof=2)
+    other = C.info(trans=True)["bytes_t"]
+    assert (shared < other) if dedup == "1" else (shared > other)
+
+
 def test_keys16_falls_back_on_wide_deltas(monkeypatch):
     """Rows whose keys span more than int16 keep 32-bit keys (and stay exact)."""
     monkeypatch.setenv("VBC_SLOTS", "1")
