@@ -93,6 +93,10 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
 #pragma unroll
             for (int e = 0; e < XV; e++) xv[u][e] = xg[gi + e];
             fl[u] = ll[u] | (kk[u] & kPad);
+            // materialise fl here: otherwise the compiler sinks it past the next key loads, keeps the
+            // old keys alive across them, and the register copies at the back edge cost a vmcnt(0)
+            // drain per iteration
+            asm volatile("" : "+v"(fl[u]));
         }
     };
     T racc = T(0);
@@ -170,7 +174,8 @@ __global__ __launch_bounds__(64) void spmv_sweep(const SweepBin *__restrict__ bi
     const int t = g - b.tile0;
     T *acc = reinterpret_cast<T *>(lds);
     const bool rd = rd_i != 0;
-    // steps per stage: ~16 values per lane per buffer whatever the width (w = 4: 4 steps in flight)
+    // Steps per stage: ~16 values per lane per buffer whatever the width (w = 4: 4 steps in flight).
+    // Twice as many (up to 256 VGPRs; occupancy is set by the LDS tile anyway) measured the same.
 #define U(W) (16 / W < 2 ? 2 : 16 / W > 8 ? 8 : 16 / W)
     switch (b.w) {
     case 1: run_sweep<T, KIND, 1, U(1), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
