@@ -73,6 +73,26 @@ def test_shared_delta_patterns(monkeypatch, dedup):
     assert (shared < other) if dedup == "1" else (shared > other)
 
 
+def test_fe_nonfinite_and_unaligned_x():
+    """The production FE layout (slotted, shared delta patterns): Inf / NaN of x stay where the
+    reference puts them, and an x view that is only 8-B aligned gives the same bits."""
+    B = V.synthetic.fe_grid_2d(120, dof=2)
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    rng = np.random.default_rng(23)
+    x = rng.uniform(-1, 1, B.m)
+    x[[0, 7, 501, B.m - 1]] = [np.nan, np.inf, -np.inf, np.nan]
+    ref = O.mul(R, x, np.zeros(B.n), trans=True)
+    for off in (0, 1):
+        buf = torch.zeros(B.m + 1, dtype=torch.float64, device=DEV)
+        buf[off:off + B.m] = dev(x)
+        y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+        V.mul_(y, B.T, buf[off:off + B.m])
+        got = y.cpu().numpy()
+        assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref)), off
+        fin = np.isfinite(ref)
+        assert np.array_equal(got[fin], ref[fin]), off
+
+
 def test_keys16_falls_back_on_wide_deltas(monkeypatch):
     """Rows whose keys span more than int16 keep 32-bit keys (and stay exact)."""
     monkeypatch.setenv("VBC_SLOTS", "1")
