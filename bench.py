@@ -180,8 +180,8 @@ def measure(args, workload, dtype, world, rank, local, device, with_cpu):
 
     # HIP events on the launching stream bracket the K back-to-back products of the timed region:
     # avg_launch_ms = event span / K (an event pair around every product would put two extra markers
-    # between consecutive kernels of the timed region); rocprofv3's per-kernel average agrees
-    # (profiles/r01_fe_kernel_stats.csv).
+    # between consecutive kernels of the timed region); rocprofv3's per-kernel average of the same
+    # process agrees (profiles/r01_bench_kernel_stats.csv).
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
