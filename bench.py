@@ -4,13 +4,24 @@ A step is one mul!(y, B', x) -- the transposed 1D-VBR product the reference's pa
 time (bin/test_table.jl:80) -- fp64, inputs resident in HBM.  Primary workload (BASELINE.json
 target: "10M x 10M, ~1e8-nnz SuiteSparse-like matrix"): `fe`, a 2D finite-element operator
 (5-point stencil, 2 unknowns per node, 1.0e7 x 1.0e7, 1.0e8 stored values) in 1DVBC form.
-Secondary (reported in the same line at N=1): `ns`, SURVEY.md §8d's NS-1DVBC, the reference's own
-uniform-random VBR generator (costs.jl:63-83) at 1e7 x 1e7, 1e8 nonzeros, width-4 stripes.
-N ranks = N GPUs, one process each (torchrun); every rank owns its own block-row shard of that size
-(weak scaling, no data-path collective: the transposed product writes disjoint y ranges).
-rank 0 prints one JSON line.
 
-    python bench.py [--gpus N --steps K --warmup W --workload fe|ns|ns-mixed --dtype f64|f32]
+N = 1 (plain `python bench.py`): the primary line carries `roofline` (HIP events on the launching
+stream + the committed rocprofv3 / PMC summaries), `cpu_baseline` (the reference's SIMD CPU kernel,
+oracle/vbc_simd.c, on the host cores) and `parity` (the GPU y of the timed region against the CPU
+oracle, oracle/vbc_oracle.c, on the same full-size input).  Secondaries in the same line:
+`fe3d` (irregular 3D stiffness stand-in, 1e7 rows / 1e8 nnz), `ns` (SURVEY §8d's uniform-random
+NS-1DVBC from the reference's own generator, costs.jl:63-83) and `c5` (2D VBC, 16 RHS, matrix cores).
+
+N > 1 (torchrun, one process per GPU): STRONG scaling of ONE matrix.  Every rank builds the same
+matrix, keeps its byte-balanced stripe range (distributed.ShardedSparseMatrix1DVBC, the GPU grid
+replacing the reference's threaded stripe loop multiply_1DVBC.jl:169-177) and times K products of
+its shard; `value` = algorithmic bytes of the WHOLE matrix / the slowest rank's time.  B'x writes
+disjoint y slices, so the primary needs no collective; `e2e` adds the all_gather that replicates y
+(RCCL over xGMI), and the C3 secondary (ldoor stand-in) reports the same plus the forward product
+with its RCCL all_reduce of y.
+
+    python bench.py [--gpus N --steps K --warmup W --workload fe|fe3d|ns|ns-mixed|c5|ldoor|ct20stif
+                     --dtype f64|f32]
 """
 import argparse
 import json
@@ -25,6 +36,16 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "1DVBC SpMV effective GB/s (and GFLOP/s) vs HBM roofline, 1/2/4/8 GPU"
+PARITY_TOL = {np.dtype(np.float64): 1e-10, np.dtype(np.float32): 1e-5}  # normwise rel-err (BASELINE)
+
+WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
+             "ns-mixed": "NS-1DVBC-mixed-w1..8-1e8nnz-uniform",
+             "fe": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2 (SuiteSparse-like mesh operator)",
+             "fe3d": "FE-3D-stiffness-dof3-1e7x1e7-1e8nnz-w3 (irregular: random 18-neighbour subsets)",
+             "c5": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS (costs.jl:200-220 generator)",
+             "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
+             "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)"}
 
 
 def algorithmic_bytes(B, esz, ti=4, nrhs=1):
@@ -49,37 +70,301 @@ def load_traffic(workload, dtype):
     return None, None
 
 
-def cpu_baseline(B, x, esz, budget_s=12.0, max_reps=20):
-    """Oracle (C restatement of multiply_1DVBC.jl:85-180 / multiply_VBC.jl:89-192, OpenMP dynamic-1
-    stripe scheduling) on the host cores, full-size product repeated until ~budget_s of CPU work;
-    several right-hand sides run one oracle product per column (the reference has no matrix mul!)."""
+def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
+    import sparsematrixvbcs_amd as V
+    if workload == "fe":
+        return V.synthetic.fe_grid_2d(int(round(2236 * scale ** 0.5)), dof=2, dtype=dtype, seed=seed)
+    if workload == "fe3d":
+        n = 3 * int(round(3333333 * scale))
+        return V.synthetic.fe_stiffness_3d_1dvbc(n, int(round(1e8 * scale)), 3, dtype=dtype, seed=seed)
+    if workload == "c5":
+        return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
+    if workload in ("ldoor", "ct20stif"):
+        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif"}[workload]
+        try:
+            A = V.io.mdopen(name, dtype=dtype).A
+        except FileNotFoundError:
+            A = V.synthetic.standin(name, dtype=dtype, seed=seed)
+        # bin/test_table.jl:27 stores A = permutedims(A): B'x multiplies the original matrix
+        return V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
+    return V.synthetic.north_star(dtype=dtype, scale=scale, seed=seed, mixed=(workload == "ns-mixed"))
+
+
+def kernel_name(B, local, k):
+    if k > 1:
+        return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
+    inf = B.info(local, True)
+    if inf["sweep_bins"] > 0:
+        return "vbc::spmv_sweep<T, TB> (row-swept tiles, csrc/vbc_sweep.hip)"
+    if inf["slot_bins"] > 0:
+        return "vbc::spmv_slots<T, 0, U, FASTE> (slotted segments, csrc/vbc_slots.h)"
+    return "vbc::spmv_ranges<T, 0, K, P> (+ vbc::fixup)"
+
+
+def timed_products(step, steps, device, stream, world, graph=True):
+    """Times EXACTLY `steps` calls of step() (barrier + synchronize on both sides).  With graph=True
+    the K products are captured once into a HIP graph (torch.cuda.CUDAGraph) and the timed region is
+    one replay; HIP events on the launching stream bracket it.  Returns (wall s, event ms / step)."""
+    import torch
+    import torch.distributed as dist
+    g = None
+    if graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                for _ in range(steps):
+                    step()
+            torch.cuda.synchronize(device)
+        except Exception:  # capture unsupported for this call sequence: eager launches
+            g = None
+            torch.cuda.synchronize(device)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        ev0.record(stream)
+        if g is not None:
+            g.replay()
+        else:
+            for _ in range(steps):
+                step()
+        ev1.record(stream)
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    return elapsed, ev0.elapsed_time(ev1) / steps, g is not None
+
+
+def parity(B, x_host, y_dev, k=1, cols=(0,)):
+    """Normwise relative error of the GPU y against the CPU oracle on the same full-size input
+    (oracle/vbc_oracle.c: multiply_1DVBC.jl:90-180 / multiply_VBC.jl:93-192 restated)."""
     from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    from oracle import simd as S
+    th = S.host_threads()
     if hasattr(B, "Pi"):
         R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
     else:
         R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
-    X = x.reshape(B.m, -1)
-    k = X.shape[1]
-    cols = [np.ascontiguousarray(X[:, j]) for j in range(k)]
-    y = np.zeros(B.n, dtype=B.val.dtype)
+    yg = y_dev.cpu().numpy()
+    X = x_host.reshape(B.m, -1)
+    Yg = yg.reshape(B.n, -1)
+    num = den = 0.0
+    bitwise = True
+    t0 = time.perf_counter()
+    for c in (cols if k > 1 else (0,)):
+        ref = O.mul(R, np.ascontiguousarray(X[:, c]), np.zeros(B.n, B.val.dtype), trans=True, nthreads=th)
+        g = Yg[:, c]
+        num += float(np.sum((g.astype(np.float64) - ref) ** 2))
+        den += float(np.sum(ref.astype(np.float64) ** 2))
+        bitwise = bitwise and bool(np.array_equal(g, ref))
+    err = (num ** 0.5) / max(den ** 0.5, 1e-300)
+    tol = PARITY_TOL[np.dtype(B.val.dtype)]
+    return {"rel_err": float(f"{err:.3e}"), "tol": tol, "pass": bool(err <= tol), "bitwise_equal": bitwise,
+            "oracle": "oracle/vbc_oracle.c orc_*_mul_t (multiply_1DVBC.jl:90-180 / multiply_VBC.jl:93-192)",
+            "columns": list(cols) if k > 1 else None, "oracle_s": round(time.perf_counter() - t0, 2)}
 
-    def product():
-        for c in cols:
-            O.mul(R, c, y, trans=True, nthreads=threads)
 
-    O.mul(R, cols[0], y, trans=True, nthreads=threads)  # warm-up (page faults)
-    times = []
-    t_start = time.perf_counter()
-    while len(times) < max_reps and (time.perf_counter() - t_start) < budget_s:
+def cpu_baseline(B, x_host, esz, budget_s=4.0):
+    """The reference's SIMD CPU kernel (oracle/vbc_simd.c: Vec{Δw} buckets, @fastmath, Int64
+    indices; multiply_1DVBC.jl:90-180) on the full workload, on all host cores with the reference's
+    one-stripe atomic self-scheduling (:169-177) and with 64-stripe grabs, and on 1 core.  `value` is
+    the faster all-core figure (the honest, not understated, baseline)."""
+    from oracle import simd as S
+    th = S.host_threads()
+    x = np.ascontiguousarray(x_host.reshape(B.m, -1)[:, 0])
+    y = np.zeros(B.n, B.val.dtype)
+    nbytes = algorithmic_bytes(B, esz)
+
+    def run(nthreads, chunk):
+        S.mul_t(B, x, y, nthreads, chunk)  # warm-up
+        ts, t_start = [], time.perf_counter()
+        while len(ts) < 30 and time.perf_counter() - t_start < budget_s:
+            t0 = time.perf_counter()
+            S.mul_t(B, x, y, nthreads, chunk)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), len(ts)
+
+    t_ref, n_ref = run(th, 1)
+    t_chk, n_chk = run(th, 64)
+    t_one, n_one = run(1, 1)
+    best = min(t_ref, t_chk)
+    return dict(value=round(nbytes / best / 1e9, 3), unit="GB/s", cores=th, kind="port",
+                sample=(f"full workload, mul!(y,B',x) with the reference's SIMD kernel (oracle/vbc_simd.c, "
+                        f"{S.isa()}, -O3 -ffast-math, Int64 indices): {th} threads reference schedule "
+                        f"(1 stripe per atomic grab) {t_ref * 1e3:.1f} ms (median of {n_ref}), 64-stripe grabs "
+                        f"{t_chk * 1e3:.1f} ms ({n_chk}), 1 core {t_one * 1e3:.1f} ms ({n_one})"),
+                ms_all_cores_ref_schedule=round(t_ref * 1e3, 3), ms_all_cores_chunk64=round(t_chk * 1e3, 3),
+                ms_1core=round(t_one * 1e3, 3), value_1core=round(nbytes / t_one / 1e9, 3),
+                nproc=os.cpu_count(), cpu_model=S.cpu_model(), isa=S.isa())
+
+
+def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=None):
+    """One single-GPU workload: build, warm up, time K products, optional CPU baseline + parity."""
+    import torch
+
+    import sparsematrixvbcs_amd as V
+
+    steps = steps or args.steps
+    esz = np.dtype(dtype).itemsize
+    t_build = time.perf_counter()
+    B = build_matrix(workload, dtype, args.scale)
+    rng = np.random.default_rng(0xC0FFEE)
+    k = args.nrhs if workload == "c5" else 1
+    x_host = rng.uniform(-1, 1, (B.m, k) if k > 1 else B.m).astype(dtype)
+    x = torch.from_numpy(x_host).to(device)  # k > 1: row-major X (right-hand sides interleaved)
+    y = torch.empty((B.n, k) if k > 1 else B.n, dtype=x.dtype, device=device)
+    Bt = B.T
+    stream = torch.cuda.Stream(device)
+    with torch.cuda.stream(stream):
+        B.handle(local, True, multi=k > 1)  # build the HBM layout outside the timed region
+        t_build = time.perf_counter() - t_build
+        for _ in range(args.warmup):
+            V.mul_(y, Bt, x)
+    torch.cuda.synchronize(device)
+    elapsed, kernel_ms, graphed = timed_products(lambda: V.mul_(y, Bt, x), steps, device, stream, 1,
+                                                 graph=not args.eager)
+    bytes_launch = algorithmic_bytes(B, esz, nrhs=k)
+    nnz = int(np.count_nonzero(B.val))
+    ms_per_step = elapsed / steps * 1e3
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(workload, "f64" if dtype == np.float64 else "f32")
+    out = {
+        "value": round(bytes_launch * steps / elapsed / 1e9, 2),
+        "unit": "GB/s",
+        "ms_per_step": round(ms_per_step, 5),
+        "gflops": round(2.0 * nnz * k * steps / elapsed / 1e9, 2),
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel_name(B, local, k),
+            "bytes_per_launch": bytes_launch, "avg_launch_ms": round(kernel_ms, 5), "traffic_source": traffic_src,
+        },
+        "config": {
+            "workload": WORKLOADS[workload] + (f"-scale{args.scale}" if args.scale != 1.0 else ""),
+            "op": ("mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if k == 1 else
+                   f"Y = B'X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:89-192 per column), "
+                   "matrix-core panel kernel"),
+            "m": B.m, "n": B.n, "stripes": len(B.Phi), "row_blocks": int(B.pos[-1] - 1), "nnz": nnz, "W": B.W,
+            "index_bytes": 4, "nrhs": k, "launch": "hipGraph of K products" if graphed else "eager",
+            "build_s": round(t_build, 1),
+        },
+        "dtype": "f64" if dtype == np.float64 else "f32",
+    }
+    if with_parity:
+        out["parity"] = parity(B, x_host, y, k, cols=(0, k - 1) if k > 1 else (0,))
+    if with_cpu:
+        out["cpu_baseline"] = cpu_baseline(B, x_host, esz)
+    B.release()
+    del x, y
+    torch.cuda.empty_cache()
+    return out
+
+
+def measure_sharded(args, workload, dtype, world, rank, local, device, forward=False):
+    """Strong scaling: ONE matrix split by stripes over the ranks; kernel-only and end-to-end."""
+    import torch
+    import torch.distributed as dist
+
+    import sparsematrixvbcs_amd as V
+
+    esz = np.dtype(dtype).itemsize
+    B = build_matrix(workload, dtype, args.scale)  # same seed on every rank: one matrix
+    S = V.distributed.ShardedSparseMatrix1DVBC(B, rank, world, split="stripes")
+    bytes_total = algorithmic_bytes(B, esz)
+    bytes_local = algorithmic_bytes(S.local, esz)
+    nnz_total = int(np.count_nonzero(B.val[:B.ofs[-1] - 1]))
+    rng = np.random.default_rng(0xC0FFEE)
+    x_host = rng.uniform(-1, 1, B.m).astype(dtype)
+    x = torch.from_numpy(x_host).to(device)
+    y_local = torch.empty(S.n_local, dtype=x.dtype, device=device)
+    stream = torch.cuda.Stream(device)
+    with torch.cuda.stream(stream):
+        S.local.handle(local, True)
+        for _ in range(args.warmup):
+            S.local_mul_t(y_local, x)
+    torch.cuda.synchronize(device)
+    elapsed, kernel_ms, graphed = timed_products(lambda: S.local_mul_t(y_local, x), args.steps, device, stream,
+                                                 world, graph=not args.eager)
+
+    # end-to-end: the product plus the all_gather that replicates y on every rank (RCCL over xGMI)
+    y_full = torch.empty(B.n, dtype=x.dtype, device=device)
+
+    def e2e():
+        S.local_mul_t(y_local, x)
+        y_full.copy_(S.gather(y_local))
+
+    e2e_steps = max(5, args.steps // 5)
+    with torch.cuda.stream(stream):
+        e2e()
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for _ in range(e2e_steps):
+            e2e()
+    torch.cuda.synchronize(device)
+    e2e_elapsed = time.perf_counter() - t0
+    dist.barrier()
+
+    fwd = None
+    if forward:  # mul!(y, B, x): partial y per rank + one RCCL all_reduce(sum)
+        S.local.handle(local, False)
+        xf = torch.from_numpy(rng.uniform(-1, 1, B.n).astype(dtype)).to(device)
+        yf = torch.empty(B.m, dtype=x.dtype, device=device)
+        with torch.cuda.stream(stream):
+            S.mul(yf, xf)
+        torch.cuda.synchronize(device)
+        dist.barrier()
         t0 = time.perf_counter()
-        product()
-        times.append(time.perf_counter() - t0)
-    t = float(np.median(times))
-    what = "mul!(y,B',x)" if k == 1 else f"B'X ({k} columns, one mul!(y,B',x) each)"
-    return dict(value=round(algorithmic_bytes(B, esz, nrhs=k) / t / 1e9, 3), unit="GB/s", cores=threads,
-                kind="port", sample=f"full workload, median of {len(times)} oracle {what} "
-                                    f"runs ({t * 1e3:.1f} ms each), {threads} OpenMP threads")
+        with torch.cuda.stream(stream):
+            for _ in range(e2e_steps):
+                S.mul(yf, xf)
+        torch.cuda.synchronize(device)
+        fwd_elapsed = time.perf_counter() - t0
+        dist.barrier()
+        fwd = fwd_elapsed
+
+    stats = torch.tensor([elapsed, kernel_ms, e2e_elapsed, fwd or 0.0], dtype=torch.float64, device=device)
+    mx = stats.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    mn = stats.clone()
+    dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+    elapsed, kernel_ms, e2e_elapsed, fwd_elapsed = (v.item() for v in mx)
+    out = {
+        "value": round(bytes_total * args.steps / elapsed / 1e9, 2),
+        "unit": "GB/s",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "gflops": round(2.0 * nnz_total * args.steps / elapsed / 1e9, 2),
+        "roofline": {
+            "bound": "hbm", "achieved": round(bytes_local / (kernel_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(bytes_local / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None, "kernel": kernel_name(S.local, local, 1), "bytes_per_launch": bytes_local,
+            "avg_launch_ms": round(kernel_ms, 5), "scope": "rank 0 shard; avg_launch_ms is the max over ranks",
+        },
+        "e2e": {"value": round(bytes_total * e2e_steps / e2e_elapsed / 1e9, 2), "unit": "GB/s",
+                "ms_per_step": round(e2e_elapsed / e2e_steps * 1e3, 4),
+                "what": "mul!(y_local, B_r', x) + all_gather of y over RCCL (replicated y on every rank)"},
+        "config": {
+            "workload": WORKLOADS[workload] + (f"-scale{args.scale}" if args.scale != 1.0 else ""),
+            "op": "mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180), stripe-sharded",
+            "m": B.m, "n": B.n, "stripes": len(B.Phi), "nnz": nnz_total, "W": B.W, "index_bytes": 4,
+            "n_local_rank0": S.n_local, "stripe_cuts": S.cuts.tolist(),
+            "parallelism": f"stripe split x{world}: disjoint y slices, no data-path collective",
+            "launch": "hipGraph of K products" if graphed else "eager",
+        },
+        "dtype": "f64" if dtype == np.float64 else "f32",
+    }
+    if forward:
+        out["forward_allreduce"] = {"value": round(bytes_total * e2e_steps / fwd_elapsed / 1e9, 2), "unit": "GB/s",
+                                    "ms_per_step": round(fwd_elapsed / e2e_steps * 1e3, 4),
+                                    "what": "mul!(y, B, x): partial y per rank + RCCL all_reduce(sum) of y"}
+    S.local.release()
+    del x, y_local, y_full
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -87,12 +372,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="fe", choices=["fe", "ns", "ns-mixed", "c5"])
+    ap.add_argument("--workload", default="fe", choices=list(WORKLOADS))
     ap.add_argument("--nrhs", type=int, default=16, help="right-hand sides of the c5 workload")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of one graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary (uniform) workload")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary workloads")
     args = ap.parse_args()
 
     import torch
@@ -105,161 +392,49 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
-
     dtype = np.float64 if args.dtype == "f64" else np.float32
-    out = measure(args, args.workload, dtype, world, rank, local, device, with_cpu=not args.no_cpu_baseline)
-    if world == 1 and not args.no_secondary:
-        sec = "ns" if args.workload != "ns" else "fe"
-        s = measure(args, sec, dtype, world, rank, local, device, with_cpu=False)
-        out["secondary"] = {k: s[k] for k in ("value", "unit", "ms_per_step", "gflops")}
-        out["secondary"]["workload"] = s["config"]["workload"]
-        out["secondary"]["roofline_frac"] = s["roofline"]["frac"]
-        out["secondary"]["kernel"] = s["roofline"]["kernel"]
-        out["secondary"]["note"] = ("uniform-random rows (costs.jl:63-83 generator): no x locality; the row-swept "
-                                    "layout keeps the grid's gathers in a moving window of x, bound by L2-miss "
-                                    "throughput, see DESIGN.md §6")
-        if args.workload != "c5":
-            c = measure(args, "c5", np.float32, world, rank, local, device, with_cpu=False)
-            out["secondary_c5"] = {k: c[k] for k in ("value", "unit", "ms_per_step", "gflops", "dtype")}
-            out["secondary_c5"]["workload"] = c["config"]["workload"]
-            out["secondary_c5"]["op"] = c["config"]["op"]
-            out["secondary_c5"]["roofline_frac"] = c["roofline"]["frac"]
-            out["secondary_c5"]["kernel_us"] = round(c["roofline"]["avg_launch_ms"] * 1e3, 1)
+    head = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "vs_baseline": None,
+            "data": "synthetic (matrix seed 0xDEADBEEF, x ~ U[-1,1) seed 0xC0FFEE); no SuiteSparse files offline"}
+
+    if world == 1:
+        p = measure(args, args.workload, dtype, device, local, with_cpu=not args.no_cpu_baseline,
+                    with_parity=not args.no_parity)
+        out = dict(head, value=p["value"], unit=p["unit"], ms_per_step=p["ms_per_step"], scaling="strong",
+                   dtype=p["dtype"], config=dict(p["config"], parallelism="single GPU"), gflops=p["gflops"],
+                   roofline=p["roofline"], cpu_baseline=p.get("cpu_baseline"), parity=p.get("parity"))
+        if "parity" in p:
+            out["rel_err"] = p["parity"]["rel_err"]
+        if not args.no_secondary:
+            sec = {}
+            for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32)):
+                if wl == args.workload:
+                    continue
+                s = measure(args, wl, dt, device, local, with_cpu=False, with_parity=not args.no_parity)
+                sec[wl] = {"workload": s["config"]["workload"], "value": s["value"], "unit": s["unit"],
+                           "ms_per_step": s["ms_per_step"], "gflops": s["gflops"], "dtype": s["dtype"],
+                           "roofline_frac": s["roofline"]["frac"], "kernel": s["roofline"]["kernel"],
+                           "kernel_us": round(s["roofline"]["avg_launch_ms"] * 1e3, 1),
+                           "bytes_per_launch": s["roofline"]["bytes_per_launch"], "op": s["config"]["op"]}
+                if "parity" in s:
+                    sec[wl]["rel_err"] = s["parity"]["rel_err"]
+                    sec[wl]["parity_pass"] = s["parity"]["pass"]
+            out["secondary"] = sec
+    else:
+        dist.init_process_group("nccl", device_id=device)
+        p = measure_sharded(args, args.workload, dtype, world, rank, local, device)
+        out = dict(head, value=p["value"], unit=p["unit"], ms_per_step=p["ms_per_step"], scaling="strong",
+                   dtype=p["dtype"], config=p["config"], gflops=p["gflops"], roofline=p["roofline"], e2e=p["e2e"],
+                   cpu_baseline=None)
+        if not args.no_secondary and args.workload != "ldoor":
+            c3 = measure_sharded(args, "ldoor", dtype, world, rank, local, device, forward=True)
+            out["secondary"] = {"c3_ldoor": {k: c3[k] for k in ("value", "unit", "ms_per_step", "e2e",
+                                                                "forward_allreduce")}}
+            out["secondary"]["c3_ldoor"]["workload"] = c3["config"]["workload"]
+            out["secondary"]["c3_ldoor"]["roofline_frac_rank0"] = c3["roofline"]["frac"]
+        dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-
-
-WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
-             "ns-mixed": "NS-1DVBC-mixed-w1..8-1e8nnz-uniform",
-             "fe": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2 (SuiteSparse-like mesh operator)",
-             "c5": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS (costs.jl:200-220 generator)"}
-
-
-def build_matrix(workload, dtype, scale, seed):
-    import sparsematrixvbcs_amd as V
-    if workload == "fe":
-        return V.synthetic.fe_grid_2d(int(round(2236 * scale ** 0.5)), dof=2, dtype=dtype, seed=seed)
-    if workload == "c5":
-        return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
-    return V.synthetic.north_star(dtype=dtype, scale=scale, seed=seed, mixed=(workload == "ns-mixed"))
-
-
-def measure(args, workload, dtype, world, rank, local, device, with_cpu):
-    import torch
-    import torch.distributed as dist
-
-    import sparsematrixvbcs_amd as V
-
-    esz = np.dtype(dtype).itemsize
-    # each rank: its own block-row shard (different stripes' values), the same replicated x
-    B = build_matrix(workload, dtype, args.scale, 0xDEADBEEF + rank)
-    rng = np.random.default_rng(0xC0FFEE)
-    k = args.nrhs if workload == "c5" else 1
-    x_host = rng.uniform(-1, 1, (B.m, k) if k > 1 else B.m).astype(dtype)
-    x = torch.from_numpy(x_host).to(device)  # k > 1: row-major X (right-hand sides interleaved)
-    y = torch.empty((B.n, k) if k > 1 else B.n, dtype=x.dtype, device=device)
-    Bt = B.T
-    B.handle(local, True, multi=k > 1)  # build the HBM layout outside the timed region
-    if k > 1:
-        kernel_name = "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
-    elif B.info(local, True)["sweep_bins"] > 0:
-        kernel_name = "vbc::spmv_sweep<T, TB> (row-swept tiles, csrc/vbc_sweep.hip)"
-    elif B.info(local, True)["slot_bins"] > 0:
-        kernel_name = "vbc::spmv_slots<T, 0, U, FASTE> (slotted segments, csrc/vbc_slots.h)"
-    else:
-        kernel_name = "vbc::spmv_ranges<T, 0, K, P> (+ vbc::fixup)"
-    stream = torch.cuda.current_stream(device)
-
-    for _ in range(args.warmup):
-        V.mul_(y, Bt, x)
-    torch.cuda.synchronize(device)
-
-    # HIP events on the launching stream bracket the K back-to-back products of the timed region:
-    # avg_launch_ms = event span / K (an event pair around every product would put two extra markers
-    # between consecutive kernels of the timed region); rocprofv3's per-kernel average of the same
-    # process agrees (profiles/r01_bench_kernel_stats.csv).
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        V.mul_(y, Bt, x)
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
-
-    bytes_rank = algorithmic_bytes(B, esz, nrhs=k)
-    nnz = int(np.count_nonzero(B.val))
-    stats = torch.tensor([elapsed, float(bytes_rank), float(nnz * k), kernel_ms], dtype=torch.float64, device=device)
-    if world > 1:
-        mx = stats.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = stats.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, kernel_ms = mx[0].item(), mx[3].item()
-        total_bytes, total_nnz = sm[1].item(), sm[2].item()
-    else:
-        total_bytes, total_nnz = float(bytes_rank), float(nnz * k)
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = total_bytes * args.steps / elapsed / 1e9
-    achieved = bytes_rank / (kernel_ms * 1e-3) / 1e9
-    wname = WORKLOADS[workload] + (f"-scale{args.scale}" if args.scale != 1.0 else "")
-    dname = "f64" if dtype == np.float64 else "f32"
-    traffic, traffic_src = load_traffic(workload, dname)
-    out = {
-        "metric": "1DVBC SpMV effective GB/s (and GFLOP/s) vs HBM roofline, 1/2/4/8 GPU",
-        "value": round(value, 2),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": dname,
-        "data": "synthetic (seed 0xDEADBEEF+rank; x ~ U[-1,1), seed 0xC0FFEE); no SuiteSparse files offline",
-        "config": {
-            "workload": wname,
-            "op": ("mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if k == 1 else
-                   f"Y = B'X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:89-192 per column), "
-                   "matrix-core panel kernel"),
-            "m": B.m, "n_per_rank": B.n, "stripes_per_rank": len(B.Phi), "row_blocks_per_rank": int(B.pos[-1] - 1),
-            "nnz_per_rank": nnz, "W": B.W, "index_bytes": 4, "nrhs": k,
-            "parallelism": f"stripe-shard x{world} (disjoint y, no collective)",
-        },
-        "gflops": round(2.0 * total_nnz * args.steps / elapsed / 1e9, 2),
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "kernel": kernel_name,
-            "bytes_per_launch": bytes_rank,
-            "avg_launch_ms": round(kernel_ms, 5),
-            "traffic_source": traffic_src,
-        },
-        "cpu_baseline": None,
-    }
-    if with_cpu and rank == 0 and world == 1:
-        out["cpu_baseline"] = cpu_baseline(B, x_host, esz)
-    B.release()
-    del x, y
-    torch.cuda.empty_cache()
-    return out
 
 
 if __name__ == "__main__":

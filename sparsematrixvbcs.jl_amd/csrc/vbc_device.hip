@@ -974,6 +974,9 @@ static void release(vbc_handle *h)
     }
     if (h->d_arena) (void)hipFree(h->d_arena);
     if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
+    for (void *p : h->d_stage)
+        if (p) (void)hipFree(p);
+    if (h->order_ev) (void)hipEventDestroy(h->order_ev);
     delete h;
 }
 
@@ -1108,6 +1111,12 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     for (size_t b = 0; b < pf.size(); b++)
         if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b], wf[b]))) { release(h); return st; }
     if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
+    h->has_scratch = h->has_t && !h->lt.bins.empty();
+    for (const Launch &l : h->lf) h->has_scratch = h->has_scratch || (h->has_f && !l.bins.empty());
+    if (h->has_scratch && hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming) != hipSuccess) {
+        release(h);
+        return fail(VBC_HIP_ERROR, "hipEventCreate failed");
+    }
     *out = h;
     return VBC_OK;
 }
@@ -1146,6 +1155,7 @@ int vbc1d_create(vbc_handle **out, int64_t m, int64_t n, int64_t W, int64_t L, c
     const int64_t q = pos[L] - 1;
     if (q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
     if (ofs[L] - 1 > nval) return fail(VBC_INVALID_ARG, "val shorter than ofs[L+1]-1");
+    if (ofs[L] - 1 > 0 && !val) return fail(VBC_INVALID_ARG, "NULL val");
     for (int64_t l = 0; l < L; l++) {
         const int64_t w = spl[l + 1] - spl[l];
         if (w < 1) return fail(VBC_INVALID_ARG, "Φ.spl must be strictly increasing");
@@ -1189,6 +1199,12 @@ int vbc2d_create(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, i
     if (ofs[L] - 1 > nval) return fail(VBC_INVALID_ARG, "val shorter than ofs[L+1]-1");
     const int64_t q = pos[L] - 1;
     if (q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
+    for (int64_t l = 0; l < L; l++)  // every stripe's blocks lie inside idx[0 .. q-1]
+        if (pos[l + 1] < pos[l] || pos[l] < 1 || pos[l + 1] - 1 > q)
+            return fail(VBC_INVALID_ARG, "pos must be non-decreasing within 1:pos[L+1]");
+    for (int64_t l = 0; l < L; l++)
+        if (ofs[l + 1] < ofs[l]) return fail(VBC_INVALID_ARG, "ofs must be non-decreasing");
+    if (ofs[L] - 1 > 0 && !val) return fail(VBC_INVALID_ARG, "NULL val");
     Stripes s;
     s.m = m; s.n = n; s.L = L;
     s.col0.resize(L); s.w.resize(L); s.rbeg.resize(L + 1); s.voff.resize(L);
@@ -1237,6 +1253,7 @@ int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t *colptr
         s.voff[j] = colptr[j] - 1;
     }
     const int64_t nnz = colptr[n] - 1;
+    if (nnz > 0 && (!rowval || !nzval)) return fail(VBC_INVALID_ARG, "NULL rowval or nzval");
     s.rbeg[n] = nnz;
     s.rows.resize(nnz);
     for (int64_t p = 0; p < nnz; p++) {
@@ -1304,6 +1321,54 @@ static void apply_quirks(int trans, unsigned flags, double &alpha, double &beta)
     if (trans) beta = 0.0;
 }
 
+// Orders the products of a handle whose layout has shared scratch (vbc_handle::has_scratch):
+// a product on a different stream than the previous one waits for that one's completion event.
+// The caller holds h->mu from before begin() until after end().  Inside a stream capture the
+// captured order is the stream's own, so the event chain is skipped.
+struct ProductOrder {
+    vbc_handle *h;
+    hipStream_t s;
+    bool active = false;
+    ProductOrder(vbc_handle *h_, hipStream_t s_) : h(h_), s(s_) {}
+    int begin()
+    {
+        if (!h->has_scratch) return VBC_OK;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess) return fail(VBC_HIP_ERROR, "hipStreamIsCapturing failed");
+        if (cs != hipStreamCaptureStatusNone) return VBC_OK;
+        active = true;
+        if (h->order_valid && h->order_stream != s && hipStreamWaitEvent(s, h->order_ev, 0) != hipSuccess)
+            return fail(VBC_HIP_ERROR, "hipStreamWaitEvent failed");
+        return VBC_OK;
+    }
+    int end()
+    {
+        if (!active) return VBC_OK;
+        if (hipEventRecord(h->order_ev, s) != hipSuccess) return fail(VBC_HIP_ERROR, "hipEventRecord failed");
+        h->order_stream = s;
+        h->order_valid = true;
+        return VBC_OK;
+    }
+};
+
+// Cached device staging buffer `which` (0: x / X, 1: y / Y) of at least `bytes` (caller holds h->mu).
+static int stage_buffer(vbc_handle *h, int which, size_t bytes, void **out)
+{
+    bytes = std::max<size_t>(bytes, 256);
+    if (h->stage_bytes[which] < bytes) {
+        // every host-pointer call synchronises its stream before returning: the old buffer is idle
+        const size_t grow = std::max(bytes, h->stage_bytes[which] + h->stage_bytes[which] / 2);
+        if (h->d_stage[which]) (void)hipFree(h->d_stage[which]);
+        h->d_stage[which] = nullptr;
+        h->stage_bytes[which] = 0;
+        if (hipMalloc(&h->d_stage[which], grow) != hipSuccess)
+            return fail(VBC_HIP_ERROR, "hipMalloc of a staging buffer failed");
+        h->stage_bytes[which] = grow;
+    }
+    *out = h->d_stage[which];
+    return VBC_OK;
+}
+
 int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
             double beta, int mem, void *stream, unsigned flags)
 {
@@ -1311,26 +1376,85 @@ int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_
     apply_quirks(trans, flags, alpha, beta);
     const int64_t esz = h->esz;
     if (ny > 0 && x == y) return fail(VBC_INVALID_ARG, "x and y must not alias");
+    if ((nx > 0 && !x) || (ny > 0 && !y)) return fail(VBC_INVALID_ARG, "NULL x or y");
+    if (mem != VBC_MEM_DEVICE && mem != VBC_MEM_HOST)
+        return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
     DeviceGuard g(h->device);
     if (!g.ok) return fail(VBC_HIP_ERROR, "hipSetDevice failed");
-    if (mem == VBC_MEM_DEVICE) return mul_dispatch(h, trans, x, y, alpha, beta, (hipStream_t)stream);
-    if (mem != VBC_MEM_HOST) return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
-    void *dx = nullptr, *dy = nullptr;
-    int st = VBC_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (hipMalloc(&dx, std::max<int64_t>(nx, 1) * esz) != hipSuccess ||
-        hipMalloc(&dy, std::max<int64_t>(ny, 1) * esz) != hipSuccess) {
-        st = fail(VBC_HIP_ERROR, "hipMalloc of staging buffers failed");
-    } else if (hipMemcpyAsync(dx, x, nx * esz, hipMemcpyHostToDevice, s) != hipSuccess ||
-               (beta != 0.0 && hipMemcpyAsync(dy, y, ny * esz, hipMemcpyHostToDevice, s) != hipSuccess)) {
-        st = fail(VBC_HIP_ERROR, "staging copy failed");
-    } else if ((st = mul_dispatch(h, trans, dx, dy, alpha, beta, s)) == VBC_OK) {
-        if (hipMemcpyAsync(y, dy, ny * esz, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            st = fail(VBC_HIP_ERROR, "result copy failed");
+    if (mem == VBC_MEM_DEVICE) {
+        if (!h->has_scratch) return mul_dispatch(h, trans, x, y, alpha, beta, s);  // lock-free: no shared state
+        std::lock_guard<std::mutex> lk(h->mu);
+        ProductOrder po(h, s);
+        int st = po.begin();
+        if (st == VBC_OK) st = mul_dispatch(h, trans, x, y, alpha, beta, s);
+        if (st == VBC_OK) st = po.end();
+        return st;
     }
-    if (dx) (void)hipFree(dx);
-    if (dy) (void)hipFree(dy);
+    // Host pointers: stage through the handle's cached device buffers (no per-call allocation).
+    std::lock_guard<std::mutex> lk(h->mu);
+    void *dx = nullptr, *dy = nullptr;
+    if (int st = stage_buffer(h, 0, nx * esz, &dx)) return st;
+    if (int st = stage_buffer(h, 1, ny * esz, &dy)) return st;
+    ProductOrder po(h, s);
+    if (int st = po.begin()) return st;
+    if (nx > 0 && hipMemcpyAsync(dx, x, nx * esz, hipMemcpyHostToDevice, s) != hipSuccess)
+        return fail(VBC_HIP_ERROR, "staging copy of x failed");
+    if (beta != 0.0 && ny > 0 && hipMemcpyAsync(dy, y, ny * esz, hipMemcpyHostToDevice, s) != hipSuccess)
+        return fail(VBC_HIP_ERROR, "staging copy of y failed");
+    if (int st = mul_dispatch(h, trans, dx, dy, alpha, beta, s)) return st;
+    if (ny > 0 && hipMemcpyAsync(y, dy, ny * esz, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return fail(VBC_HIP_ERROR, "result copy failed");
+    if (int st = po.end()) return st;
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(VBC_HIP_ERROR, "hipStreamSynchronize failed");
+    return VBC_OK;
+}
+
+// 2D copy of `rows` rows of `width` bytes between pitched buffers (no-op when empty).
+static bool copy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows,
+                   hipMemcpyKind kind, hipStream_t s)
+{
+    if (width == 0 || rows == 0) return true;
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s) == hipSuccess;
+}
+
+static int mul_mat_device(vbc_handle *h, int trans, int64_t nrhs, const char *dX, int64_t ldx, int64_t nx,
+                          char *dY, int64_t ldy, int64_t ny, double alpha, double beta, bool rowmajor,
+                          hipStream_t s)
+{
+    const int64_t esz = h->esz;
+    int st = VBC_OK;
+    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t;
+    for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
+    fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty();  // the fused vector kernel reads the merge layout only
+    if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
+        const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
+        const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;
+        return mulmat_panel_any(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
+    }
+    if (fused) return mulmat_rowmajor(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
+    if (!rowmajor) {
+        for (int64_t r = 0; r < nrhs && st == VBC_OK; r++)
+            st = mul_dispatch(h, trans, dX + r * ldx * esz, dY + r * ldy * esz, alpha, beta, s);
+        return st;
+    }
+    // row-major, per column through contiguous temporaries (strided 2D copies)
+    void *tx = nullptr, *ty = nullptr;
+    if (hipMalloc(&tx, std::max<int64_t>(nx, 1) * esz) != hipSuccess ||
+        hipMalloc(&ty, std::max<int64_t>(ny, 1) * esz) != hipSuccess)
+        st = fail(VBC_HIP_ERROR, "hipMalloc of column temporaries failed");
+    for (int64_t r = 0; r < nrhs && st == VBC_OK; r++) {
+        if (!copy2d(tx, esz, dX + r * esz, ldx * esz, esz, nx, hipMemcpyDeviceToDevice, s))
+            st = fail(VBC_HIP_ERROR, "column gather failed");
+        if (st == VBC_OK && beta != 0.0 && !copy2d(ty, esz, dY + r * esz, ldy * esz, esz, ny, hipMemcpyDeviceToDevice, s))
+            st = fail(VBC_HIP_ERROR, "column gather failed");
+        if (st == VBC_OK) st = mul_dispatch(h, trans, tx, ty, alpha, beta, s);
+        if (st == VBC_OK && !copy2d(dY + r * esz, ldy * esz, ty, esz, esz, ny, hipMemcpyDeviceToDevice, s))
+            st = fail(VBC_HIP_ERROR, "column scatter failed");
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && st == VBC_OK) st = fail(VBC_HIP_ERROR, "sync failed");
+    if (tx) (void)hipFree(tx);
+    if (ty) (void)hipFree(ty);
     return st;
 }
 
@@ -1344,69 +1468,44 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
         (rowmajor && (ldx < std::max<int64_t>(nrhs, 1) || ldy < std::max<int64_t>(nrhs, 1))))
         return fail(VBC_INVALID_ARG, "bad nrhs / leading dimensions");
     if (X == Y && nrhs > 0) return fail(VBC_INVALID_ARG, "X and Y must not alias");
+    if (nrhs > 0 && ((nx > 0 && !X) || (ny > 0 && !Y))) return fail(VBC_INVALID_ARG, "NULL X or Y");
+    if (mem != VBC_MEM_DEVICE && mem != VBC_MEM_HOST)
+        return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
     apply_quirks(trans, flags, alpha, beta);
     const int64_t esz = h->esz;
     DeviceGuard g(h->device);
     if (!g.ok) return fail(VBC_HIP_ERROR, "hipSetDevice failed");
     hipStream_t s = (hipStream_t)stream;
-    const int64_t xbytes = (rowmajor ? nx * ldx : ldx * nrhs) * esz;
-    const int64_t ybytes = (rowmajor ? ny * ldy : ldy * nrhs) * esz;
-    const char *dX = static_cast<const char *>(X);
-    char *dY = static_cast<char *>(Y);
-    void *sx = nullptr, *sy = nullptr, *tx = nullptr, *ty = nullptr;
-    int st = VBC_OK;
-    if (mem == VBC_MEM_HOST) {
-        if (hipMalloc(&sx, std::max<int64_t>(xbytes, 1)) != hipSuccess ||
-            hipMalloc(&sy, std::max<int64_t>(ybytes, 1)) != hipSuccess) {
-            if (sx) (void)hipFree(sx);
-            return fail(VBC_HIP_ERROR, "hipMalloc of staging buffers failed");
-        }
-        (void)hipMemcpyAsync(sx, X, xbytes, hipMemcpyHostToDevice, s);
-        if (beta != 0.0) (void)hipMemcpyAsync(sy, Y, ybytes, hipMemcpyHostToDevice, s);
-        dX = static_cast<const char *>(sx);
-        dY = static_cast<char *>(sy);
-    } else if (mem != VBC_MEM_DEVICE) {
-        return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
+    std::lock_guard<std::mutex> lk(h->mu);  // the fused kernel's carry buffer and the staging buffers
+    ProductOrder po(h, s);
+    if (mem == VBC_MEM_DEVICE) {
+        int st = po.begin();
+        if (st == VBC_OK)
+            st = mul_mat_device(h, trans, nrhs, static_cast<const char *>(X), ldx, nx, static_cast<char *>(Y), ldy,
+                                ny, alpha, beta, rowmajor, s);
+        if (st == VBC_OK) st = po.end();
+        return st;
     }
-    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t;
-    for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
-    fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty();  // the fused vector kernel reads the merge layout only
-    if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
-        const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
-        const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;
-        st = mulmat_panel_any(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
-    } else if (fused) {
-        st = mulmat_rowmajor(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
-    } else if (!rowmajor) {
-        for (int64_t r = 0; r < nrhs && st == VBC_OK; r++)
-            st = mul_dispatch(h, trans, dX + r * ldx * esz, dY + r * ldy * esz, alpha, beta, s);
-    } else {  // row-major, per column through contiguous temporaries (strided 2D copies)
-        if (hipMalloc(&tx, std::max<int64_t>(nx, 1) * esz) != hipSuccess ||
-            hipMalloc(&ty, std::max<int64_t>(ny, 1) * esz) != hipSuccess)
-            st = fail(VBC_HIP_ERROR, "hipMalloc of column temporaries failed");
-        for (int64_t r = 0; r < nrhs && st == VBC_OK; r++) {
-            if (nx && hipMemcpy2DAsync(tx, esz, dX + r * esz, ldx * esz, esz, nx, hipMemcpyDeviceToDevice, s) != hipSuccess)
-                st = fail(VBC_HIP_ERROR, "column gather failed");
-            if (st == VBC_OK && beta != 0.0 && ny &&
-                hipMemcpy2DAsync(ty, esz, dY + r * esz, ldy * esz, esz, ny, hipMemcpyDeviceToDevice, s) != hipSuccess)
-                st = fail(VBC_HIP_ERROR, "column gather failed");
-            if (st == VBC_OK) st = mul_dispatch(h, trans, tx, ty, alpha, beta, s);
-            if (st == VBC_OK && ny &&
-                hipMemcpy2DAsync(dY + r * esz, ldy * esz, ty, esz, esz, ny, hipMemcpyDeviceToDevice, s) != hipSuccess)
-                st = fail(VBC_HIP_ERROR, "column scatter failed");
-        }
-        if (hipStreamSynchronize(s) != hipSuccess && st == VBC_OK) st = fail(VBC_HIP_ERROR, "sync failed");
-        if (tx) (void)hipFree(tx);
-        if (ty) (void)hipFree(ty);
-    }
-    if (mem == VBC_MEM_HOST) {
-        if (st == VBC_OK && (hipMemcpyAsync(Y, sy, ybytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                             hipStreamSynchronize(s) != hipSuccess))
-            st = fail(VBC_HIP_ERROR, "result copy failed");
-        (void)hipFree(sx);
-        (void)hipFree(sy);
-    }
-    return st;
+    // Host operands: only the logical extent moves (pitched 2D copies into packed device buffers),
+    // so the padding of a caller's view (ld > extent) is never read or written.
+    const int64_t xr = rowmajor ? nx : nrhs, xw = rowmajor ? nrhs : nx;  // rows x row-width (elements)
+    const int64_t yr = rowmajor ? ny : nrhs, yw = rowmajor ? nrhs : ny;
+    void *sx = nullptr, *sy = nullptr;
+    if (int st = stage_buffer(h, 0, xr * xw * esz, &sx)) return st;
+    if (int st = stage_buffer(h, 1, yr * yw * esz, &sy)) return st;
+    if (int st = po.begin()) return st;
+    if (!copy2d(sx, xw * esz, X, ldx * esz, xw * esz, xr, hipMemcpyHostToDevice, s))
+        return fail(VBC_HIP_ERROR, "staging copy of X failed");
+    if (beta != 0.0 && !copy2d(sy, yw * esz, Y, ldy * esz, yw * esz, yr, hipMemcpyHostToDevice, s))
+        return fail(VBC_HIP_ERROR, "staging copy of Y failed");
+    if (int st = mul_mat_device(h, trans, nrhs, static_cast<const char *>(sx), std::max<int64_t>(xw, 1), nx,
+                                static_cast<char *>(sy), std::max<int64_t>(yw, 1), ny, alpha, beta, rowmajor, s))
+        return st;
+    if (!copy2d(Y, ldy * esz, sy, yw * esz, yw * esz, yr, hipMemcpyDeviceToHost, s))
+        return fail(VBC_HIP_ERROR, "result copy failed");
+    if (int st = po.end()) return st;
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(VBC_HIP_ERROR, "hipStreamSynchronize failed");
+    return VBC_OK;
 }
 
 }  // extern "C"

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <vector>
 
 #include "vbc_internal.h"
@@ -97,6 +98,20 @@ struct vbc_handle {
     int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
     int sweep_mode = -1;              // VBC_SWEEP: -1 auto (no x locality), 0 never, 1 always (w <= 8)
     int sweep_tile = vbc::kSweepTileBytes;  // VBC_SWEEP_TILE=16: 16 KB of LDS accumulators per wave
+
+    // Mutable per-handle state, guarded by `mu` (the layout itself is immutable after create):
+    //  * host-pointer staging buffers, grown on demand and reused across calls (VBC_MEM_HOST);
+    //  * the product order of handles whose layout has shared scratch (the merge layout's carry
+    //    slots and the fused multi-RHS carries): a product enqueued on a different stream than the
+    //    previous one first waits for that one's completion event, so concurrent products on
+    //    distinct streams stay correct.  Slotted / swept / panel layouts hold no scratch and skip it.
+    std::mutex mu;
+    void *d_stage[2] = {nullptr, nullptr};  // x / X and y / Y staging (device)
+    size_t stage_bytes[2] = {0, 0};
+    bool has_scratch = false;         // set at create: some launch of this handle uses carry slots
+    hipEvent_t order_ev = nullptr;    // recorded after each product with scratch
+    hipStream_t order_stream = nullptr;
+    bool order_valid = false;
 };
 
 

@@ -1,16 +1,27 @@
 """Multi-GPU products: one process per GPU, torch.distributed (RCCL over xGMI for `nccl`).
 
-SURVEY.md §8e.  The stored matrix B (m x n, column stripes) is split into contiguous stripe ranges
-balanced by bytes (a stripe's share = w·|rows|·sizeof(Tv) + 4·|rows| + 12), one per rank:
-  * mul!(y, B', x): each rank owns the y columns of its stripes -> no data-path collective; the
-    optional `gather` assembles the full y with one all_gather;
-  * mul!(y, B, x):  each rank forms the partial α·B_r·x_r over its columns, one all_reduce(sum)
-    combines them and β·y is applied once.
+SURVEY.md §8e.  The reference's only parallel region is the threaded stripe loop of the transposed
+product (multiply_1DVBC.jl:169-177, multiply_VBC.jl:182-189); here the stripes (or the rows) of the
+stored matrix B (m x n) are split into contiguous ranges balanced by HBM bytes, one per rank, and
+every rank builds its own libvbc handle from its slice:
+
+  split="stripes" (block rows of A when B stores Aᵀ, as bin/test_table.jl:27 does):
+    * mul!(y, B', x): each rank owns the y columns of its stripes -> no data-path collective
+      (`local_mul_t`); `mul_t` replicates y with one all_gather;
+    * mul!(y, B, x): each rank forms the partial α·B_r·x_r over its columns and one
+      all_reduce(sum) combines them (the north star's "RCCL all-reduce of y").
+  split="rows" (every stripe's stored rows filtered to the rank's row range at create time):
+    * mul!(y, B, x): each rank owns y rows [r0, r1) -> no data-path collective (`local_mul`);
+      `mul` replicates y with one all_gather;
+    * mul!(y, B', x): partial y from the rank's rows, one all_reduce(sum).
+
+`comm="cpu"` runs the collectives on host copies (gloo process groups on one GPU in tests); the
+per-rank product is always libvbc's GPU kernel unless a `local_mul` is injected (CPU-only tests).
 The reference has no distributed code at all; this is new in the build.
 """
 import numpy as np
 
-from .matrices import SparseMatrix1DVBC
+from .matrices import SparseMatrix1DVBC, _simd_pad
 from .partition import SplitPartition
 
 
@@ -32,59 +43,144 @@ def shard(B, lo, hi):
     col0 = int(spl[0] - 1)
     pos, ofs = B.pos[lo:hi + 1], B.ofs[lo:hi + 1]
     idx = B.idx[pos[0] - 1:pos[-1] - 1]
-    val = B.val[ofs[0] - 1:ofs[-1] - 1]
+    nv = int(ofs[-1] - ofs[0])
+    val = np.zeros(nv + _simd_pad(B.W, B.val.dtype), B.val.dtype)  # keep the SIMD tail pad
+    val[:nv] = B.val[ofs[0] - 1:ofs[-1] - 1]
     S = SparseMatrix1DVBC(B.W, B.m, int(spl[-1] - spl[0]), SplitPartition(spl - col0), pos - (pos[0] - 1), idx,
                           ofs - (ofs[0] - 1), val)
     return S, col0
 
 
+def _row_widths(B):
+    """Width of the stripe of every stored row (length q)."""
+    w = np.diff(B.Phi.spl)
+    return np.repeat(w, np.diff(B.pos))
+
+
+def row_split(B, parts):
+    """Row boundaries r_0 = 0 < ... < r_parts = m (0-based) balancing the stored bytes per part."""
+    esz = B.val.dtype.itemsize
+    per_row = np.bincount(B.idx - 1, weights=_row_widths(B) * esz + 4, minlength=B.m)
+    cost = np.concatenate([[0.0], np.cumsum(per_row)])
+    targets = cost[-1] * np.arange(1, parts) / parts
+    cuts = np.clip(np.searchsorted(cost, targets, side="left"), 0, B.m)
+    return np.concatenate([[0], np.maximum.accumulate(cuts), [B.m]]).astype(np.int64)
+
+
+def row_shard(B, r0, r1):
+    """Rows [r0, r1) of B: every stripe keeps its stored rows inside the range (in stored order, so the
+    per-stripe summation order of mul!(y, B', x) is the reference's); returns an (r1-r0) x n matrix."""
+    w = _row_widths(B)
+    keep = (B.idx > r0) & (B.idx <= r1)
+    L = len(B.Phi)
+    stripe = np.repeat(np.arange(L), np.diff(B.pos))
+    counts = np.bincount(stripe[keep], minlength=L).astype(np.int64)
+    pos = np.concatenate([[1], 1 + np.cumsum(counts)]).astype(np.int64)
+    wl = np.diff(B.Phi.spl)
+    ofs = np.concatenate([[1], 1 + np.cumsum(counts * wl)]).astype(np.int64)
+    # value offsets of the kept rows: ofs[l] + (Q - pos[l]) * w_l
+    q0 = np.arange(len(B.idx), dtype=np.int64) - (B.pos[stripe] - 1)
+    start = (B.ofs[stripe] - 1) + q0 * w
+    ks, kw = start[keep], w[keep]
+    nv = int(ofs[-1] - 1)
+    if nv:
+        elem = np.repeat(ks - np.concatenate([[0], np.cumsum(kw)[:-1]]), kw) + np.arange(nv)
+    else:
+        elem = np.zeros(0, np.int64)
+    val = np.zeros(nv + _simd_pad(B.W, B.val.dtype), B.val.dtype)
+    val[:nv] = B.val[elem]
+    return SparseMatrix1DVBC(B.W, int(r1 - r0), B.n, SplitPartition(B.Phi.spl.copy()), pos, B.idx[keep] - r0, ofs,
+                             val)
+
+
 class ShardedSparseMatrix1DVBC:
-    """Stripe-sharded SparseMatrix1DVBC across the ranks of `group` (torch.distributed).
+    """A SparseMatrix1DVBC split across the ranks of `group` (torch.distributed), one libvbc handle
+    per rank.  See the module docstring for the two splits and which product needs a collective."""
 
-    `local_mul(y, op, x, alpha, beta)` performs this rank's product; it defaults to the libvbc GPU
-    path (sparsematrixvbcs.mul_) and exists so the collective logic can be exercised with gloo on CPU
-    tests (there is no CPU fallback in the product path)."""
-
-    def __init__(self, B, rank, world, group=None, local_mul=None, device=None):
+    def __init__(self, B, rank, world, group=None, local_mul=None, device=None, split="stripes", comm="device"):
+        if split not in ("stripes", "rows"):
+            raise ValueError("split must be 'stripes' or 'rows'")
+        if comm not in ("device", "cpu"):
+            raise ValueError("comm must be 'device' or 'cpu'")
         self.m, self.n, self.W = B.m, B.n, B.W
         self.rank, self.world, self.group = rank, world, group
-        self.cuts = stripe_split(B, world)
-        self.col_splits = [int(B.Phi.spl[c] - 1) for c in self.cuts]
-        self.local, self.col0 = shard(B, int(self.cuts[rank]), int(self.cuts[rank + 1]))
-        self.n_local = self.local.n
+        self.split, self.comm = split, comm
+        if split == "stripes":
+            self.cuts = stripe_split(B, world)
+            self.splits = [int(B.Phi.spl[c] - 1) for c in self.cuts]  # column ranges
+            self.local, self.col0 = shard(B, int(self.cuts[rank]), int(self.cuts[rank + 1]))
+            self.row0, self.n_local, self.m_local = 0, self.local.n, B.m
+        else:
+            self.cuts = row_split(B, world)
+            self.splits = [int(c) for c in self.cuts]  # row ranges
+            self.row0 = int(self.cuts[rank])
+            self.local = row_shard(B, self.row0, int(self.cuts[rank + 1]))
+            self.col0, self.n_local, self.m_local = 0, B.n, self.local.m
+        self.col_splits = self.splits if split == "stripes" else None  # (round-1 name)
         if local_mul is None:
             from .multiply import mul_
             local_mul = mul_
-        self.local_mul = local_mul
+        self._product = local_mul  # mul!(y, op, x, α, β) on this rank's handle
         self.device = device
 
-    # --- mul!(y, B', x): no data-path collective -------------------------------------------------
-    def mul_t(self, y_local, x, alpha=1.0, beta=0.0):
-        """y_local (length n_local: columns col0 .. col0+n_local-1 of y) = α·B_rᵀ x + β·y_local."""
-        return self.local_mul(y_local, self.local.T, x, alpha, beta)
+    # --- collectives ----------------------------------------------------------------------------
+    def _all_reduce(self, t):
+        import torch.distributed as dist
+        if self.comm == "cpu" and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
 
     def gather(self, y_local):
-        """Full y (length n) from every rank's slice: one all_gather of equal-length padded slices."""
+        """Replicated vector from every rank's slice of the split dimension: one all_gather of
+        equal-length padded slices."""
         import torch
         import torch.distributed as dist
-        sizes = [self.col_splits[r + 1] - self.col_splits[r] for r in range(self.world)]
-        mx = max(sizes)
-        buf = torch.zeros(mx, dtype=y_local.dtype, device=y_local.device)
-        buf[:self.n_local] = y_local
+        sizes = [self.splits[r + 1] - self.splits[r] for r in range(self.world)]
+        dev = "cpu" if self.comm == "cpu" else y_local.device
+        buf = torch.zeros(max(sizes), dtype=y_local.dtype, device=dev)
+        buf[:len(y_local)] = y_local.to(dev)
         outs = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(outs, buf, group=self.group)
-        return torch.cat([o[:s] for o, s in zip(outs, sizes)])
+        return torch.cat([o[:s] for o, s in zip(outs, sizes)]).to(y_local.device)
 
-    # --- mul!(y, B, x): one all_reduce -----------------------------------------------------------
+    # --- mul!(y, B', x) ---------------------------------------------------------------------------
+    def local_mul_t(self, y_local, x, alpha=1.0, beta=0.0):
+        """This rank's part of α·B'x + β·y.  stripes: y_local = columns col0 .. col0+n_local-1 of y
+        (final, no collective); rows: a length-n partial from x[row0 : row0+m_local] (β applied)."""
+        if self.split == "stripes":
+            return self._product(y_local, self.local.T, x, alpha, beta)
+        xs = x[self.row0:self.row0 + self.m_local] if len(x) == self.m else x
+        return self._product(y_local, self.local.T, xs, alpha, beta if self.rank == 0 else 0.0)
+
+    def mul_t(self, y, x, alpha=1.0, beta=0.0):
+        """Replicated y (length n) = α·B'x + β·y; x replicated (length m)."""
+        if self.split == "stripes":
+            part = y[self.col0:self.col0 + self.n_local].clone()
+            self.local_mul_t(part, x, alpha, beta)
+            y.copy_(self.gather(part))
+            return y
+        self.local_mul_t(y, x, alpha, beta)
+        return self._all_reduce(y)
+
+    # --- mul!(y, B, x) ----------------------------------------------------------------------------
+    def local_mul(self, y_local, x, alpha=1.0, beta=0.0):
+        """This rank's part of α·Bx + β·y.  rows: y_local = rows row0 .. row0+m_local-1 of y (final,
+        no collective); stripes: a length-m partial from x[col0 : col0+n_local] (β applied on rank 0)."""
+        if self.split == "rows":
+            return self._product(y_local, self.local, x, alpha, beta)
+        xs = x[self.col0:self.col0 + self.n_local] if len(x) == self.n else x
+        return self._product(y_local, self.local, xs, alpha, beta if self.rank == 0 else 0.0)
+
     def mul(self, y, x, alpha=1.0, beta=0.0):
-        """y (length m, replicated) = α·B x + β·y; x is the full (replicated) vector of length n."""
-        import torch
-        import torch.distributed as dist
-        part = torch.empty_like(y)
-        self.local_mul(part, self.local, x[self.col0:self.col0 + self.n_local], alpha, 0.0)
-        dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
-        if beta == 0.0:
-            y.copy_(part)
-        else:
-            y.mul_(beta).add_(part)
-        return y
+        """Replicated y (length m) = α·Bx + β·y; x replicated (length n)."""
+        if self.split == "rows":
+            part = y[self.row0:self.row0 + self.m_local].clone()
+            self.local_mul(part, x, alpha, beta)
+            y.copy_(self.gather(part))
+            return y
+        self.local_mul(y, x, alpha, beta)
+        return self._all_reduce(y)

@@ -86,11 +86,15 @@ def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None
 
 def _layout(M):
     """'R' for row-major (C-contiguous, right-hand sides interleaved), 'C' for column-major."""
-    if isinstance(M, np.ndarray):
-        if M.flags.c_contiguous and M.shape[1] > 1:
-            return "R", M.strides[0] // M.itemsize
-        if M.flags.f_contiguous:
-            return "C", (M.strides[1] // M.itemsize) if M.shape[1] > 1 else max(M.shape[0], 1)
+    if isinstance(M, np.ndarray):  # views with ld > extent are fine: only the extent is touched
+        s0, s1 = M.strides[0] // M.itemsize, M.strides[1] // M.itemsize
+        if M.strides[1] == M.itemsize and M.shape[1] > 1 and s0 >= M.shape[1]:
+            return "R", s0
+        if M.strides[0] == M.itemsize or M.shape[0] <= 1:
+            if M.shape[1] <= 1:
+                return "C", max(M.shape[0], 1)
+            if s1 >= M.shape[0]:
+                return "C", s1
     else:
         if M.stride(1) == 1 and M.shape[1] > 1:
             return "R", M.stride(0)
@@ -114,6 +118,12 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="
     if X.shape[1] != Y.shape[1]:
         raise _L.DimensionMismatch("X and Y have different numbers of columns")
     if X.shape[1] <= 1:
+        # a single column is passed as a contiguous vector: it must have unit stride along dim 0
+        # (a column view of a wider row-major array does not)
+        for M, name in ((X, "X"), (Y, "Y")):
+            st = (M.strides[0] // M.itemsize) if isinstance(M, np.ndarray) else M.stride(0)
+            if M.shape[0] > 1 and st != 1:
+                raise _L.ArgumentError(f"{name}: a single-column operand needs unit stride along its rows")
         lx = ly = "C"
         ldx, ldy = max(X.shape[0], 1), max(Y.shape[0], 1)
     else:

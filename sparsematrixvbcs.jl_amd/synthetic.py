@@ -135,12 +135,9 @@ def c5(dtype=np.float32, scale=1.0, u=8, w=8, seed=0xDEADBEEF):
 STANDINS = {"Boeing/ct20stif": (52329, 2600295), "GHS_psdef/ldoor": (952203, 42493817)}
 
 
-def fe_stiffness_3d(n, nnz, dof=3, dtype=np.float64, seed=0xDEADBEEF):
-    """A symmetric 3D finite-element stiffness stand-in with exactly n rows and nnz within 9 of the
-    target: n/dof mesh nodes on a near-cubic grid (row-major), each node coupled to itself and to a
-    random symmetric subset of its 18 face/edge neighbours, every coupling a dense dof x dof block of
-    U[-1, 1) values (symmetric: block(j, i) = block(i, j)').  Returns a sorted scipy CSC matrix."""
-    import scipy.sparse as sp
+def _stiffness_blocks(n, nnz, dof, seed):
+    """Block structure of fe_stiffness_3d: node pairs (bi, bj) -- the N diagonal blocks, then each kept
+    neighbour pair in both orientations -- and their dof x dof values (symmetric overall)."""
     if n % dof:
         raise ValueError("n must be a multiple of dof")
     rng = np.random.default_rng(seed)
@@ -168,12 +165,42 @@ def fe_stiffness_3d(n, nnz, dof=3, dtype=np.float64, seed=0xDEADBEEF):
     blk = rng.uniform(-1, 1, (N + keep, dof, dof))
     diag = (blk[:N] + np.transpose(blk[:N], (0, 2, 1))) / 2
     vals = np.concatenate([diag, blk[N:], np.transpose(blk[N:], (0, 2, 1))])
+    return N, bi, bj, vals
+
+
+def fe_stiffness_3d(n, nnz, dof=3, dtype=np.float64, seed=0xDEADBEEF):
+    """A symmetric 3D finite-element stiffness stand-in with exactly n rows and nnz within 9 of the
+    target: n/dof mesh nodes on a near-cubic grid (row-major), each node coupled to itself and to a
+    random symmetric subset of its 18 face/edge neighbours, every coupling a dense dof x dof block of
+    U[-1, 1) values (symmetric: block(j, i) = block(i, j)').  Returns a sorted scipy CSC matrix."""
+    import scipy.sparse as sp
+    N, bi, bj, vals = _stiffness_blocks(n, nnz, dof, seed)
     r = (bi[:, None, None] * dof + np.arange(dof)[None, :, None]).repeat(dof, axis=2)
     cidx = (bj[:, None, None] * dof + np.arange(dof)[None, None, :]).repeat(dof, axis=1)
     A = sp.csc_matrix((vals.reshape(-1).astype(dtype), (r.reshape(-1), cidx.reshape(-1))), shape=(n, n))
     A.sum_duplicates()
     A.sort_indices()
     return A
+
+
+def fe_stiffness_3d_1dvbc(n, nnz, dof=3, W=8, dtype=np.float64, seed=0xDEADBEEF):
+    """fe_stiffness_3d(n, nnz, dof) directly as SparseMatrix1DVBC{W} with one stripe per mesh node
+    (= SparseMatrix1DVBC{W}(A, EquiChunker(dof)) on that matrix, without materialising the CSC):
+    stripe j holds, for every coupled node i in ascending order, the dof rows i*dof .. i*dof+dof-1,
+    each the dof-wide row of block(i, j).  Irregular rows per stripe (1 + a random subset of 18
+    neighbours) -- the SuiteSparse-like 3D counterpart of fe_grid_2d at any size."""
+    N, bi, bj, vals = _stiffness_blocks(n, nnz, dof, seed)
+    order = np.lexsort((bi, bj))  # by stripe (node column j), then row node i
+    bi, bj, vals = bi[order], bj[order], vals[order]
+    cnt = np.bincount(bj, minlength=N).astype(np.int64)  # blocks per stripe
+    spl = 1 + np.arange(N + 1, dtype=np.int64) * dof
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt * dof)]).astype(np.int64)
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * dof * dof)]).astype(np.int64)
+    rows = (bi[:, None] * dof + np.arange(dof)[None, :]).reshape(-1) + 1
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + _simd_pad(W, dtype), dtype)
+    val[:nv] = vals.reshape(-1)  # block row-major == dof stored rows of dof values each
+    return SparseMatrix1DVBC(W, n, n, SplitPartition(spl), pos, rows, ofs, val)
 
 
 def standin(name, dtype=np.float64, seed=0xDEADBEEF):

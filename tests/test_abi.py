@@ -71,3 +71,40 @@ def test_product_path_fails_loudly_without_gpu():
         V.mul_(np.zeros(8), B, np.zeros(6))
     with pytest.raises(V.DimensionMismatch):
         V.mul_(np.zeros(7), B, np.zeros(6))
+
+
+def test_vbc2d_create_rejects_malformed_pos():
+    """pos must be non-decreasing and stay inside idx (no out-of-bounds host reads)."""
+    lib = L.lib()
+    h = C.c_void_p()
+    pspl = np.array([1, 3], dtype=np.int64)
+    spl = np.array([1, 2, 3], dtype=np.int64)
+    idx = np.array([1, 1], dtype=np.int64)
+    val = np.zeros(8)
+    for pos, ofs in (([1, 1000, 3], [1, 3, 5]), ([1, 3, 2], [1, 5, 3])):
+        pos = np.array(pos, dtype=np.int64)
+        ofs = np.array(ofs, dtype=np.int64)
+        st = lib.vbc2d_create(C.byref(h), 2, 2, 2, 1, 1, pspl.ctypes.data, 2, spl.ctypes.data, pos.ctypes.data,
+                              idx.ctypes.data, ofs.ctypes.data, val.ctypes.data, len(val), L.VBC_F64, 0, 0)
+        assert st == L.VBC_INVALID_ARG, st
+        assert "pos" in L.last_error()
+
+
+def test_csc_create_rejects_null_arrays():
+    lib = L.lib()
+    h = C.c_void_p()
+    colptr = np.array([1, 2], dtype=np.int64)
+    st = lib.vbc_csc_create(C.byref(h), 1, 1, colptr.ctypes.data, None, None, L.VBC_F64, 0, 0)
+    assert st == L.VBC_INVALID_ARG and "NULL" in L.last_error()
+
+
+def test_single_column_operand_needs_unit_row_stride():
+    """a column view of a row-major array is not a contiguous vector; mulmat_ must refuse it
+    (before any handle or device call) instead of reading / writing the wrong elements."""
+    import scipy.sparse as sp
+    A = sp.random(8, 6, 0.5, random_state=0, format="csc")
+    B = V.SparseMatrix1DVBC[2](A, V.EquiChunker(2))
+    X = np.zeros((8, 4))
+    Y = np.zeros((6, 4))
+    with pytest.raises(V.ArgumentError):
+        V.mul_(Y[:, 1:2], B.T, X[:, 1:2])

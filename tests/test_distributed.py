@@ -30,25 +30,33 @@ def make_matrix():
     return V.synthetic.vbr_1dvbc(500, 60, 700, w, W=8, seed=7)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         B = make_matrix()
-        S = V.distributed.ShardedSparseMatrix1DVBC(B, rank, world, local_mul=oracle_mul)
+        S = V.distributed.ShardedSparseMatrix1DVBC(B, rank, world, local_mul=oracle_mul, split=split)
         rng = np.random.default_rng(3)
         xt = torch.from_numpy(rng.uniform(-1, 1, B.m))
         xf = torch.from_numpy(rng.uniform(-1, 1, B.n))
         y0 = torch.from_numpy(rng.uniform(-1, 1, B.m))
-        yl = torch.zeros(S.n_local, dtype=torch.float64)
-        S.mul_t(yl, xt)
-        yt = S.gather(yl)
+        y0t = torch.from_numpy(rng.uniform(-1, 1, B.n))
+        yt = y0t.clone()
+        S.mul_t(yt, xt, 1.5, 0.25)
         yf = y0.clone()
         S.mul(yf, xf, 2.0, 0.5)
-        q.put((rank, yt.numpy(), yf.numpy(), S.cuts.tolist(), S.n_local))
+        # the collective-free halves
+        if split == "stripes":
+            yl = torch.zeros(S.n_local, dtype=torch.float64)
+            S.local_mul_t(yl, xt)
+        else:
+            yl = torch.zeros(S.m_local, dtype=torch.float64)
+            S.local_mul(yl, xf)
+        q.put((rank, yt.numpy(), yf.numpy(), yl.numpy(), S.cuts.tolist(), S.n_local, S.m_local, S.col0, S.row0))
         dist.destroy_process_group()
     except Exception as e:  # surface worker failures in the parent
-        q.put((rank, repr(e)))
+        import traceback
+        q.put((rank, traceback.format_exc()))
 
 
 def free_port():
@@ -59,29 +67,55 @@ def free_port():
     return p
 
 
-def test_sharded_products_world2():
+@pytest.mark.parametrize("split", ["stripes", "rows"])
+def test_sharded_products_world2(split):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     for r in res:
-        assert len(r) == 5, r
+        assert len(r) == 9, r
     B = make_matrix()
     R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
     rng = np.random.default_rng(3)
     xt, xf, y0 = rng.uniform(-1, 1, B.m), rng.uniform(-1, 1, B.n), rng.uniform(-1, 1, B.m)
-    ref_t = O.mul(R, xt, np.zeros(B.n), trans=True)
+    y0t = rng.uniform(-1, 1, B.n)
+    ref_t = O.mul(R, xt, y0t.copy(), 1.5, 0.25, trans=True, ref_semantics=False)
+    ref_t1 = O.mul(R, xt, np.zeros(B.n), trans=True)
     ref_f = O.mul(R, xf, y0.copy(), 2.0, 0.5, ref_semantics=False)
-    for rank, yt, yf, cuts, nloc in res:
-        assert np.array_equal(yt, ref_t)            # disjoint slices: same per-stripe arithmetic
+    ref_f1 = O.mul(R, xf, np.zeros(B.m), ref_semantics=False)
+    for rank, yt, yf, yl, cuts, nloc, mloc, col0, row0 in res:
+        assert np.allclose(yt, ref_t, rtol=1e-13, atol=1e-13)
         assert np.allclose(yf, ref_f, rtol=1e-13, atol=1e-13)
-    assert sum(r[4] for r in res) == B.n
+        if split == "stripes":   # disjoint y columns: the same per-stripe arithmetic, bit for bit
+            assert np.array_equal(yt, ref_t)
+            assert np.array_equal(yl, ref_t1[col0:col0 + nloc])
+        else:                    # disjoint y rows of the forward product
+            assert np.allclose(yl, ref_f1[row0:row0 + mloc], rtol=1e-13, atol=1e-13)
+    if split == "stripes":
+        assert sum(r[5] for r in res) == B.n
+    else:
+        assert sum(r[6] for r in res) == B.m
+
+
+def test_row_split_reassembly():
+    """Row shards partition the stored rows: the shards' dense forms stack to B's."""
+    B = make_matrix()
+    D = O.vbc_to_dense(O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val))
+    for parts in (1, 2, 3, 7):
+        cuts = V.distributed.row_split(B, parts)
+        assert cuts[0] == 0 and cuts[-1] == B.m and np.all(np.diff(cuts) >= 0)
+        blocks = []
+        for p in range(parts):
+            S = V.distributed.row_shard(B, int(cuts[p]), int(cuts[p + 1]))
+            blocks.append(O.vbc_to_dense(O.Ref1DVBC(S.m, S.n, S.W, S.Phi.spl, S.pos, S.idx, S.ofs, S.val)))
+        assert np.array_equal(np.vstack(blocks), D)
 
 
 def test_stripe_split_balance_and_reassembly():
@@ -95,7 +129,7 @@ def test_stripe_split_balance_and_reassembly():
         for p in range(parts):
             S, col0 = V.distributed.shard(B, int(cuts[p]), int(cuts[p + 1]))
             share.append(len(S.val) * esz + len(S.idx) * 4)
-            vals.append(S.val)
+            vals.append(S.val[:S.ofs[-1] - 1])
             idxs.append(S.idx)
             assert col0 == B.Phi.spl[cuts[p]] - 1
         assert np.array_equal(np.concatenate(vals), B.val[:B.ofs[-1] - 1])
