@@ -38,8 +38,16 @@ typedef enum vbc_status {
     VBC_ASSERTION = 6          /* -> AssertionError (w <= W, u <= U) */
 } vbc_status;
 
-/* Element types (Tv; x and y must have the same eltype as Tv on the GPU path). */
-typedef enum vbc_dtype { VBC_F64 = 0, VBC_F32 = 1 } vbc_dtype;
+/* Element types.  vbc*_create / vbc_mul / vbc_mul_mat: Tv = x = y = F64 or F32.  The *_ex entry
+ * points below add the reference's other eltypes (Bool and Int32 matrices: runtests.jl:15-16; the
+ * product computes in eltype(y): multiply_1DVBC.jl:27,34,102) and Int32 index arrays (Ti). */
+typedef enum vbc_dtype {
+    VBC_F64 = 0,
+    VBC_F32 = 1,
+    VBC_I64 = 2,  /* Int64: exact two's-complement wrapping arithmetic (Julia Int64 semantics)     */
+    VBC_I32 = 3,  /* Int32: computed as Int64, stored back truncated (Julia Int32 wraparound)      */
+    VBC_BOOL = 4  /* Bool as one byte, 0 / 1 (values and x only)                                     */
+} vbc_dtype;
 
 /* Where x / y live for vbc_mul / vbc_mul_mat. */
 typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
@@ -92,6 +100,31 @@ VBC_API int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t
 
 VBC_API int vbc_destroy(vbc_handle *h);
 
+/* Type parameters of the *_ex create calls: the reference's SparseMatrix1DVBC{W,Tv,Ti} with any
+ * Tv in {Float64, Float32, Int64, Int32, Bool} and Ti in {Int64, Int32}, and the eltype the products
+ * compute in.  The reference computes in eltype(y) (multiply_1DVBC.jl:27,34,102 convert val and x to
+ * it), so a binding creates one handle per eltype(y) it meets:
+ *   compute_dtype = VBC_F64 / VBC_F32: values converted once at create (Bool / integer -> float is
+ *                   exact below 2^53 / 2^24); the float kernels (slotted / swept / merge / panel);
+ *   compute_dtype = VBC_I64: Int64 values, exact wrapping arithmetic (vbc_generic.hip), for
+ *                   integer y (Int64, or Int32 stored back truncated -- Julia's wraparound). */
+typedef struct vbc_types {
+    int32_t val_dtype;     /* eltype of val / nzval as passed (vbc_dtype) */
+    int32_t index_bits;    /* 64 or 32: width of spl / pos / idx / ofs (colptr / rowval, Π.spl) */
+    int32_t compute_dtype; /* VBC_F64, VBC_F32 or VBC_I64 */
+    int32_t reserved;      /* 0 */
+} vbc_types;
+
+VBC_API int vbc1d_create_ex(vbc_handle **out, int64_t m, int64_t n, int64_t W, int64_t L, const void *spl,
+                            const void *pos, const void *idx, const void *ofs, const void *val, int64_t nval,
+                            const vbc_types *types, int device, unsigned flags);
+VBC_API int vbc2d_create_ex(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K,
+                            const void *pspl, int64_t L, const void *spl, const void *pos, const void *idx,
+                            const void *ofs, const void *val, int64_t nval, const vbc_types *types, int device,
+                            unsigned flags);
+VBC_API int vbc_csc_create_ex(vbc_handle **out, int64_t m, int64_t n, const void *colptr, const void *rowval,
+                              const void *nzval, const vbc_types *types, int device, unsigned flags);
+
 /* ---------------------------------------------------------------------------------------------
  * Products
  * ------------------------------------------------------------------------------------------- */
@@ -106,6 +139,18 @@ VBC_API int vbc_destroy(vbc_handle *h);
  * x and y must not alias (the reference has the same precondition). */
 VBC_API int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
             double beta, int mem, void *stream, unsigned flags);
+
+/* mul!(y::StridedVector, op(B), x::StridedVector, α, β) with any strides and eltypes the
+ * reference accepts (multiply_1DVBC.jl:9,85 take StridedVector; :102 converts x to eltype(y)).
+ * x_dtype: any vbc_dtype, converted to the handle's compute eltype (a float x is refused on an
+ * integer handle: Julia's convert would throw InexactError); y_dtype: the compute eltype, or VBC_I32
+ * on an integer handle.  incx / incy: element strides (any nonzero value; negative = reversed view,
+ * the pointer is that of x[1] / y[1]).  Contiguous operands of the compute eltype go straight to the
+ * kernels; others through the handle's staging buffers (a conversion kernel on each side).
+ * mem, stream, flags as vbc_mul. */
+VBC_API int vbc_mul_ex(vbc_handle *h, int trans, const void *x, int x_dtype, int64_t incx, int64_t nx, void *y,
+                       int y_dtype, int64_t incy, int64_t ny, double alpha, double beta, int mem, void *stream,
+                       unsigned flags);
 
 /* Multi-RHS Y = α·op(B)·X + β·Y.  X is nx × nrhs, Y is ny × nrhs; column-major (ldx >= nx, ldy >=
  * ny) by default, row-major with VBC_MAT_ROWMAJOR (ldx, ldy >= nrhs).  The reference has no matrix

@@ -61,7 +61,7 @@ VBC_API int vbcx_partition_dynamic_table(int64_t m, int64_t n, const int64_t *co
 VBC_API int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
                      const int64_t *spl, int64_t *pos, int64_t *ofs);
 /* pass 2 fills idx[pos[L]-1] and val[ofs[L]-1 + pad] (pad trailing zeros, :35-39).
- * dtype: VBC_F64 / VBC_F32 (nzval and val have that eltype). */
+ * dtype: any vbc_dtype (nzval and val have that eltype; values are copied, never converted). */
 VBC_API int vbcx_1dvbc_fill(int64_t m, int64_t n, int64_t W, const int64_t *colptr, const int64_t *rowval,
                     const void *nzval, int dtype, int64_t L, const int64_t *spl, const int64_t *pos,
                     const int64_t *ofs, int64_t *idx, void *val, int64_t pad);

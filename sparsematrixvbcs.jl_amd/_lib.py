@@ -14,7 +14,7 @@ LIB_PATH = Path(os.environ.get("VBC_LIBRARY", PKG_DIR / "libvbc.so"))
 
 VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR, VBC_UNSUPPORTED_DTYPE, \
     VBC_ASSERTION = range(7)
-VBC_F64, VBC_F32 = 0, 1
+VBC_F64, VBC_F32, VBC_I64, VBC_I32, VBC_BOOL = range(5)
 VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
 VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD, VBC_CREATE_MULTI = 0x1, 0x2, 0x4
 VBC_MUL_REFERENCE_QUIRKS = 0x1
@@ -23,6 +23,7 @@ VBC_MAT_ROWMAJOR = 0x2
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
     "vbc1d_create", "vbc2d_create", "vbc_csc_create", "vbc_destroy", "vbc_mul", "vbc_mul_mat",
+    "vbc1d_create_ex", "vbc2d_create_ex", "vbc_csc_create_ex", "vbc_mul_ex",
     "vbc_get_info", "vbc_last_error", "vbc_version",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
     "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
@@ -44,6 +45,12 @@ class HIPError(RuntimeError):
 
 class UnsupportedDtype(TypeError):
     pass
+
+
+class vbc_types(C.Structure):
+    """include/vbc.h vbc_types: the reference's Tv / Ti type parameters and the compute eltype."""
+    _fields_ = [("val_dtype", C.c_int32), ("index_bits", C.c_int32), ("compute_dtype", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class vbc_info(C.Structure):
@@ -81,6 +88,11 @@ def lib():
         L.vbc2d_create.argtypes = [C.POINTER(P), I64, I64, I64, I64, I64, P, I64, P, P, P, P, P, I64,
                                    INT, INT, U]
         L.vbc_csc_create.argtypes = [C.POINTER(P), I64, I64, P, P, P, INT, INT, U]
+        T = C.POINTER(vbc_types)
+        L.vbc1d_create_ex.argtypes = [C.POINTER(P), I64, I64, I64, I64, P, P, P, P, P, I64, T, INT, U]
+        L.vbc2d_create_ex.argtypes = [C.POINTER(P), I64, I64, I64, I64, I64, P, I64, P, P, P, P, P, I64, T, INT, U]
+        L.vbc_csc_create_ex.argtypes = [C.POINTER(P), I64, I64, P, P, P, T, INT, U]
+        L.vbc_mul_ex.argtypes = [P, INT, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]
         L.vbc_destroy.argtypes = [P]
         L.vbc_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
         L.vbc_mul_mat.argtypes = [P, INT, I64, P, I64, I64, P, I64, I64, D, D, INT, P, U]
@@ -130,10 +142,24 @@ def ptr(a):
     return a.data_ptr()
 
 
+_CODES = {np.dtype(np.float64): VBC_F64, np.dtype(np.float32): VBC_F32, np.dtype(np.int64): VBC_I64,
+          np.dtype(np.int32): VBC_I32, np.dtype(np.bool_): VBC_BOOL}
+
+
 def dtype_code(dtype):
-    dtype = np.dtype(dtype)
-    if dtype == np.float64:
-        return VBC_F64
-    if dtype == np.float32:
-        return VBC_F32
-    raise UnsupportedDtype(f"the GPU path supports Float64 / Float32 eltypes, got {dtype}")
+    """vbc_dtype of a numpy dtype, a torch dtype or its name."""
+    name = str(dtype).replace("torch.", "")
+    try:
+        dtype = np.dtype("bool" if name == "bool" else name)
+    except TypeError:
+        raise UnsupportedDtype(f"no GPU eltype for {dtype}")
+    if dtype not in _CODES:
+        raise UnsupportedDtype(f"the GPU path supports Float64/Float32/Int64/Int32/Bool eltypes, got {dtype}")
+    return _CODES[dtype]
+
+
+def compute_code(val_dtype):
+    """The compute eltype a matrix of this value eltype runs in by default: floats in themselves,
+    integers and Bool in exact Int64 (vbc.h vbc_types)."""
+    c = dtype_code(val_dtype)
+    return c if c in (VBC_F64, VBC_F32) else VBC_I64

@@ -989,13 +989,50 @@ static int64_t count_nonzeros(const char *val, int64_t n)
     return c;
 }
 
+// Integer eltypes: the reference layout itself (0-based) in one arena, read by vbc_generic.hip.
+static int create_int(vbc_handle *h, const Stripes &s, const int64_t *val, int64_t nval)
+{
+    Arena ar;
+    const int64_t L = s.L, q = (int64_t)s.rows.size();
+    const size_t o_col0 = ar.reserve(L * 4), o_w = ar.reserve(L * 4), o_rows = ar.reserve(q * 4);
+    const size_t o_c2s = ar.reserve(s.n * 4), o_r2s = ar.reserve(q * 4);
+    const size_t o_rbeg = ar.reserve((L + 1) * 8), o_voff = ar.reserve(L * 8), o_val = ar.reserve(nval * 8);
+    for (int64_t l = 0; l < L; l++) {
+        ar.at<int32_t>(o_col0)[l] = (int32_t)s.col0[l];
+        ar.at<int32_t>(o_w)[l] = s.w[l];
+        ar.at<int64_t>(o_voff)[l] = s.voff[l];
+        for (int64_t c = 0; c < s.w[l]; c++) ar.at<int32_t>(o_c2s)[s.col0[l] + c] = (int32_t)l;
+        for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) ar.at<int32_t>(o_r2s)[r] = (int32_t)l;
+    }
+    std::memcpy(ar.at<int64_t>(o_rbeg), s.rbeg.data(), (L + 1) * 8);
+    if (q) std::memcpy(ar.at<int32_t>(o_rows), s.rows.data(), q * 4);
+    if (nval) std::memcpy(ar.at<int64_t>(o_val), val, nval * 8);
+    h->arena_bytes = ar.host.size();
+    VBC_HIP(hipMalloc(&h->d_arena, h->arena_bytes));
+    VBC_HIP(hipMemcpy(h->d_arena, ar.host.data(), h->arena_bytes, hipMemcpyHostToDevice));
+    char *b = static_cast<char *>(h->d_arena);
+    IntLayout &li = h->li;
+    li.L = L;
+    li.nrows = q;
+    li.col0 = reinterpret_cast<const int32_t *>(b + o_col0);
+    li.w = reinterpret_cast<const int32_t *>(b + o_w);
+    li.rows = reinterpret_cast<const int32_t *>(b + o_rows);
+    li.col2stripe = reinterpret_cast<const int32_t *>(b + o_c2s);
+    li.row2stripe = reinterpret_cast<const int32_t *>(b + o_r2s);
+    li.rbeg = reinterpret_cast<const int64_t *>(b + o_rbeg);
+    li.voff = reinterpret_cast<const int64_t *>(b + o_voff);
+    li.val = reinterpret_cast<const int64_t *>(b + o_val);
+    h->bytes_t = h->bytes_f = nval * 8 + q * 4 + (s.m + s.n) * 8;
+    return VBC_OK;
+}
+
 static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtype, int device,
                          unsigned flags, int64_t nval, int64_t K, int64_t nblocks)
 {
     if (!out) return fail(VBC_INVALID_ARG, "out handle pointer is NULL");
     *out = nullptr;
-    if (dtype != VBC_F64 && dtype != VBC_F32)
-        return fail(VBC_UNSUPPORTED_DTYPE, "GPU path supports Float64 and Float32 eltypes");
+    if (dtype != VBC_F64 && dtype != VBC_F32 && dtype != VBC_I64)
+        return fail(VBC_UNSUPPORTED_DTYPE, "GPU products compute in Float64, Float32 or Int64 (see vbc_types)");
     if (int st = check_limits(s)) return st;
     int ndev = 0;
     VBC_HIP(hipGetDeviceCount(&ndev));
@@ -1014,10 +1051,22 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     h->esz = elem_size(dtype);
     h->device = device;
     const char *v = static_cast<const char *>(val);
-    h->nnz = dtype == VBC_F64 ? count_nonzeros<double>(v, nval) : count_nonzeros<float>(v, nval);
+    h->nnz = dtype == VBC_F64 ? count_nonzeros<double>(v, nval)
+           : dtype == VBC_F32 ? count_nonzeros<float>(v, nval) : count_nonzeros<int64_t>(v, nval);
 
     DeviceGuard g(device);
     if (!g.ok) { release(h); return fail(VBC_HIP_ERROR, "hipSetDevice failed"); }
+    if (hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming) != hipSuccess) {
+        release(h);
+        return fail(VBC_HIP_ERROR, "hipEventCreate failed");
+    }
+    if (dtype == VBC_I64) {  // exact integer products (vbc_generic.hip): one layout, both directions
+        if (int st = create_int(h, s, static_cast<const int64_t *>(val), nval)) { release(h); return st; }
+        h->has_t = (flags & (VBC_CREATE_TRANSPOSED | VBC_CREATE_MULTI)) != 0;
+        h->has_f = (flags & VBC_CREATE_FORWARD) != 0;
+        *out = h;
+        return VBC_OK;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipGetDeviceProperties failed"); }
     h->tile_k = dtype == VBC_F64 ? 4 : 8;  // measured best (tools/ab.py, FE workload)
@@ -1113,10 +1162,6 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
     h->has_scratch = h->has_t && !h->lt.bins.empty();
     for (const Launch &l : h->lf) h->has_scratch = h->has_scratch || (h->has_f && !l.bins.empty());
-    if (h->has_scratch && hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming) != hipSuccess) {
-        release(h);
-        return fail(VBC_HIP_ERROR, "hipEventCreate failed");
-    }
     *out = h;
     return VBC_OK;
 }
@@ -1329,10 +1374,11 @@ struct ProductOrder {
     vbc_handle *h;
     hipStream_t s;
     bool active = false;
-    ProductOrder(vbc_handle *h_, hipStream_t s_) : h(h_), s(s_) {}
+    bool force = false;  // the product uses the handle's staging buffers on the device path
+    ProductOrder(vbc_handle *h_, hipStream_t s_, bool force_ = false) : h(h_), s(s_), force(force_) {}
     int begin()
     {
-        if (!h->has_scratch) return VBC_OK;
+        if (!h->has_scratch && !force) return VBC_OK;
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(s, &cs) != hipSuccess) return fail(VBC_HIP_ERROR, "hipStreamIsCapturing failed");
         if (cs != hipStreamCaptureStatusNone) return VBC_OK;
@@ -1424,7 +1470,7 @@ static int mul_mat_device(vbc_handle *h, int trans, int64_t nrhs, const char *dX
 {
     const int64_t esz = h->esz;
     int st = VBC_OK;
-    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t;
+    bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t && h->dtype != VBC_I64;
     for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
     fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty();  // the fused vector kernel reads the merge layout only
     if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
@@ -1506,6 +1552,202 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
     if (int st = po.end()) return st;
     if (hipStreamSynchronize(s) != hipSuccess) return fail(VBC_HIP_ERROR, "hipStreamSynchronize failed");
     return VBC_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic eltypes and index widths (vbc_types), strided operands
+// ---------------------------------------------------------------------------------------------
+
+extern "C++" {  // helpers of the typed entry points (templates need C++ linkage)
+static bool is_float(int dt) { return dt == VBC_F64 || dt == VBC_F32; }
+static bool known_dtype(int dt) { return dt >= VBC_F64 && dt <= VBC_BOOL; }
+
+template <typename To>
+static void host_convert(const void *src, int dt, int64_t n, int64_t inc, To *dst)
+{
+    const char *p = static_cast<const char *>(src);
+    for (int64_t i = 0; i < n; i++) {
+        const char *e = p + i * inc * elem_size(dt);
+        switch (dt) {
+        case VBC_F64: dst[i] = (To) * reinterpret_cast<const double *>(e); break;
+        case VBC_F32: dst[i] = (To) * reinterpret_cast<const float *>(e); break;
+        case VBC_I64: dst[i] = (To) * reinterpret_cast<const int64_t *>(e); break;
+        case VBC_I32: dst[i] = (To) * reinterpret_cast<const int32_t *>(e); break;
+        default: dst[i] = (To) * reinterpret_cast<const uint8_t *>(e); break;
+        }
+    }
+}
+
+// Values converted to the compute eltype (empty when no conversion is needed: use `val` as is).
+static int convert_values(const void *val, int64_t nval, const vbc_types *t, std::vector<char> &out)
+{
+    if (t->val_dtype == t->compute_dtype) return VBC_OK;
+    if (nval > 0 && !val) return fail(VBC_INVALID_ARG, "NULL val");
+    out.resize((size_t)std::max<int64_t>(nval, 1) * elem_size(t->compute_dtype));
+    if (t->compute_dtype == VBC_F64) host_convert(val, t->val_dtype, nval, 1, reinterpret_cast<double *>(out.data()));
+    else if (t->compute_dtype == VBC_F32) host_convert(val, t->val_dtype, nval, 1, reinterpret_cast<float *>(out.data()));
+    else host_convert(val, t->val_dtype, nval, 1, reinterpret_cast<int64_t *>(out.data()));
+    return VBC_OK;
+}
+
+static int check_types(const vbc_types *t)
+{
+    if (!t) return fail(VBC_INVALID_ARG, "NULL vbc_types");
+    if (t->reserved != 0) return fail(VBC_INVALID_ARG, "vbc_types.reserved must be 0");
+    if (t->index_bits != 32 && t->index_bits != 64) return fail(VBC_INVALID_ARG, "index_bits must be 32 or 64");
+    if (!known_dtype(t->val_dtype)) return fail(VBC_UNSUPPORTED_DTYPE, "unknown val_dtype");
+    if (t->compute_dtype != VBC_F64 && t->compute_dtype != VBC_F32 && t->compute_dtype != VBC_I64)
+        return fail(VBC_UNSUPPORTED_DTYPE, "compute_dtype must be VBC_F64, VBC_F32 or VBC_I64");
+    if (t->compute_dtype == VBC_I64 && is_float(t->val_dtype))
+        return fail(VBC_UNSUPPORTED_DTYPE, "floating-point values on an integer handle (InexactError)");
+    return VBC_OK;
+}
+
+// Index array as Int64 (a copy only for Ti = Int32).
+struct Idx64 {
+    std::vector<int64_t> buf;
+    const int64_t *p = nullptr;
+    void set(const void *src, int bits, int64_t n)
+    {
+        if (!src || bits == 64) {
+            p = static_cast<const int64_t *>(src);
+            return;
+        }
+        const int32_t *s32 = static_cast<const int32_t *>(src);
+        buf.assign(s32, s32 + std::max<int64_t>(n, 0));
+        p = buf.data();
+    }
+};
+
+}  // extern "C++"
+
+int vbc1d_create_ex(vbc_handle **out, int64_t m, int64_t n, int64_t W, int64_t L, const void *spl, const void *pos,
+                    const void *idx, const void *ofs, const void *val, int64_t nval, const vbc_types *t, int device,
+                    unsigned flags)
+{
+    if (int st = check_types(t)) return st;
+    if (L < 0 || !spl || !pos || !ofs) return fail(VBC_INVALID_ARG, "bad stripe arrays");
+    Idx64 S, P, I, O;
+    S.set(spl, t->index_bits, L + 1);
+    P.set(pos, t->index_bits, L + 1);
+    O.set(ofs, t->index_bits, L + 1);
+    const int64_t q = P.p[L] - 1;
+    if (q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
+    I.set(idx, t->index_bits, q);
+    std::vector<char> cv;
+    if (int st = convert_values(val, nval, t, cv)) return st;
+    return vbc1d_create(out, m, n, W, L, S.p, P.p, I.p, O.p, cv.empty() ? val : cv.data(), nval, t->compute_dtype,
+                        device, flags);
+}
+
+int vbc2d_create_ex(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K, const void *pspl,
+                    int64_t L, const void *spl, const void *pos, const void *idx, const void *ofs, const void *val,
+                    int64_t nval, const vbc_types *t, int device, unsigned flags)
+{
+    if (int st = check_types(t)) return st;
+    if (K < 0 || L < 0 || !pspl || !spl || !pos || !ofs) return fail(VBC_INVALID_ARG, "bad partition arrays");
+    Idx64 PS, S, P, I, O;
+    PS.set(pspl, t->index_bits, K + 1);
+    S.set(spl, t->index_bits, L + 1);
+    P.set(pos, t->index_bits, L + 1);
+    O.set(ofs, t->index_bits, L + 1);
+    const int64_t q = P.p[L] - 1;
+    if (q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
+    I.set(idx, t->index_bits, q);
+    std::vector<char> cv;
+    if (int st = convert_values(val, nval, t, cv)) return st;
+    return vbc2d_create(out, m, n, U, W, K, PS.p, L, S.p, P.p, I.p, O.p, cv.empty() ? val : cv.data(), nval,
+                        t->compute_dtype, device, flags);
+}
+
+int vbc_csc_create_ex(vbc_handle **out, int64_t m, int64_t n, const void *colptr, const void *rowval,
+                      const void *nzval, const vbc_types *t, int device, unsigned flags)
+{
+    if (int st = check_types(t)) return st;
+    if (n < 0 || !colptr) return fail(VBC_INVALID_ARG, "colptr[1] must be 1");
+    Idx64 CP, RV;
+    CP.set(colptr, t->index_bits, n + 1);
+    const int64_t nnz = CP.p[n] - 1;
+    if (nnz < 0) return fail(VBC_INVALID_ARG, "bad colptr");
+    RV.set(rowval, t->index_bits, nnz);
+    std::vector<char> cv;
+    if (int st = convert_values(nzval, nnz, t, cv)) return st;
+    return vbc_csc_create(out, m, n, CP.p, RV.p, cv.empty() ? nzval : cv.data(), t->compute_dtype, device, flags);
+}
+
+int vbc_mul_ex(vbc_handle *h, int trans, const void *x, int x_dtype, int64_t incx, int64_t nx, void *y, int y_dtype,
+               int64_t incy, int64_t ny, double alpha, double beta, int mem, void *stream, unsigned flags)
+{
+    if (int st = check_mul(h, trans, nx, ny)) return st;
+    const int cdt = h->dtype;
+    if (!known_dtype(x_dtype) || !known_dtype(y_dtype)) return fail(VBC_UNSUPPORTED_DTYPE, "unknown eltype");
+    if (cdt == VBC_I64 && is_float(x_dtype))
+        return fail(VBC_UNSUPPORTED_DTYPE, "floating-point x on an integer handle (InexactError)");
+    if (is_float(cdt) ? y_dtype != cdt : (y_dtype != VBC_I64 && y_dtype != VBC_I32))
+        return fail(VBC_UNSUPPORTED_DTYPE, "eltype(y) must be the handle's compute eltype (or Int32 on an Int64 handle)");
+    if ((nx > 0 && incx == 0) || (ny > 0 && incy == 0)) return fail(VBC_INVALID_ARG, "zero stride");
+    if ((nx > 0 && !x) || (ny > 0 && !y)) return fail(VBC_INVALID_ARG, "NULL x or y");
+    if (cdt == VBC_I64 && (alpha != std::trunc(alpha) || beta != std::trunc(beta)))
+        return fail(VBC_INVALID_ARG, "alpha and beta must be integers on an integer handle (InexactError)");
+    if (mem != VBC_MEM_DEVICE && mem != VBC_MEM_HOST)
+        return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
+    const bool direct_x = x_dtype == cdt && (incx == 1 || nx <= 1);
+    const bool direct_y = y_dtype == cdt && (incy == 1 || ny <= 1);
+    if (direct_x && direct_y) return vbc_mul(h, trans, x, nx, y, ny, alpha, beta, mem, stream, flags);
+    const int64_t esz = h->esz;
+    if (mem == VBC_MEM_HOST) {  // convert on the host, then the contiguous host path
+        std::vector<char> xs, ys((size_t)std::max<int64_t>(ny, 1) * esz);
+        const void *xp = x;
+        if (!direct_x) {
+            xs.resize((size_t)std::max<int64_t>(nx, 1) * esz);
+            if (cdt == VBC_F64) host_convert(x, x_dtype, nx, incx, reinterpret_cast<double *>(xs.data()));
+            else if (cdt == VBC_F32) host_convert(x, x_dtype, nx, incx, reinterpret_cast<float *>(xs.data()));
+            else host_convert(x, x_dtype, nx, incx, reinterpret_cast<int64_t *>(xs.data()));
+            xp = xs.data();
+        }
+        if (beta != 0.0) {
+            if (cdt == VBC_F64) host_convert(y, y_dtype, ny, incy, reinterpret_cast<double *>(ys.data()));
+            else if (cdt == VBC_F32) host_convert(y, y_dtype, ny, incy, reinterpret_cast<float *>(ys.data()));
+            else host_convert(y, y_dtype, ny, incy, reinterpret_cast<int64_t *>(ys.data()));
+        }
+        if (int st = vbc_mul(h, trans, xp, nx, ys.data(), ny, alpha, beta, mem, stream, flags)) return st;
+        char *yp = static_cast<char *>(y);
+        const int yesz = elem_size(y_dtype);
+        for (int64_t i = 0; i < ny; i++) {
+            char *e = yp + i * incy * yesz;
+            if (y_dtype == VBC_F64) *reinterpret_cast<double *>(e) = reinterpret_cast<const double *>(ys.data())[i];
+            else if (y_dtype == VBC_F32) *reinterpret_cast<float *>(e) = reinterpret_cast<const float *>(ys.data())[i];
+            else if (y_dtype == VBC_I64) *reinterpret_cast<int64_t *>(e) = reinterpret_cast<const int64_t *>(ys.data())[i];
+            else *reinterpret_cast<int32_t *>(e) = (int32_t)reinterpret_cast<const int64_t *>(ys.data())[i];
+        }
+        return VBC_OK;
+    }
+    // device operands: conversion kernels into / out of the handle's staging buffers
+    apply_quirks(trans, flags, alpha, beta);
+    DeviceGuard g(h->device);
+    if (!g.ok) return fail(VBC_HIP_ERROR, "hipSetDevice failed");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(h->mu);
+    ProductOrder po(h, s, true);
+    void *dx = const_cast<void *>(x), *dy = y;
+    if (!direct_x) {
+        if (int st = stage_buffer(h, 0, nx * esz, &dx)) return st;
+    }
+    if (!direct_y) {
+        if (int st = stage_buffer(h, 1, ny * esz, &dy)) return st;
+    }
+    if (int st = po.begin()) return st;
+    if (!direct_x) {
+        if (int st = convert_gather(x, x_dtype, incx, dx, cdt, nx, s)) return st;
+    }
+    if (!direct_y && beta != 0.0) {
+        if (int st = convert_gather(y, y_dtype, incy, dy, cdt, ny, s)) return st;
+    }
+    if (int st = mul_dispatch(h, trans, dx, dy, alpha, beta, s)) return st;
+    if (!direct_y) {
+        if (int st = convert_scatter(dy, cdt, y, y_dtype, incy, ny, s)) return st;
+    }
+    return po.end();
 }
 
 }  // extern "C"

@@ -50,6 +50,17 @@ struct PanelLaunch {
     const int32_t *d_fill = nullptr;
 };
 
+// Integer-eltype layout (vbc_generic.hip): the reference layout itself, 0-based, on the device.
+struct IntLayout {
+    int64_t L = 0, nrows = 0;
+    const int32_t *col0 = nullptr, *w = nullptr, *rows = nullptr;  // per stripe / per stored row
+    const int32_t *col2stripe = nullptr;  // per column j: its stripe
+    const int32_t *row2stripe = nullptr;  // per stored row: its stripe
+    const int64_t *rbeg = nullptr;        // L+1 prefix into rows
+    const int64_t *voff = nullptr;        // per stripe: first value
+    const int64_t *val = nullptr;         // values as Int64
+};
+
 // Host description of the input stripes, common to 1D, 2D (expanded) and CSC inputs.
 struct Stripes {
     int64_t m = 0, n = 0, L = 0;
@@ -74,6 +85,7 @@ struct vbc_handle {
     int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
+    vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch
     std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
     bool f_scale = false;         // forward with several buckets: scale y by beta first
@@ -123,6 +135,10 @@ int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, double 
 int mulmat_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy, double alpha,
                     double beta, hipStream_t s);
 void occupancy_ranges(int esz, int K, int P, int occ[2]);
+// vbc_generic.hip
+int mul_int(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta, hipStream_t s);
+int convert_gather(const void *src, int src_dtype, int64_t inc, void *dst, int dst_dtype, int64_t n, hipStream_t s);
+int convert_scatter(const void *src, int src_dtype, void *dst, int dst_dtype, int64_t inc, int64_t n, hipStream_t s);
 // vbc_panel_launch.hip
 int mulmat_panel_any(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
                      int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s);

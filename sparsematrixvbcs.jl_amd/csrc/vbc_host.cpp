@@ -280,7 +280,13 @@ int vbcx_1dvbc_fill(int64_t m, int64_t n, int64_t W, const int64_t *colptr, cons
     if (dtype == VBC_F32)
         return fill_1d(m, W, colptr, rowval, (const float *)nzval, L, spl, pos, ofs, idx,
                        (float *)val, pad);
-    return fail(VBC_UNSUPPORTED_DTYPE, "dtype must be VBC_F64 or VBC_F32");
+    if (dtype == VBC_I64)
+        return fill_1d(m, W, colptr, rowval, (const int64_t *)nzval, L, spl, pos, ofs, idx, (int64_t *)val, pad);
+    if (dtype == VBC_I32)
+        return fill_1d(m, W, colptr, rowval, (const int32_t *)nzval, L, spl, pos, ofs, idx, (int32_t *)val, pad);
+    if (dtype == VBC_BOOL)
+        return fill_1d(m, W, colptr, rowval, (const uint8_t *)nzval, L, spl, pos, ofs, idx, (uint8_t *)val, pad);
+    return fail(VBC_UNSUPPORTED_DTYPE, "unknown dtype");
 }
 
 int vbcx_vbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t K,
@@ -328,7 +334,16 @@ int vbcx_vbc_fill(int64_t m, int64_t n, int64_t U, int64_t W, const int64_t *col
     if (dtype == VBC_F32)
         return fill_2d(m, U, W, colptr, rowval, (const float *)nzval, K, pspl, L, spl, pos, ofs,
                        idx, (float *)val, pad);
-    return fail(VBC_UNSUPPORTED_DTYPE, "dtype must be VBC_F64 or VBC_F32");
+    if (dtype == VBC_I64)
+        return fill_2d(m, U, W, colptr, rowval, (const int64_t *)nzval, K, pspl, L, spl, pos, ofs, idx,
+                       (int64_t *)val, pad);
+    if (dtype == VBC_I32)
+        return fill_2d(m, U, W, colptr, rowval, (const int32_t *)nzval, K, pspl, L, spl, pos, ofs, idx,
+                       (int32_t *)val, pad);
+    if (dtype == VBC_BOOL)
+        return fill_2d(m, U, W, colptr, rowval, (const uint8_t *)nzval, K, pspl, L, spl, pos, ofs, idx,
+                       (uint8_t *)val, pad);
+    return fail(VBC_UNSUPPORTED_DTYPE, "unknown dtype");
 }
 
 int vbcx_transpose_pattern(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,

@@ -17,6 +17,14 @@ inline int fail(int status, const char *what)
     return status;
 }
 
-inline int elem_size(int dtype) { return dtype == VBC_F64 ? 8 : dtype == VBC_F32 ? 4 : 0; }
+inline int elem_size(int dtype)
+{
+    switch (dtype) {
+    case VBC_F64: case VBC_I64: return 8;
+    case VBC_F32: case VBC_I32: return 4;
+    case VBC_BOOL: return 1;
+    default: return 0;
+    }
+}
 
 }  // namespace vbc

@@ -125,6 +125,7 @@ static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, do
 int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
                  hipStream_t stream)
 {
+    if (h->dtype == VBC_I64) return mul_int(h, trans, x, y, alpha, beta, stream);
     return h->dtype == VBC_F64 ? mul_device<double>(h, trans, x, y, alpha, beta, stream)
                                : mul_device<float>(h, trans, x, y, alpha, beta, stream);
 }

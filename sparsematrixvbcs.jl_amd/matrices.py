@@ -24,11 +24,12 @@ def _simd_pad(W, dtype, U=1):
 
 
 def _value_dtype(A):
-    """Bool / integer matrices are promoted to Float64 (exact for |v| < 2^53); fp32 stays fp32."""
-    if A.dtype == np.float32:
-        return np.float32
-    if A.dtype == np.float64 or A.dtype.kind in "biu":
-        return np.float64
+    """The reference's Tv as stored: Float64 / Float32 / Int64 / Int32 / Bool stay as they are (the
+    products compute in eltype(y), multiply_1DVBC.jl:102); other integer widths widen to Int64."""
+    if A.dtype in (np.float64, np.float32, np.int64, np.int32, np.bool_):
+        return A.dtype
+    if A.dtype.kind in "iu":
+        return np.int64
     raise _L.UnsupportedDtype(f"eltype {A.dtype} has no GPU kernel")
 
 
@@ -69,15 +70,26 @@ class _DeviceMatrix:
         self._handles = _Handles()
         self._finalizer = weakref.finalize(self, _Handles.release, self._handles)
 
-    def handle(self, device=0, trans=True, multi=False):
+    def handle(self, device=0, trans=True, multi=False, compute=None):
         """libvbc handle for mul!(y, B', x) (trans), mul!(y, B, x), or -- multi=True -- the
-        matrix-core multi-RHS product Y = B'X (a separate panel layout, built on first use)."""
+        matrix-core multi-RHS product Y = B'X (a separate panel layout, built on first use).
+        `compute` = the vbc_dtype the product runs in (eltype(y)); default: the value eltype's own
+        (floats) or exact Int64 (integers, Bool).  One handle per (device, layout, compute)."""
         flags = _L.VBC_CREATE_MULTI if multi else (_L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD)
-        return self._handles.get((int(device), flags), lambda out: self._create(out, int(device), flags))
+        compute = _L.compute_code(self.val.dtype) if compute is None else int(compute)
+        if compute == _L.VBC_I64 and self.val.dtype.kind == "f":
+            raise _L.UnsupportedDtype("a floating-point matrix cannot run in an integer eltype (InexactError)")
+        if multi and compute == _L.VBC_I64:
+            flags = _L.VBC_CREATE_TRANSPOSED  # integer eltypes: one SpMV per column
+        return self._handles.get((int(device), flags, compute),
+                                 lambda out: self._create(out, int(device), flags, compute))
 
-    def info(self, device=0, trans=True, multi=False):
+    def _types(self, compute):
+        return _L.vbc_types(_L.dtype_code(self.val.dtype), 64, compute, 0)
+
+    def info(self, device=0, trans=True, multi=False, compute=None):
         inf = _L.vbc_info()
-        _L.check(_L.lib().vbc_get_info(self.handle(device, trans, multi), C.byref(inf)), "info")
+        _L.check(_L.lib().vbc_get_info(self.handle(device, trans, multi, compute), C.byref(inf)), "info")
         return {f: getattr(inf, f) for f, _ in _L.vbc_info._fields_}
 
     def release(self):
@@ -160,12 +172,12 @@ class SparseMatrix1DVBC(_DeviceMatrix):
                  "SparseMatrix1DVBC")
         return cls(W, m, n, Phi, pos, idx, ofs, val)
 
-    def _create(self, out, device, flags):
+    def _create(self, out, device, flags, compute):
         spl = self.Phi.spl
-        return _L.lib().vbc1d_create(out, self.m, self.n, self.W, len(self.Phi), spl.ctypes.data,
-                                     self.pos.ctypes.data, self.idx.ctypes.data, self.ofs.ctypes.data,
-                                     self.val.ctypes.data, len(self.val), _L.dtype_code(self.val.dtype),
-                                     device, flags)
+        t = self._types(compute)
+        return _L.lib().vbc1d_create_ex(out, self.m, self.n, self.W, len(self.Phi), spl.ctypes.data,
+                                        self.pos.ctypes.data, self.idx.ctypes.data, self.ofs.ctypes.data,
+                                        self.val.ctypes.data, len(self.val), C.byref(t), device, flags)
 
     def __repr__(self):
         return (f"SparseMatrix1DVBC{{{self.W},{self.val.dtype},Int64}}({self.m}×{self.n}, "
@@ -231,11 +243,12 @@ class SparseMatrixVBC(_DeviceMatrix):
                  "SparseMatrixVBC")
         return cls(U, W, m, n, Pi, Phi, pos, idx, ofs, val)
 
-    def _create(self, out, device, flags):
-        return _L.lib().vbc2d_create(out, self.m, self.n, self.U, self.W, len(self.Pi), self.Pi.spl.ctypes.data,
-                                     len(self.Phi), self.Phi.spl.ctypes.data, self.pos.ctypes.data,
-                                     self.idx.ctypes.data, self.ofs.ctypes.data, self.val.ctypes.data,
-                                     len(self.val), _L.dtype_code(self.val.dtype), device, flags)
+    def _create(self, out, device, flags, compute):
+        t = self._types(compute)
+        return _L.lib().vbc2d_create_ex(out, self.m, self.n, self.U, self.W, len(self.Pi), self.Pi.spl.ctypes.data,
+                                        len(self.Phi), self.Phi.spl.ctypes.data, self.pos.ctypes.data,
+                                        self.idx.ctypes.data, self.ofs.ctypes.data, self.val.ctypes.data,
+                                        len(self.val), C.byref(t), device, flags)
 
     def __repr__(self):
         return (f"SparseMatrixVBC{{{self.U},{self.W},{self.val.dtype},Int64}}({self.m}×{self.n}, "
@@ -250,9 +263,10 @@ class SparseMatrixCSC(_DeviceMatrix):
         self.val = self.nzval
         self._init_handles()
 
-    def _create(self, out, device, flags):
-        return _L.lib().vbc_csc_create(out, self.m, self.n, self.colptr.ctypes.data, self.rowval.ctypes.data,
-                                       self.nzval.ctypes.data, _L.dtype_code(self.nzval.dtype), device, flags)
+    def _create(self, out, device, flags, compute):
+        t = self._types(compute)
+        return _L.lib().vbc_csc_create_ex(out, self.m, self.n, self.colptr.ctypes.data, self.rowval.ctypes.data,
+                                          self.nzval.ctypes.data, C.byref(t), device, flags)
 
 
 class Adjoint:

@@ -6,8 +6,9 @@
     B @ x, B.T @ x             Base.:*                                multiply_1DVBC.jl:182-185
 
 x / y are torch CUDA tensors (the product is enqueued on torch's current stream of that device, no
-synchronisation) or numpy arrays (staged through HBM by libvbc; returns when y is final).  The
-eltype of x and y must equal the matrix's.  Semantics are BLAS (y = α·op(B)·x + β·y); pass
+synchronisation) or numpy arrays (staged through HBM by libvbc; returns when y is final).  Like the
+reference, the product computes in eltype(y) with the matrix values and x converted to it
+(multiply_1DVBC.jl:27,34,102), and x / y may be any strided vectors.  Semantics are BLAS (y = α·op(B)·x + β·y); pass
 `quirks=True` to reproduce the reference's α/β handling bit for bit (vbc.h VBC_MUL_REFERENCE_QUIRKS).
 There is no CPU fallback: without libvbc or a GPU these raise.
 """
@@ -54,15 +55,31 @@ def _check_dtype(a, dtype, name):
         raise _L.UnsupportedDtype(f"{name} eltype {a.dtype} != matrix eltype {np.dtype(dtype)}")
 
 
-def _check_vec(a, dtype, name):
-    _check_dtype(a, dtype, name)
-    contiguous = a.flags.c_contiguous if isinstance(a, np.ndarray) else a.is_contiguous()
-    if not contiguous:
-        raise _L.ArgumentError(f"{name} must be contiguous (StridedVector with stride 1)")
+def _stride(a):
+    """Element stride of a 1-D numpy array or torch tensor (StridedVector; may be negative in numpy)."""
+    if isinstance(a, np.ndarray):
+        if a.strides[0] % a.itemsize:
+            raise _L.ArgumentError("stride is not a multiple of the element size")
+        return a.strides[0] // a.itemsize if a.shape[0] > 1 else 1
+    return a.stride(0) if a.shape[0] > 1 else 1
+
+
+def _compute_for(y, B):
+    """The eltype the product computes in: eltype(y) (multiply_1DVBC.jl:27,34,102)."""
+    cy = _L.dtype_code(y.dtype)
+    if cy in (_L.VBC_F64, _L.VBC_F32):
+        return cy
+    if cy in (_L.VBC_I64, _L.VBC_I32):
+        if B.dtype.kind == "f":
+            raise _L.UnsupportedDtype(f"integer y with a {B.dtype} matrix (InexactError in the reference)")
+        return _L.VBC_I64
+    raise _L.UnsupportedDtype(f"no GPU product into a {y.dtype} y")
 
 
 def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None, engine="auto"):
-    """LinearAlgebra.mul!(y, A, x, α, β); returns y.  Matrix x / y go to mulmat_ (engine)."""
+    """LinearAlgebra.mul!(y, A, x, α, β); returns y.  Any StridedVector x / y (strides, eltypes: the
+    product computes in eltype(y) with x converted, as multiply_1DVBC.jl:102 does).  Matrix x / y go
+    to mulmat_ (engine)."""
     B, trans = _unwrap(A)
     if not isinstance(B, _DeviceMatrix):
         raise TypeError(f"mul_ expects SparseMatrix1DVBC / SparseMatrixVBC / SparseMatrixCSC, got {type(B)}")
@@ -71,16 +88,21 @@ def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None
     mem, dev, stream = _mem_device_stream(x, y, stream)
     if device is not None and mem == _L.VBC_MEM_HOST:
         dev = device
-    _check_vec(x, B.dtype, "x")
-    _check_vec(y, B.dtype, "y")
     # DimensionMismatch before any handle is built (multiply_1DVBC.jl:44-45, :139-140)
     nx, ny = x.shape[0], y.shape[0]
     if (nx, ny) != ((B.m, B.n) if trans else (B.n, B.m)):
         raise _L.DimensionMismatch(f"size(A)={A.shape}, length(x)={nx}, length(y)={ny}")
-    h = B.handle(dev, trans)
+    cdt = _compute_for(y, B)
+    xdt, ydt = _L.dtype_code(x.dtype), _L.dtype_code(y.dtype)
+    incx, incy = _stride(x), _stride(y)
+    h = B.handle(dev, trans, compute=cdt)
     flags = _L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0
-    _L.check(_L.lib().vbc_mul(h, int(trans), _L.ptr(x), nx, _L.ptr(y), ny, float(alpha), float(beta), mem,
-                              stream, flags), "mul!")
+    if xdt == cdt and ydt == cdt and incx == 1 and incy == 1:
+        _L.check(_L.lib().vbc_mul(h, int(trans), _L.ptr(x), nx, _L.ptr(y), ny, float(alpha), float(beta), mem,
+                                  stream, flags), "mul!")
+    else:
+        _L.check(_L.lib().vbc_mul_ex(h, int(trans), _L.ptr(x), xdt, incx, nx, _L.ptr(y), ydt, incy, ny,
+                                     float(alpha), float(beta), mem, stream, flags), "mul!")
     return y
 
 
@@ -113,22 +135,19 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="
     row-major B'X, one SpMV per column otherwise)."""
     B, trans = _unwrap(A)
     mem, dev, stream = _mem_device_stream(X, Y, stream)
-    _check_dtype(X, B.dtype, "X")
-    _check_dtype(Y, B.dtype, "Y")
+    cdt = _compute_for(Y, B)
     if X.shape[1] != Y.shape[1]:
         raise _L.DimensionMismatch("X and Y have different numbers of columns")
-    if X.shape[1] <= 1:
-        # a single column is passed as a contiguous vector: it must have unit stride along dim 0
-        # (a column view of a wider row-major array does not)
-        for M, name in ((X, "X"), (Y, "Y")):
-            st = (M.strides[0] // M.itemsize) if isinstance(M, np.ndarray) else M.stride(0)
-            if M.shape[0] > 1 and st != 1:
-                raise _L.ArgumentError(f"{name}: a single-column operand needs unit stride along its rows")
-        lx = ly = "C"
-        ldx, ldy = max(X.shape[0], 1), max(Y.shape[0], 1)
-    else:
-        lx, ldx = _layout(X)
-        ly, ldy = _layout(Y)
+    if X.shape[1] <= 1 or cdt == _L.VBC_I64 or X.dtype != Y.dtype:
+        # column by column as strided vectors (a single column, integer eltypes, mixed eltypes):
+        # every column view keeps its own stride, so a column of a wider row-major array is read
+        # and written exactly where it lives
+        for c in range(X.shape[1]):
+            mul_(Y[:, c], A, X[:, c], alpha, beta, stream=stream, quirks=quirks)
+        return Y
+    _check_dtype(X, Y.dtype, "X")  # eltype(X) == eltype(Y); the matrix runs in that eltype
+    lx, ldx = _layout(X)
+    ly, ldy = _layout(Y)
     if lx != ly:
         raise _L.ArgumentError("X and Y must have the same layout")
     nrhs = X.shape[1]
@@ -136,8 +155,8 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="
         raise _L.ArgumentError(f"engine must be 'auto', 'mfma' or 'vector', got {engine!r}")
     if engine == "mfma" and not trans:
         raise _L.ArgumentError("the matrix-core engine computes B'X (pass an adjoint)")
-    mfma = trans and (engine == "mfma" or (engine == "auto" and nrhs >= MFMA_MIN_RHS))
-    h = B.handle(dev, trans, multi=mfma)
+    mfma = trans and cdt != _L.VBC_I64 and (engine == "mfma" or (engine == "auto" and nrhs >= MFMA_MIN_RHS))
+    h = B.handle(dev, trans, multi=mfma, compute=cdt)
     flags = (_L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0) | (_L.VBC_MAT_ROWMAJOR if lx == "R" else 0)
     _L.check(_L.lib().vbc_mul_mat(h, int(trans), nrhs, _L.ptr(X), max(ldx, 1), X.shape[0], _L.ptr(Y),
                                   max(ldy, 1), Y.shape[0], float(alpha), float(beta), mem, stream, flags),

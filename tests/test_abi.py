@@ -98,13 +98,42 @@ def test_csc_create_rejects_null_arrays():
     assert st == L.VBC_INVALID_ARG and "NULL" in L.last_error()
 
 
-def test_single_column_operand_needs_unit_row_stride():
-    """a column view of a row-major array is not a contiguous vector; mulmat_ must refuse it
-    (before any handle or device call) instead of reading / writing the wrong elements."""
+def test_typed_create_validation_without_gpu():
+    """vbc*_create_ex checks the type description before any device call."""
+    lib = L.lib()
+    h = C.c_void_p()
+    spl = np.array([1, 2], dtype=np.int32)
+    z = np.array([1, 1], dtype=np.int32)
+    bad = [L.vbc_types(L.VBC_F64, 16, L.VBC_F64, 0),      # index_bits
+           L.vbc_types(L.VBC_F64, 32, L.VBC_I32, 0),      # compute eltype
+           L.vbc_types(L.VBC_F32, 32, L.VBC_I64, 0),      # float values on an integer handle
+           L.vbc_types(9, 32, L.VBC_F64, 0)]              # unknown val eltype
+    for t in bad:
+        st = lib.vbc1d_create_ex(C.byref(h), 1, 1, 1, 1, spl.ctypes.data, z.ctypes.data, None, z.ctypes.data,
+                                 None, 0, C.byref(t), 0, 0)
+        assert st in (L.VBC_INVALID_ARG, L.VBC_UNSUPPORTED_DTYPE), st
+    # Int32 indices are widened and then validated like the Int64 path: W = 0 -> ArgumentError
+    t = L.vbc_types(L.VBC_I32, 32, L.VBC_I64, 0)
+    st = lib.vbc1d_create_ex(C.byref(h), 1, 1, 0, 1, spl.ctypes.data, z.ctypes.data, None, z.ctypes.data,
+                             None, 0, C.byref(t), 0, 0)
+    assert st == L.VBC_INVALID_ARG and "W must be > 0" in L.last_error()
+
+
+def test_mirror_keeps_reference_eltypes():
+    """Bool / Int32 / Int64 matrices keep their eltype (SparseMatrix1DVBC{W,Bool} etc.); their default
+    compute eltype is exact Int64, Float32 / Float64 compute in themselves."""
     import scipy.sparse as sp
-    A = sp.random(8, 6, 0.5, random_state=0, format="csc")
-    B = V.SparseMatrix1DVBC[2](A, V.EquiChunker(2))
-    X = np.zeros((8, 4))
-    Y = np.zeros((6, 4))
-    with pytest.raises(V.ArgumentError):
-        V.mul_(Y[:, 1:2], B.T, X[:, 1:2])
+    for dt, comp in ((np.bool_, L.VBC_I64), (np.int32, L.VBC_I64), (np.int64, L.VBC_I64),
+                     (np.float32, L.VBC_F32), (np.float64, L.VBC_F64)):
+        A = sp.csc_matrix(np.array([[1, 0, 1], [0, 1, 1]], dtype=dt))
+        B = V.SparseMatrix1DVBC[4](A, V.StrictChunker(4))
+        assert B.val.dtype == np.dtype(dt)
+        assert L.compute_code(B.val.dtype) == comp
+        D = np.zeros((2, 3), dtype=np.int64)
+        for l in range(len(B.Phi)):
+            j, w = B.Phi.spl[l] - 1, B.Phi.spl[l + 1] - B.Phi.spl[l]
+            q = B.ofs[l] - 1
+            for Q in range(B.pos[l] - 1, B.pos[l + 1] - 1):
+                D[B.idx[Q] - 1, j:j + w] += B.val[q:q + w].astype(np.int64)
+                q += w
+        assert np.array_equal(D, A.toarray().astype(np.int64))

@@ -1,0 +1,192 @@
+"""Generic eltypes, index widths, strided operands and concurrent products at the C ABI (vbc.h *_ex).
+
+The reference's mul! is generic: Tv in SIMD.VecTypes (Bool and Int32 matrices are in its test corpus,
+runtests.jl:15-16), Ti any integer, x / y any StridedVector, and the product computes in eltype(y)
+with values and x converted to it (multiply_1DVBC.jl:27,34,102).  Expected values:
+  * Bool / Int32 / Int64: numpy Int64 products (wrapping), Int32 results truncated -- exactly Julia's
+    Int64 / Int32 arithmetic; checked bit for bit, including the one-hot protocol (runtests.jl:29-53)
+    with y = A*x's eltype (Bool*Bool -> Int64, Int32*Int32 -> Int32);
+  * mixed float eltypes: the oracle in eltype(y) on the converted values (normwise 1e-12 / 1e-5).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import sparsematrixvbcs_amd as V
+from oracle import oracle as O
+from sparsematrixvbcs_amd import _lib as L
+from tests.conftest import SIZES
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+DEV = "cuda:0"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def int_matrix(m, n, kind, rng, density=0.2):
+    mask = rng.random((m, n)) < density
+    if kind == "bool":
+        return sp.csc_matrix(mask)
+    vals = rng.integers(-2**31, 2**31, (m, n)).astype(np.int32)
+    vals[vals == 0] = 1
+    return sp.csc_matrix(np.where(mask, vals, 0).astype(np.int32))
+
+
+def expected(A, x, trans, ydt):
+    D = A.toarray().astype(np.int64)
+    y = (D.T if trans else D) @ x.astype(np.int64)  # wraps mod 2^64 like Julia's Int64
+    return y.astype(ydt)                            # Int32: truncation = Julia's Int32 wraparound
+
+
+@pytest.mark.parametrize("kind", ["bool", "i32"])
+def test_integer_one_hot_size_grid(kind):
+    """runtests.jl:14-53 on Bool / Int32 matrices with their own eltypes: one-hot probes, y of A*x's
+    eltype (Int64 for Bool, Int32 for Int32), exact."""
+    rng = np.random.default_rng(0xDEADBEEF)
+    for m in SIZES[::2]:
+        for n in SIZES[1::2]:
+            A = int_matrix(m, n, kind, rng)
+            for meth in (V.StrictChunker(4), V.OverlapChunker(0.9, 4)):
+                B = V.SparseMatrix1DVBC[4](A, meth)
+                assert B.val.dtype == A.dtype
+                xdt = np.bool_ if kind == "bool" else np.int32
+                ydt = np.int64 if kind == "bool" else np.int32
+                for trans, nin, nout in ((False, n, m), (True, m, n)):
+                    op = B.T if trans else B
+                    for j in range(nin):
+                        x = np.zeros(nin, xdt)
+                        x[j] = 1
+                        y = torch.full((nout,), -7, dtype=getattr(torch, np.dtype(ydt).name), device=DEV)
+                        V.mul_(y, op, dev(x), True, False)
+                        assert np.array_equal(y.cpu().numpy(), expected(A, x, trans, ydt)), (m, n, trans, j)
+                B.release()
+
+
+@pytest.mark.parametrize("kind", ["bool", "i32"])
+def test_integer_random_x_wraparound(kind):
+    """Random Int32 x: the Int32 products overflow and wrap exactly like the reference; alpha / beta
+    integers; 2D VBC and CSC (TrSpMV!) handles too."""
+    rng = np.random.default_rng(7)
+    A = int_matrix(300, 200, kind, rng, 0.05)
+    x32 = rng.integers(-2**31, 2**31, 300).astype(np.int32)
+    xf = rng.integers(-2**31, 2**31, 200).astype(np.int32)
+    y0 = rng.integers(-2**31, 2**31, 200).astype(np.int32)
+    B = V.SparseMatrix1DVBC[8](A, V.StrictChunker(8))
+    y = dev(y0.copy())
+    V.mul_(y, B.T, dev(x32), 3, -2)
+    want = (3 * expected(A, x32, True, np.int64) - 2 * y0.astype(np.int64)).astype(np.int32)
+    assert np.array_equal(y.cpu().numpy(), want)
+    yf = dev(np.zeros(300, np.int64))
+    V.mul_(yf, B, dev(xf))
+    assert np.array_equal(yf.cpu().numpy(), expected(A, xf, False, np.int64))
+    C2 = V.SparseMatrixVBC[4, 4](A, V.AlternatingPacker(V.StrictChunker(4), V.StrictChunker(4)))
+    y2 = dev(np.zeros(200, np.int32))
+    V.mul_(y2, C2.T, dev(x32))
+    assert np.array_equal(y2.cpu().numpy(), expected(A, x32, True, np.int32))
+    y3 = dev(np.zeros(200, np.int32))
+    V.TrSpMV_(y3, A, dev(x32))
+    assert np.array_equal(y3.cpu().numpy(), expected(A, x32, True, np.int32))
+    # host operands
+    yh = np.zeros(200, np.int32)
+    V.mul_(yh, B.T, x32)
+    assert np.array_equal(yh, expected(A, x32, True, np.int32))
+
+
+def test_int32_index_arrays_match_int64():
+    """Ti = Int32 (SparseMatrix1DVBC{W,Tv,Int32}): the *_ex create widens the indices; results equal
+    the Int64 handle's bit for bit."""
+    rng = np.random.default_rng(11)
+    B = V.synthetic.vbr_1dvbc(5000, 900, 20000, np.arange(900) % 8 + 1, W=8, seed=5)
+    h = C.c_void_p()
+    t = L.vbc_types(L.VBC_F64, 32, L.VBC_F64, 0)
+    a32 = [np.ascontiguousarray(a, dtype=np.int32) for a in (B.Phi.spl, B.pos, B.idx, B.ofs)]
+    L.check(L.lib().vbc1d_create_ex(C.byref(h), B.m, B.n, B.W, len(B.Phi), *(a.ctypes.data for a in a32),
+                                    B.val.ctypes.data, len(B.val), C.byref(t), 0, L.VBC_CREATE_TRANSPOSED))
+    try:
+        x = dev(rng.uniform(-1, 1, B.m))
+        y32 = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+        y64 = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+        stream = torch.cuda.current_stream().cuda_stream
+        L.check(L.lib().vbc_mul(h, 1, x.data_ptr(), B.m, y32.data_ptr(), B.n, 1.0, 0.0, L.VBC_MEM_DEVICE, stream, 0))
+        V.mul_(y64, B.T, x)
+        assert torch.equal(y32, y64)
+    finally:
+        L.lib().vbc_destroy(h)
+
+
+def test_mixed_float_eltypes_compute_in_eltype_y():
+    """Float32 matrix, Float32 x, Float64 y -> computed in Float64 (values and x converted); Float64
+    matrix with Float32 y -> computed in Float32 (multiply_1DVBC.jl:102)."""
+    rng = np.random.default_rng(13)
+    B = V.synthetic.vbr_1dvbc(4000, 700, 9000, np.arange(700) % 5 + 1, W=8, dtype=np.float32, seed=9)
+    x = rng.uniform(-1, 1, B.m).astype(np.float32)
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    ref = O.mul(R64, x.astype(np.float64), np.zeros(B.n), trans=True)
+    y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert np.linalg.norm(y.cpu().numpy() - ref) <= 1e-12 * np.linalg.norm(ref)
+    B64 = V.synthetic.vbr_1dvbc(4000, 700, 9000, np.arange(700) % 5 + 1, W=8, dtype=np.float64, seed=9)
+    y32 = torch.zeros(B.n, dtype=torch.float32, device=DEV)
+    V.mul_(y32, B64.T, dev(x.astype(np.float64)))
+    R32 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B64.val.astype(np.float32))
+    ref32 = O.mul(R32, x, np.zeros(B.n, np.float32), trans=True)
+    assert np.linalg.norm(y32.cpu().numpy() - ref32) <= 1e-5 * np.linalg.norm(ref32)
+
+
+def test_strided_vectors():
+    """StridedVector x / y (multiply_1DVBC.jl:9,85): torch views with stride 3, numpy reversed views
+    (negative stride), column views of row-major matrices; beta != 0 reads y through the stride."""
+    rng = np.random.default_rng(17)
+    B = V.synthetic.vbr_1dvbc(3000, 600, 8000, np.arange(600) % 7 + 1, W=8, seed=21)
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    xs = rng.uniform(-1, 1, 3 * B.m)
+    ys = rng.uniform(-1, 1, 3 * B.n)
+    ref = O.mul(R, xs[::3].copy(), ys[1::3].copy(), 0.5, 2.0, trans=True, ref_semantics=False)
+    xt, yt = dev(xs), dev(ys)
+    V.mul_(yt[1::3], B.T, xt[::3], 0.5, 2.0)
+    got = yt.cpu().numpy()
+    assert np.linalg.norm(got[1::3] - ref) <= 1e-12 * np.linalg.norm(ref)
+    assert np.array_equal(got[0::3], ys[0::3]) and np.array_equal(got[2::3], ys[2::3])  # untouched
+    # numpy reversed views (host path)
+    xr = rng.uniform(-1, 1, B.n)
+    yr = np.zeros(B.m)
+    V.mul_(yr[::-1], B, xr[::-1])
+    assert np.linalg.norm(yr[::-1] - O.mul(R, xr[::-1].copy(), np.zeros(B.m))) <= 1e-12 * np.linalg.norm(yr)
+    # a single column of a row-major matrix
+    X = rng.uniform(-1, 1, (B.m, 4))
+    Y = np.full((B.n, 4), 5.0)
+    V.mul_(Y[:, 2:3], B.T, X[:, 2:3])
+    assert np.linalg.norm(Y[:, 2] - O.mul(R, X[:, 2].copy(), np.zeros(B.n), trans=True)) <= 1e-12 * np.linalg.norm(Y[:, 2])
+    assert np.all(Y[:, [0, 1, 3]] == 5.0)
+
+
+@pytest.mark.parametrize("layout", ["merge", "auto"])
+def test_concurrent_products_on_two_streams(monkeypatch, layout):
+    """Products on one handle from two streams at once: the merge layout's shared carry slots are
+    ordered by the handle's event chain (vbc_handle::mu), so every result equals the serial one."""
+    if layout == "merge":
+        monkeypatch.setenv("VBC_SLOTS", "0")
+        monkeypatch.setenv("VBC_SWEEP", "0")
+    rng = np.random.default_rng(23)
+    B = V.synthetic.vbr_1dvbc(200000, 40000, 2000000, rng.integers(1, 9, 40000), W=8, seed=4)
+    xs = [dev(rng.uniform(-1, 1, B.m)) for _ in range(8)]
+    serial = []
+    for x in xs:
+        y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+        V.mul_(y, B.T, x)
+        serial.append(y)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros(B.n, dtype=torch.float64, device=DEV) for _ in xs]
+    for i, x in enumerate(xs):
+        with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+            V.mul_(outs[i], B.T, x)
+    torch.cuda.synchronize()
+    for a, b in zip(outs, serial):
+        assert torch.equal(a, b)
