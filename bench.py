@@ -94,6 +94,8 @@ def kernel_name(B, local, k):
     if k > 1:
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     inf = B.info(local, True)
+    if inf["planar_bins"] > 0:
+        return "vbc::spmv_planar<T, W, FASTE, NB, KC> (planar slotted chunks, csrc/vbc_planar.h)"
     if inf["sweep_bins"] > 0:
         return "vbc::spmv_sweep<T, TB> (row-swept tiles, csrc/vbc_sweep.hip)"
     if inf["slot_bins"] > 0:

@@ -181,10 +181,10 @@ typedef struct vbc_info {
     int64_t bytes_t;        /* HBM bytes one transposed product moves in this layout */
     int64_t bytes_f;        /* same for the forward product */
     int32_t bins_m;         /* width buckets of the multi-RHS panel layout (0 = absent) */
-    int32_t slot_bins;      /* buckets laid out slotted (vbc_slots.h), both directions */
+    int32_t slot_bins;      /* buckets laid out slotted (vbc_slots.h / vbc_planar.h), both directions */
     int64_t bytes_m;        /* matrix bytes (keys + values, panel-padded) one panel pass streams */
     int32_t sweep_bins;     /* B'x buckets laid out row-swept (vbc_sweep.hip) */
-    int32_t reserved_;
+    int32_t planar_bins;    /* B'x buckets laid out planar (vbc_planar.h) */
 } vbc_info;
 
 VBC_API int vbc_get_info(const vbc_handle *h, vbc_info *info);

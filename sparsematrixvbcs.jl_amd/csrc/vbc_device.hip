@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "vbc_handle.h"
+#include "vbc_planar.h"
 
 namespace vbc {
 
@@ -235,9 +236,19 @@ static int slot_spl(const vbc_handle *h, int kind, int w)
     return (h->esz == 4 && w == 2) ? 2 : 1;  // the only narrow form that measured faster (vbc_slots.h)
 }
 
+// Planar chunk rows (vbc_planar.h) for a B'x bucket of width w: one stripe per lane whenever a row
+// is wider than one 16-B lane vector would hold with a single lane (fp64 w >= 3, fp32 w >= 5) and for
+// fp32 w = 3 (12-B rows, no padding to 4).
+static bool slot_planar(const vbc_handle *h, int kind, int w)
+{
+    if (kind != 0 || h->slot_planar == 0 || w < 3 || w > 8) return false;
+    return h->esz == 8 || w != 4;
+}
+
 // Slots per chunk of a bucket stored w wide (lane-vector width as in the kernel).
 static int slot_rpi(const vbc_handle *h, int kind, int w)
 {
+    if (slot_planar(h, kind, w)) return 64;
     const int spl = slot_spl(h, kind, w);
     if (spl > 1) return 64 * spl;
     const int V = w <= 8 ? vec_elems(h->esz, w) : 1;
@@ -335,7 +346,9 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     const int64_t nch = (int64_t)cr.size();
     int64_t rows = 0;
     for (int32_t c : cr) rows += c;
-    int64_t nr = (int64_t)std::llround((double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1));
+    const bool planar = slot_planar(h, kind, w);
+    const double target = planar ? (double)h->target_ranges_p : (double)h->target_ranges_s[kind];
+    int64_t nr = (int64_t)std::llround(target * (double)real / (double)std::max<int64_t>(total_entries, 1));
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
     bool affine = true;
     for (size_t q = 1; q < out.size() && affine; q++)
@@ -366,6 +379,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.u = h->slot_u;
     b.diag = h->diag;
     b.spl = slot_spl(h, kind, w);
+    b.planar = planar ? 1 : 0;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -374,11 +388,12 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     if (getenv("VBC_NO_AFFINE")) b.out_affine = 0;  // A/B knob
     {
         const int V = w <= 8 ? vec_elems(esz, w) : 1;
-        const bool full = b.spl > 1 || (RPI * (w / V) == 64 && V * esz <= 16);
+        const bool full = b.spl > 1 || planar || (RPI * (w / V) == 64 && V * esz <= 16);
         b.contig = b.out_affine && (kind == 0 ? (full && wsrc == w && (nseg <= 1 || b.out_stride == w))
                                               : (nseg <= 1 || b.out_stride == 1));
     }
-    range0 += (int)nr;
+    if (planar) b.range0 = 0;  // its own launch
+    else range0 += (int)nr;
     const int64_t E = rows * RPI;
     ps.rows = rows;
     ps.keys.resize(E);
@@ -397,13 +412,21 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             const uint32_t last = qr + 1 == cr[c] ? kLast : 0u;
             for (int sl = 0; sl < RPI; sl++) {
                 const int64_t seg = c * RPI + sl, e = row * RPI + sl;
-                if (seg < nseg && sbeg[seg] + qr < sbeg[seg + 1]) {
-                    const Entry &en = ents[pstart[seg] + qr];
-                    key[e] = en.key | last;
-                    std::memcpy(vv + e * w * esz, val + en.voff * esz, (size_t)wsrc * esz);
+                const bool real_row = seg < nseg && sbeg[seg] + qr < sbeg[seg + 1];
+                const Entry *en = real_row ? &ents[pstart[seg] + qr] : nullptr;
+                // padding rows gather x[0] (m >= 1: the bucket has entries), taken as 0
+                key[e] = real_row ? (en->key | last) : (kPad | last);
+                if (planar) {  // column-group-major chunk row (vbc_planar.h)
+                    char *rowp = vv + row * RPI * w * esz;
+                    for (int cc = 0; cc < w; cc++) {
+                        char *dst = rowp + planar_off(esz, w, sl, cc) * esz;
+                        if (real_row && cc < wsrc) std::memcpy(dst, val + (en->voff + cc) * esz, (size_t)esz);
+                        else std::memset(dst, 0, (size_t)esz);
+                    }
+                } else if (real_row) {
+                    std::memcpy(vv + e * w * esz, val + en->voff * esz, (size_t)wsrc * esz);
                     if (wsrc < w) std::memset(vv + (e * w + wsrc) * esz, 0, (size_t)(w - wsrc) * esz);
                 } else {
-                    key[e] = kPad | last;  // gathers x[0] (m >= 1: the bucket has entries), taken as 0
                     std::memset(vv + e * w * esz, 0, (size_t)w * esz);
                 }
             }
@@ -620,7 +643,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         const int wp = padded_width(h, w);
         // the slotted kernel has no scan to feed: fp64 w = 3 runs unpadded (8-B lanes), measured
         // 117 -> 106 us on the ldoor stand-in (fp32 keeps 3 -> 4: 73 vs 84 us unpadded)
-        const int wps = (h->esz == 8 && w == 3 && !getenv("VBC_PAD")) ? 3 : wp;
+        const int wps = slot_planar(h, 0, w) ? w : (h->esz == 8 && w == 3 && !getenv("VBC_PAD")) ? 3 : wp;
         std::vector<int64_t> sbeg{0}, order;
         for (int64_t l : kv.second) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
         if (want_slots(h, 0, wps, sbeg, total, s.m, order)) {
@@ -936,6 +959,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.carry_seg = reinterpret_cast<int32_t *>(base + pb.o_cseg);
         L.bins.push_back(b);
     }
+    L.pbins.clear();
     for (const PendingSlot &ps : pss) {
         SlotBin b = ps.b;
         b.key = reinterpret_cast<const uint32_t *>(base + ps.o_key);
@@ -945,7 +969,11 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.rchunk = reinterpret_cast<const int32_t *>(base + ps.o_rchunk);
         b.base = reinterpret_cast<const uint32_t *>(base + ps.o_base);
         b.kdoff = reinterpret_cast<const uint32_t *>(base + ps.o_doff);
-        L.sbins.push_back(b);
+        (b.planar ? L.pbins : L.sbins).push_back(b);
+    }
+    if (!L.pbins.empty()) {
+        VBC_HIP(hipMalloc(&L.d_pbins, L.pbins.size() * sizeof(SlotBin)));
+        VBC_HIP(hipMemcpy(L.d_pbins, L.pbins.data(), L.pbins.size() * sizeof(SlotBin), hipMemcpyHostToDevice));
     }
     L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
     if (!L.bins.empty()) {
@@ -966,11 +994,13 @@ static void release(vbc_handle *h)
     if (h->lt.d_bins) (void)hipFree(h->lt.d_bins);
     if (h->lt.d_sbins) (void)hipFree(h->lt.d_sbins);
     if (h->lt.d_wbins) (void)hipFree(h->lt.d_wbins);
+    if (h->lt.d_pbins) (void)hipFree(h->lt.d_pbins);
     if (h->lm.d_bins) (void)hipFree(h->lm.d_bins);
     for (auto &l : h->lf) {
         if (l.d_bins) (void)hipFree(l.d_bins);
         if (l.d_sbins) (void)hipFree(l.d_sbins);
         if (l.d_wbins) (void)hipFree(l.d_wbins);
+        if (l.d_pbins) (void)hipFree(l.d_pbins);
     }
     if (h->d_arena) (void)hipFree(h->d_arena);
     if (h->d_carry_mm) (void)hipFree(h->d_carry_mm);
@@ -1096,6 +1126,9 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     h->sweep_tile = (h->esz == 8 ? 4 : 2) * kSweepTileBytes;  // measured on NS: fp64 32 KB 473 us (16 KB 508), fp32 16 KB 313 us (32 KB 353)
     if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
+    if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    h->target_ranges_p = prop.multiProcessorCount * std::max(1, std::min(occupancy_planar(h->esz), 8)) * kWavesPerBlock;
+    if (const char *e = getenv("VBC_TARGET_RANGES_P")) h->target_ranges_p = std::max(1, atoi(e));
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
     if (flags & VBC_CREATE_MULTI) {
         const int om = occupancy_panel(h->esz);
@@ -1336,12 +1369,14 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
     info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : 0;
-    int32_t sl = h->has_t ? (int32_t)h->lt.sbins.size() : 0;
+    int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)l.sbins.size() : 0;
     info->slot_bins = sl;
     int32_t sw = h->has_t ? (int32_t)h->lt.wbins.size() : 0;
     for (auto &l : h->lf) sw += h->has_f ? (int32_t)l.wbins.size() : 0;
     info->sweep_bins = sw;
+    int32_t pl = h->has_t ? (int32_t)h->lt.pbins.size() : 0;
+    info->planar_bins = pl;
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }
@@ -1472,7 +1507,7 @@ static int mul_mat_device(vbc_handle *h, int trans, int64_t nrhs, const char *dX
     int st = VBC_OK;
     bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t && h->dtype != VBC_I64;
     for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
-    fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty();  // the fused vector kernel reads the merge layout only
+    fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty() && h->lt.pbins.empty();  // the fused vector kernel reads the merge layout only
     if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
         const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
         const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;

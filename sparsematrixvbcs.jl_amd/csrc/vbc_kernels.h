@@ -87,6 +87,8 @@ struct SlotBin {
     int32_t contig;      // affine and chunk outputs contiguous in y (LDS-staged writes allowed)
     int32_t kc;          // compressed keys: per-row base + int16 per-slot deltas
     int32_t spl;         // segments per lane (narrow B'x rows: 16 / (w * sizeof(T))), else 1
+    int32_t planar;      // 1: planar chunk rows (vbc_planar.h: one stripe per lane, column groups)
+    int32_t pad_;
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key
@@ -138,6 +140,10 @@ int launch_sweep(int esz, int kind, const SweepBin *d_bins, int nbins, int total
 int launch_slots(int esz, int kind, const SlotBin *d_bins, int nbins, int total_ranges, bool faste, int xcd, int u, int diag, int stage, bool kc,
                  const void *x, void *y, double alpha, double beta, bool rd, hipStream_t stream);
 int occupancy_slots(int esz, int kind);
+// vbc_planar.hip
+int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
+                  double alpha, double beta, bool rd, hipStream_t s);
+int occupancy_planar(int esz);
 
 __host__ __device__ constexpr int vec_elems(int esz, int w)
 {

@@ -44,6 +44,17 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
             return VBC_HIP_ERROR;
         }
     }
+    for (size_t i = 0; i < L.pbins.size(); i++) {  // planar buckets (vbc_planar.h): one launch each
+        const SlotBin &pb = L.pbins[i];
+        const bool faste = !rd && pb.out_affine && !getenv("VBC_NO_FASTE");
+        const bool staged = faste && pb.contig && slot_stage != 0;
+        const hipError_t e = (hipError_t)launch_planar((int)sizeof(T), pb, L.d_pbins + i, faste, staged, x, y, alpha,
+                                                       beta, rd, stream);
+        if (e != hipSuccess) {
+            set_error("spmv_planar launch failed: %s", hipGetErrorString(e));
+            return VBC_HIP_ERROR;
+        }
+    }
     if (L.total_ranges > 0) {
         const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
         const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;

@@ -1,0 +1,229 @@
+// gfx950 planar slotted kernel for mul!(y, B', x) with stripes 3..8 columns wide (device code,
+// included by vbc_planar.hip only).
+//
+// The slotted layout of vbc_slots.h gives a segment (stripe) LPR = w / V lanes when a stored row is
+// wider than one 16-B lane vector: fp64 w = 3 runs 3 lanes per stripe with 8-B loads, 21 stripes per
+// 63-lane wave, and the three lanes of a stripe gather the same x element.  Irregular 3-dof operators
+// (SuiteSparse ldoor / 3D stiffness matrices: every node column a w = 3 stripe) then issue one
+// 8-B-per-lane load, one key load and one gather per 21 stripe-rows -- request-rate bound (0.3-0.5 of
+// the HBM roofline).  The *planar* chunk keeps one stripe per lane (64 stripes per chunk, RPI = 64) and
+// stores each chunk row column-group-major: for the 16-B column groups g of the row (fp64: columns
+// {0,1}, {2,3}, ...; fp32: {0..3}, {4..7}; the last group narrower), the 64 lanes' group-g values are
+// contiguous, so every value load is one fully coalesced sweep (1 KiB for a 16-B group) and a lane
+// holds its stripe's whole row.  Per stored row a lane issues cld(w, 16 B / sizeof(T)) value loads,
+// one key load and one x gather (x[idx[Q]], multiply_1DVBC.jl:102) for 64 stripe-rows, folds the
+// w columns serially in stored (reference) row order, and at the chunk's LAST row writes its w
+// outputs (y[j : j+w-1], :114-116).  PAD / LAST / compressed keys, ranges of whole chunks, the
+// two-stage pipeline and LDS-staged contiguous y writes follow vbc_slots.h.
+#pragma once
+#include "vbc_kernels.h"
+
+namespace vbc {
+
+// Column groups of a W_-wide row: 16-B groups of G = 16 / sizeof(T) elements, the last one narrower.
+template <typename T>
+__host__ __device__ constexpr int planar_g() { return 16 / (int)sizeof(T); }
+template <typename T, int W_>
+__host__ __device__ constexpr int planar_ngroups() { return (W_ + planar_g<T>() - 1) / planar_g<T>(); }
+template <typename T, int W_, int GI>
+__host__ __device__ constexpr int planar_vg() { return (W_ - GI * planar_g<T>()) < planar_g<T>() ? (W_ - GI * planar_g<T>()) : planar_g<T>(); }
+
+// Element offset of (slot s, column c) inside a planar chunk row of width w (host and device).
+__host__ __device__ inline int64_t planar_off(int esz, int w, int s, int c)
+{
+    const int G = 16 / esz, g = c / G, vg = (w - g * G) < G ? (w - g * G) : G;
+    return (int64_t)64 * g * G + (int64_t)s * vg + (c - g * G);
+}
+
+// VG consecutive elements of a group (non-temporal: the value stream is read once); a 12-B group
+// (fp32, 3 columns) is one dwordx3 load.
+template <typename T, int VG>
+__device__ __forceinline__ void ld_group(gptr<const T> p, T *r)
+{
+    if constexpr (VG == 3) {
+        struct __attribute__((packed, aligned(4))) p3 { T a, b, c; };
+        const __attribute__((address_space(1))) p3 *q = (const __attribute__((address_space(1))) p3 *)p;
+        r[0] = q->a;  // merged into one dwordx3 load
+        r[1] = q->b;
+        r[2] = q->c;
+    } else if constexpr (VG == 1) {
+        r[0] = __builtin_nontemporal_load(p);
+    } else {
+        typedef T vt __attribute__((ext_vector_type(VG)));
+        const vt t = __builtin_nontemporal_load((gptr<const vt>)p);
+#pragma unroll
+        for (int e = 0; e < VG; e++) r[e] = t[e];
+    }
+}
+
+template <typename T, int W_, int GI>
+__device__ __forceinline__ void ld_row(gptr<const T> row, int lane, T (&v)[W_])
+{
+    if constexpr (GI < planar_ngroups<T, W_>()) {
+        constexpr int G = planar_g<T>(), VG = planar_vg<T, W_, GI>();
+        ld_group<T, VG>(row + 64 * GI * G + lane * VG, v + GI * G);
+        ld_row<T, W_, GI + 1>(row, lane, v);
+    }
+}
+
+// One range (wave): chunks [rchunk[r], rchunk[r+1]), rows [rrow[r], rrow[r+1]).
+// FASTE: affine y map and beta = 0 (no loads on the write path); NB > 0 (FASTE, contiguous chunk
+// outputs): NB finished chunks staged in LDS and written as one run of 16-B stores.
+template <typename T, int W_, int U, bool FASTE, int NB, bool KC>
+__device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, const T *__restrict__ x,
+                                           T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave, int *lds_out)
+{
+    const int R0 = G(b.rrow)[r], R1 = G(b.rrow)[r + 1];
+    if (R0 >= R1) return;
+    int c = G(b.rchunk)[r];
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> xg = G(x);
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;
+    const cptr bases = (cptr)b.base;
+    const cptr doffs = (cptr)b.kdoff;
+    auto load = [&](int R, uint32_t (&kk)[U], uint32_t (&bs)[U], T (&v)[U][W_]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int Rc = min(R + u, R1 - 1);
+            if constexpr (KC) {
+                kk[u] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + lane];
+                bs[u] = bases[Rc];
+            } else {
+                kk[u] = __builtin_nontemporal_load(key + (size_t)Rc * 64 + lane);
+                bs[u] = 0;
+            }
+            ld_row<T, W_, 0>(val + (size_t)Rc * 64 * W_, lane, v[u]);
+        }
+    };
+    constexpr uint32_t kPad16 = 0xFFFF8000u;
+    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&bs)[U], T (&xv)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t gi = KC ? (bs[u] & kSlotIdx) + (kk[u] == kPad16 ? 0u : kk[u]) : kk[u] & kSlotIdx;
+            xv[u] = xg[gi];
+        }
+    };
+    T acc[W_];
+#pragma unroll
+    for (int e = 0; e < W_; e++) acc[e] = T(0);
+    int nbuf = 0, cfirst = c;
+    const int c0 = c;
+    if constexpr (!FASTE) {
+        if (!b.out_affine) {
+            const int n = min(kSlotOutEntries, b.nseg - c0 * 64);
+            for (int i = lane; i < n; i += 64) lds_out[i] = G(b.out)[c0 * 64 + i];
+        }
+    }
+    // staged chunks [cfirst, cfirst + nbuf) -> y: one contiguous run of 64 * W_ values per chunk
+    auto write_out = [&]() {
+        const int64_t segs = min((int64_t)nbuf * 64, (int64_t)b.nseg - (int64_t)cfirst * 64);
+        const int64_t bytes = segs * W_ * (int64_t)sizeof(T);
+        char *dst = reinterpret_cast<char *>(y + b.out_base + (int64_t)cfirst * 64 * W_);
+        if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
+                if (off + 16 <= bytes) {
+                    *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                } else {
+                    for (int64_t q = off; q < bytes; q += sizeof(T))
+                        *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);
+                }
+            }
+        } else {
+            for (int64_t off = (int64_t)lane * sizeof(T); off < bytes; off += 64 * sizeof(T))
+                *(gptr<T>)(dst + off) = *reinterpret_cast<const T *>(lds_wave + off);
+        }
+        nbuf = 0;
+    };
+    auto flush = [&]() {
+        const int seg = c * 64 + lane;
+        if constexpr (NB > 0) {
+            T *st = reinterpret_cast<T *>(lds_wave) + ((size_t)nbuf * 64 + lane) * W_;
+#pragma unroll
+            for (int e = 0; e < W_; e++) st[e] = alpha * acc[e];
+            if (nbuf == 0) cfirst = c;
+        } else if (seg < b.nseg) {
+            const int o = (FASTE || b.out_affine) ? b.out_base + seg * b.out_stride : lds_out[(c - c0) * 64 + lane];
+            gptr<T> yo = G(y) + o;
+            const int lim = b.wst;  // padding columns (w > wst) are never written
+#pragma unroll
+            for (int e = 0; e < W_; e++) {
+                if (e < lim) {
+                    T q = alpha * acc[e];
+                    if (!FASTE && rd) q = fmadd(beta, yo[e], q);
+                    yo[e] = q;
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < W_; e++) acc[e] = T(0);
+        c++;
+        if constexpr (NB > 0) {
+            if (++nbuf == NB) write_out();
+        }
+    };
+    int R1v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
+    auto compute = [&](int R, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const T (&v)[U][W_],
+                       const T (&xv)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool live = R + u < R1v;
+            const bool pad = KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0;
+            const T xe = pad ? T(0) : xv[u];
+#pragma unroll
+            for (int e = 0; e < W_; e++) {
+                const T nv = fmadd(v[u][e], xe, acc[e]);
+                acc[e] = live ? nv : acc[e];
+            }
+            const uint32_t lastw = KC ? bs[u] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[u]);
+            if (R + u < R1 && (lastw & kLast)) flush();
+        }
+    };
+    uint32_t kA[U], kB[U], bA[U], bB[U];
+    T vA[U][W_], vB[U][W_], xv[U];
+    load(R0, kA, bA, vA);
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int R = R0; R < R1; R += 2 * U) {
+        gather(kA, bA, xv);
+        load(R + U, kB, bB, vB);
+        compute(R, kA, bA, vA, xv);
+        gather(kB, bB, xv);
+        load(R + 2 * U, kA, bA, vA);
+        compute(R + U, kB, bB, vB, xv);
+    }
+    if constexpr (NB > 0) {
+        if (nbuf > 0) write_out();
+    }
+}
+
+// Rows per pipeline step: about 24 values per lane per stage (fp64 w = 3: 8 rows).
+template <typename T, int W_>
+__host__ __device__ constexpr int planar_step()
+{
+    return (24 / W_) < 2 ? 2 : ((24 / W_) > 8 ? 8 : (24 / W_));
+}
+// Chunks staged per y write: 8 KB of LDS per wave.
+template <typename T, int W_>
+__host__ __device__ constexpr int planar_nb()
+{
+    return (8192 / (64 * W_ * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * W_ * (int)sizeof(T)));
+}
+
+template <typename T, int W_, bool FASTE, int NB, bool KC>
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__restrict__ bp, const T *__restrict__ x,
+                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const SlotBin b = *bp;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= b.nranges) return;
+    const int lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * 8192 : 16];
+    char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * 8192 : 0);
+    __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutEntries];
+    int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutEntries);
+    run_planar<T, W_, planar_step<T, W_>(), FASTE, NB, KC>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
+}
+
+}  // namespace vbc

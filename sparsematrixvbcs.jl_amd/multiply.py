@@ -47,12 +47,8 @@ def _mem_device_stream(x, y, stream):
 
 
 def _check_dtype(a, dtype, name):
-    if isinstance(a, np.ndarray):
-        same = a.dtype == np.dtype(dtype)
-    else:
-        same = str(a.dtype) == "torch." + np.dtype(dtype).name
-    if not same:
-        raise _L.UnsupportedDtype(f"{name} eltype {a.dtype} != matrix eltype {np.dtype(dtype)}")
+    if _L.dtype_code(a.dtype) != _L.dtype_code(dtype):
+        raise _L.UnsupportedDtype(f"{name} eltype {a.dtype} != {dtype}")
 
 
 def _stride(a):

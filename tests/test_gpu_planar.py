@@ -1,0 +1,113 @@
+"""GPU parity of the planar slotted layout (csrc/vbc_planar.h: one stripe per lane, column-group-major
+chunk rows) for mul!(y, B', x) with stripes 3..8 wide, against the oracle.  The library picks it for
+those widths automatically (fp64 w >= 3, fp32 w = 3 and w >= 5); VBC_SLOT_PLANAR=0 / 1 force the
+previous slotted form / planar.  Tolerances as test_gpu_parity.py: one-hot probes bit-exact (the
+reference's protocol, runtests.jl:29-53), random x <= 1e-12 (fp64) / 1e-5 (fp32)."""
+import numpy as np
+import pytest
+
+import sparsematrixvbcs_amd as V
+from oracle import oracle as O
+from tests.test_gpu_parity import TOL32, TOL64, dev, one_hot_probes, rel
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+DEV = "cuda:0"
+
+
+def ref_of(B):
+    return O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+
+
+def planar_bins(B):
+    return B.info(trans=True)["planar_bins"]
+
+
+@pytest.mark.parametrize("planar", ["0", "1"])
+def test_golden_one_hot_w8(golden, monkeypatch, planar):
+    """The reference corpus under StrictChunker(8) / OverlapChunker(0.9, 8): stripes up to 8 wide."""
+    monkeypatch.setenv("VBC_SLOTS", "1")
+    monkeypatch.setenv("VBC_SLOT_PLANAR", planar)
+    seen = 0
+    for key, g in golden.items():
+        for meth in (V.StrictChunker(8), V.OverlapChunker(0.9, 8)):
+            B = V.SparseMatrix1DVBC[8](g["A"], meth)
+            one_hot_probes(B, g["A"])
+            seen += planar_bins(B)
+    assert (seen > 0) == (planar == "1")
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w", [3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("keys16", ["0", "1"])
+def test_widths_random_x(monkeypatch, dtype, w, keys16):
+    """Every planar width, both key forms, natural (affine, LDS-staged writes) and length-sorted
+    (table-mapped) segment orders, alpha / beta."""
+    monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
+    rng = np.random.default_rng(w)
+    for ragged in (False, True):
+        L = 5000
+        q = 40000 if not ragged else 25000
+        B = V.synthetic.vbr_1dvbc(30000, L, q, w, W=8, dtype=dtype, seed=w + 7 * ragged)
+        if not ragged:  # near-uniform rows per stripe: natural order
+            pass
+        R = ref_of(B)
+        x = rng.uniform(-1, 1, B.m).astype(dtype)
+        y0 = rng.uniform(-1, 1, B.n).astype(dtype)
+        tol = TOL64 if dtype == np.float64 else TOL32
+        for alpha, beta in ((1.0, 0.0), (0.5, 2.0)):
+            y = dev(y0.copy())
+            V.mul_(y, B.T, dev(x), alpha, beta)
+            R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+            ref = O.mul(R64, x.astype(np.float64), y0.astype(np.float64), alpha, beta, trans=True,
+                        ref_semantics=False)
+            assert rel(y.cpu().numpy(), ref) <= tol, (w, ragged, alpha, beta)
+        exp_planar = w >= 3 and not (dtype == np.float32 and w == 4)
+        assert (planar_bins(B) > 0) == exp_planar or B.info(trans=True)["sweep_bins"] > 0
+
+
+@pytest.mark.parametrize("stage", ["0", "8"])
+def test_fe3d_planar_matches_oracle_bitwise(monkeypatch, stage):
+    """The irregular 3D stiffness operator (w = 3): planar result equals the oracle bit for bit
+    (same per-lane FMA order as multiply_1DVBC.jl:101-104), staged and direct y writes."""
+    monkeypatch.setenv("VBC_SLOT_STAGE", stage)
+    B = V.synthetic.fe_stiffness_3d_1dvbc(300000, 3_000_000)
+    assert planar_bins(B) == 1
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-1, 1, B.m)
+    y = torch.full((B.n,), float("nan"), dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    ref = O.mul(ref_of(B), x, np.zeros(B.n), trans=True)
+    assert np.array_equal(y.cpu().numpy(), ref)
+
+
+def test_planar_nonfinite_x():
+    """Inf / NaN in x land exactly where the reference puts them (padding rows take x as 0)."""
+    B = V.synthetic.fe_stiffness_3d_1dvbc(30000, 300000)
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, B.m)
+    x[[0, 17, 999]] = [np.inf, np.nan, -np.inf]
+    y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    ref = O.mul(ref_of(B), x, np.zeros(B.n), trans=True)
+    got = y.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    assert np.array_equal(got[fin], ref[fin])
+
+
+def test_planar_quirks_and_forward_unaffected():
+    """quirks mode (transposed overwrites y) and the forward product (not planar) on the same matrix."""
+    B = V.synthetic.fe_stiffness_3d_1dvbc(60000, 600000, dtype=np.float32)
+    R = ref_of(B)
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-1, 1, B.m).astype(np.float32)
+    y = dev(rng.uniform(-1, 1, B.n).astype(np.float32))
+    V.mul_(y, B.T, dev(x), 3.0, 7.0, quirks=True)
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    assert rel(y.cpu().numpy(), O.mul(R64, x.astype(np.float64), np.zeros(B.n), trans=True)) <= TOL32
+    xf = rng.uniform(-1, 1, B.n).astype(np.float32)
+    yf = torch.zeros(B.m, dtype=torch.float32, device=DEV)
+    V.mul_(yf, B, dev(xf))
+    assert rel(yf.cpu().numpy(), O.mul(R64, xf.astype(np.float64), np.zeros(B.m))) <= TOL32

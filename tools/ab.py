@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="fe", help="fe | ns | ns-mixed | c5 | ct20stif | ldoor | ldoor-csc")
+    ap.add_argument("--workload", default="fe", help="fe | fe3d | ns | ns-mixed | c5 | ct20stif | ldoor | ldoor-csc")
     ap.add_argument("--variants", default="VBC_TILE_K=4;VBC_TILE_K=8")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
@@ -39,16 +39,8 @@ def main():
     dtype = np.float64 if args.dtype == "f64" else np.float32
     if args.workload == "ldoor-csc":
         B = V.SparseMatrixCSC(V.synthetic.standin("GHS_psdef/ldoor").T.tocsc().astype(dtype))
-    elif args.workload in ("ct20stif", "ldoor"):
-        name = {"ct20stif": "Boeing/ct20stif", "ldoor": "GHS_psdef/ldoor"}[args.workload]
-        A = V.synthetic.standin(name).T.tocsc().astype(dtype)
-        B = V.SparseMatrix1DVBC[8](A, V.StrictChunker(8))
-    elif args.workload == "c5":
-        B = V.synthetic.c5(dtype=dtype, scale=args.scale)
-    elif args.workload == "fe":
-        B = V.synthetic.fe_grid_2d(int(round(2236 * args.scale ** 0.5)), dof=2, dtype=dtype)
-    else:
-        B = V.synthetic.north_star(dtype=dtype, scale=args.scale, mixed=(args.workload == "ns-mixed"))
+    else:  # fe | fe3d | ns | ns-mixed | c5 | ldoor | ct20stif: the bench's own matrices
+        B = bench.build_matrix(args.workload, dtype, args.scale)
     esz = np.dtype(dtype).itemsize
     trans = bool(args.trans)
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
@@ -81,7 +73,7 @@ def main():
         flags = L.VBC_CREATE_TRANSPOSED if trans else L.VBC_CREATE_FORWARD
         if "@multi" in v:  # matrix-core panel layout (multi-RHS transposed product)
             flags = L.VBC_CREATE_MULTI
-        L.check(B._create(C.byref(hp), 0, flags), "create")
+        L.check(B._create(C.byref(hp), 0, flags, L.compute_code(B.val.dtype)), "create")
         os.environ.clear()
         os.environ.update(saved)
         handles.append(hp)
