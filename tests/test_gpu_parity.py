@@ -203,8 +203,12 @@ def test_edge_cases():
         assert rel(y.cpu().numpy(), D @ xf) <= TOL64
     with pytest.raises(V.DimensionMismatch):
         V.mul_(torch.zeros(11, dtype=torch.float64, device=DEV), B.T, dev(x))
-    with pytest.raises(V.UnsupportedDtype):
-        V.mul_(torch.zeros(12, dtype=torch.float32, device=DEV), B.T, dev(x))
+    # eltype(y) = Float32 with a Float64 matrix computes in Float32 (multiply_1DVBC.jl:102 converts)
+    y32 = torch.zeros(12, dtype=torch.float32, device=DEV)
+    V.mul_(y32, B.T, dev(x))
+    assert rel(y32.cpu().numpy().astype(np.float64), D.T @ x) <= 1e-5
+    with pytest.raises(V.UnsupportedDtype):    # no GPU product into a Float16 y
+        V.mul_(torch.zeros(12, dtype=torch.float16, device=DEV), B.T, dev(x))
 
 
 def test_integer_valued_exact():

@@ -26,12 +26,13 @@ def planar_bins(B):
 
 @pytest.mark.parametrize("planar", ["0", "1"])
 def test_golden_one_hot_w8(golden, monkeypatch, planar):
-    """The reference corpus under StrictChunker(8) / OverlapChunker(0.9, 8): stripes up to 8 wide."""
+    """The reference corpus cut into 3-, 5- and 8-wide stripes (EquiChunker; the corpus' own column
+    patterns give Strict/Overlap chunkers stripes of at most 2 columns)."""
     monkeypatch.setenv("VBC_SLOTS", "1")
     monkeypatch.setenv("VBC_SLOT_PLANAR", planar)
     seen = 0
     for key, g in golden.items():
-        for meth in (V.StrictChunker(8), V.OverlapChunker(0.9, 8)):
+        for meth in (V.EquiChunker(3), V.EquiChunker(5), V.EquiChunker(8)):
             B = V.SparseMatrix1DVBC[8](g["A"], meth)
             one_hot_probes(B, g["A"])
             seen += planar_bins(B)
