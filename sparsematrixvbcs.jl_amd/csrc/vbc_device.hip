@@ -322,6 +322,28 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
     return 0;
 }
 
+// Row runs of a planar bucket (SlotBin::run): the largest R in {3, 2} such that every segment's rows
+// come in aligned runs of R consecutive x rows -- the dof rows of a node in a stiffness operator
+// stored by node stripes (fe3d, the ldoor / ct20stif stand-ins).  The kernel then reads one key per
+// run and gathers the run's R x values at once.  VBC_SLOT_RUNS=0 disables it (A/B, tests).
+static int slot_runs(const vbc_handle *h, const std::vector<Entry> &ents, const std::vector<int64_t> &sbeg)
+{
+    if (h->slot_runs == 0) return 1;
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    for (int R = 3; R >= 2; R--) {
+        bool ok = sbeg[nseg] > sbeg[0];
+        for (int64_t q = 0; q < nseg && ok; q++) {
+            const int64_t b = sbeg[q], len = sbeg[q + 1] - b;
+            if (len % R) { ok = false; break; }
+            for (int64_t t = 0; t < len && ok; t += R)
+                for (int d = 1; d < R; d++)
+                    if (ents[b + t + d].key != ents[b + t].key + (uint32_t)d) { ok = false; break; }
+        }
+        if (ok) return R;
+    }
+    return 1;
+}
+
 // Lay out a slotted bucket: chunk rows row-major over the slots, PAD / LAST keys, ranges of whole
 // chunks balanced by rows.  ents[sbeg[q] ...] are segment q's entries (keys = gather index only).
 static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vector<Entry> &ents,
@@ -342,11 +364,13 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     }
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     const int64_t real = sbeg[nseg] - sbeg[0];
-    const std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
+    const bool planar = slot_planar(h, kind, w);
+    const int run = planar ? slot_runs(h, ents, sbeg0) : 1;  // sbeg0: the input order ents is in
+    std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
+    for (int32_t &c : cr) c = (c + run - 1) / run * run;  // whole runs (an empty chunk: one padding run)
     const int64_t nch = (int64_t)cr.size();
     int64_t rows = 0;
     for (int32_t c : cr) rows += c;
-    const bool planar = slot_planar(h, kind, w);
     const double target = planar ? (double)h->target_ranges_p : (double)h->target_ranges_s[kind];
     int64_t nr = (int64_t)std::llround(target * (double)real / (double)std::max<int64_t>(total_entries, 1));
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
@@ -380,6 +404,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.diag = h->diag;
     b.spl = slot_spl(h, kind, w);
     b.planar = planar ? 1 : 0;
+    b.run = run;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -409,7 +434,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     int64_t row = 0;
     for (int64_t c = 0; c < nch; c++) {
         for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
-            const uint32_t last = qr + 1 == cr[c] ? kLast : 0u;
+            const uint32_t last = qr + run == cr[c] ? kLast : 0u;  // on the last run's first row
             for (int sl = 0; sl < RPI; sl++) {
                 const int64_t seg = c * RPI + sl, e = row * RPI + sl;
                 const bool real_row = seg < nseg && sbeg[seg] + qr < sbeg[seg + 1];
@@ -1127,6 +1152,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * std::max(1, std::min(occupancy_planar(h->esz), 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) h->target_ranges_p = std::max(1, atoi(e));
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
@@ -1377,6 +1403,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->sweep_bins = sw;
     int32_t pl = h->has_t ? (int32_t)h->lt.pbins.size() : 0;
     info->planar_bins = pl;
+    info->planar_run = 1;
+    if (h->has_t)
+        for (const auto &b : h->lt.pbins) info->planar_run = std::max<int32_t>(info->planar_run, b.run);
+    info->reserved_ = 0;
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }

@@ -88,7 +88,8 @@ struct SlotBin {
     int32_t kc;          // compressed keys: per-row base + int16 per-slot deltas
     int32_t spl;         // segments per lane (narrow B'x rows: 16 / (w * sizeof(T))), else 1
     int32_t planar;      // 1: planar chunk rows (vbc_planar.h: one stripe per lane, column groups)
-    int32_t pad_;
+    int32_t run;         // planar: every segment's rows come in runs of `run` consecutive x rows (1 = none);
+                         // keys / LAST are read from each run's first row, x gathered `run` elements wide
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key

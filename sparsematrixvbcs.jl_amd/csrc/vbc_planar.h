@@ -66,10 +66,29 @@ __device__ __forceinline__ void ld_row(gptr<const T> row, int lane, T (&v)[W_])
     }
 }
 
+// RUN consecutive elements of x from one lane: one gather of RUN * sizeof(T) bytes (fp64 RUN = 3:
+// dwordx4 + dwordx2; fp32 RUN = 3: dwordx3) instead of RUN separate requests.  Only element
+// alignment is known (a run starts at any x row).
+template <typename T, int RUN>
+__device__ __forceinline__ void ld_run(gptr<const T> p, T (&r)[RUN])
+{
+    if constexpr (RUN == 1) {
+        r[0] = *p;
+    } else {
+        struct __attribute__((packed, aligned(sizeof(T)))) pr { T e[RUN]; };
+        const __attribute__((address_space(1))) pr *q = (const __attribute__((address_space(1))) pr *)p;
+#pragma unroll
+        for (int d = 0; d < RUN; d++) r[d] = q->e[d];  // merged into wide loads
+    }
+}
+
 // One range (wave): chunks [rchunk[r], rchunk[r+1]), rows [rrow[r], rrow[r+1]).
+// RUN > 1 (b.run): every lane's rows come in aligned runs of RUN consecutive x rows (a node's dof
+// rows in a 3-dof stiffness operator): keys and the chunk's LAST flag are read from each run's first
+// row only, and the run's x values are one RUN-wide gather.
 // FASTE: affine y map and beta = 0 (no loads on the write path); NB > 0 (FASTE, contiguous chunk
 // outputs): NB finished chunks staged in LDS and written as one run of 16-B stores.
-template <typename T, int W_, int U, bool FASTE, int NB, bool KC>
+template <typename T, int W_, int U, bool FASTE, int NB, bool KC, int RUN>
 __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, const T *__restrict__ x,
                                            T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave, int *lds_out)
 {
@@ -82,26 +101,32 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     typedef __attribute__((address_space(4))) const uint32_t *cptr;
     const cptr bases = (cptr)b.base;
     const cptr doffs = (cptr)b.kdoff;
-    auto load = [&](int R, uint32_t (&kk)[U], uint32_t (&bs)[U], T (&v)[U][W_]) {
+    constexpr int NR = U / RUN;  // runs per step (ranges start and end on run boundaries)
+    static_assert(NR * RUN == U, "a step holds whole runs");
+    auto load = [&](int R, uint32_t (&kk)[NR], uint32_t (&bs)[NR], T (&v)[U][W_]) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int Rc = min(R + u, R1 - 1);
+        for (int j = 0; j < NR; j++) {
+            const int Rk = min(R + j * RUN, R1 - RUN);  // the run's first row (clamped: rows past the range)
             if constexpr (KC) {
-                kk[u] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + lane];
-                bs[u] = bases[Rc];
+                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + lane];
+                bs[j] = bases[Rk];
             } else {
-                kk[u] = __builtin_nontemporal_load(key + (size_t)Rc * 64 + lane);
-                bs[u] = 0;
+                kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
+                bs[j] = 0;
             }
-            ld_row<T, W_, 0>(val + (size_t)Rc * 64 * W_, lane, v[u]);
+#pragma unroll
+            for (int d = 0; d < RUN; d++) {
+                const int Rc = min(R + j * RUN + d, R1 - 1);
+                ld_row<T, W_, 0>(val + (size_t)Rc * 64 * W_, lane, v[j * RUN + d]);
+            }
         }
     };
     constexpr uint32_t kPad16 = 0xFFFF8000u;
-    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&bs)[U], T (&xv)[U]) {
+    auto gather = [&](const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], T (&xv)[NR][RUN]) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t gi = KC ? (bs[u] & kSlotIdx) + (kk[u] == kPad16 ? 0u : kk[u]) : kk[u] & kSlotIdx;
-            xv[u] = xg[gi];
+        for (int j = 0; j < NR; j++) {
+            const uint32_t gi = KC ? (bs[j] & kSlotIdx) + (kk[j] == kPad16 ? 0u : kk[j]) : kk[j] & kSlotIdx;
+            ld_run<T, RUN>(xg + gi, xv[j]);
         }
     };
     T acc[W_];
@@ -165,24 +190,27 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     };
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
-    auto compute = [&](int R, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const T (&v)[U][W_],
-                       const T (&xv)[U]) {
+    auto compute = [&](int R, const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], const T (&v)[U][W_],
+                       const T (&xv)[NR][RUN]) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const bool live = R + u < R1v;
-            const bool pad = KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0;
-            const T xe = pad ? T(0) : xv[u];
+        for (int j = 0; j < NR; j++) {
+            const bool live = R + j * RUN < R1v;
+            const bool pad = KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0;
 #pragma unroll
-            for (int e = 0; e < W_; e++) {
-                const T nv = fmadd(v[u][e], xe, acc[e]);
-                acc[e] = live ? nv : acc[e];
+            for (int d = 0; d < RUN; d++) {  // the run's rows in stored (reference) order
+                const T xe = pad ? T(0) : xv[j][d];
+#pragma unroll
+                for (int e = 0; e < W_; e++) {
+                    const T nv = fmadd(v[j * RUN + d][e], xe, acc[e]);
+                    acc[e] = live ? nv : acc[e];
+                }
             }
-            const uint32_t lastw = KC ? bs[u] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[u]);
-            if (R + u < R1 && (lastw & kLast)) flush();
+            const uint32_t lastw = KC ? bs[j] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[j]);
+            if (R + j * RUN < R1 && (lastw & kLast)) flush();
         }
     };
-    uint32_t kA[U], kB[U], bA[U], bB[U];
-    T vA[U][W_], vB[U][W_], xv[U];
+    uint32_t kA[NR], kB[NR], bA[NR], bB[NR];
+    T vA[U][W_], vB[U][W_], xv[NR][RUN];
     load(R0, kA, bA, vA);
     __builtin_amdgcn_s_waitcnt(0);
     for (int R = R0; R < R1; R += 2 * U) {
@@ -198,11 +226,12 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     }
 }
 
-// Rows per pipeline step: about 24 values per lane per stage (fp64 w = 3: 8 rows).
-template <typename T, int W_>
+// Rows per pipeline step: about 24 values per lane per stage (fp64 w = 3: 8 rows), whole runs.
+template <typename T, int W_, int RUN>
 __host__ __device__ constexpr int planar_step()
 {
-    return (24 / W_) < 2 ? 2 : ((24 / W_) > 8 ? 8 : (24 / W_));
+    constexpr int u = (24 / W_) < 2 ? 2 : ((24 / W_) > 8 ? 8 : (24 / W_));
+    return u / RUN * RUN < RUN ? RUN : u / RUN * RUN;
 }
 // Chunks staged per y write: 8 KB of LDS per wave.
 template <typename T, int W_>
@@ -211,7 +240,7 @@ __host__ __device__ constexpr int planar_nb()
     return (8192 / (64 * W_ * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * W_ * (int)sizeof(T)));
 }
 
-template <typename T, int W_, bool FASTE, int NB, bool KC>
+template <typename T, int W_, bool FASTE, int NB, bool KC, int RUN>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__restrict__ bp, const T *__restrict__ x,
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
 {
@@ -223,7 +252,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
     char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * 8192 : 0);
     __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutEntries];
     int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutEntries);
-    run_planar<T, W_, planar_step<T, W_>(), FASTE, NB, KC>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
+    run_planar<T, W_, planar_step<T, W_, RUN>(), FASTE, NB, KC, RUN>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds,
+                                                                      lds_out);
 }
 
 }  // namespace vbc

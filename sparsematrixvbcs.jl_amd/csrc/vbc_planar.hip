@@ -1,12 +1,12 @@
 // Launchers of the planar slotted kernel (vbc_planar.h): one launch per planar bucket, one kernel
-// instantiation per (value type, width 3..8, write path, key form).
+// instantiation per (value type, width 3..8, write path, key form, row run 1..3).
 #include <hip/hip_runtime.h>
 
 #include "vbc_planar.h"
 
 namespace vbc {
 
-template <typename T, int W_, bool KC>
+template <typename T, int W_, bool KC, int RUN>
 static void launch_w(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                      double alpha, double beta, bool rd, hipStream_t s)
 {
@@ -15,30 +15,43 @@ static void launch_w(const SlotBin &hb, const SlotBin *d_b, bool faste, bool sta
     T *ys = static_cast<T *>(y);
     constexpr int NB = planar_nb<T, W_>();
     if (faste && staged)
-        hipLaunchKernelGGL((spmv_planar<T, W_, true, NB, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar<T, W_, true, NB, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else if (faste)
-        hipLaunchKernelGGL((spmv_planar<T, W_, true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar<T, W_, true, 0, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else
-        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
 }
 
+template <typename T, bool KC, int RUN>
+static int launch_r(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
+                    double alpha, double beta, bool rd, hipStream_t s)
+{
+    switch (hb.wkey) {
+    case 3: launch_w<T, 3, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    case 4: launch_w<T, 4, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    case 5: launch_w<T, 5, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    case 6: launch_w<T, 6, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    case 7: launch_w<T, 7, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    case 8: launch_w<T, 8, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
+// row runs (SlotBin::run): 1 (none), 2 or 3 consecutive x rows per gather
 template <typename T, bool KC>
 static int launch_t(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                     double alpha, double beta, bool rd, hipStream_t s)
 {
-    switch (hb.wkey) {
-    case 3: launch_w<T, 3, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
-    case 4: launch_w<T, 4, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
-    case 5: launch_w<T, 5, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
-    case 6: launch_w<T, 6, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
-    case 7: launch_w<T, 7, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
-    case 8: launch_w<T, 8, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
+    switch (hb.run) {
+    case 1: return launch_r<T, KC, 1>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+    case 2: return launch_r<T, KC, 2>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+    case 3: return launch_r<T, KC, 3>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
     default: return (int)hipErrorInvalidValue;
     }
-    return (int)hipGetLastError();
 }
 
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
@@ -55,8 +68,8 @@ int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bo
 int occupancy_planar(int esz)
 {
     int occ = 0;
-    if (esz == 8) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar<double, 3, true, 0, true>, kBlockThreads, 0);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar<float, 3, true, 0, true>, kBlockThreads, 0);
+    if (esz == 8) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar<double, 3, true, 0, true, 1>, kBlockThreads, 0);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar<float, 3, true, 0, true, 1>, kBlockThreads, 0);
     return occ;
 }
 

@@ -112,3 +112,80 @@ def test_planar_quirks_and_forward_unaffected():
     yf = torch.zeros(B.m, dtype=torch.float32, device=DEV)
     V.mul_(yf, B, dev(xf))
     assert rel(yf.cpu().numpy(), O.mul(R64, xf.astype(np.float64), np.zeros(B.m))) <= TOL32
+
+
+def expand_runs(B, R, seed, break_one=False):
+    """B with every stored row i replaced by the run of R consecutive rows R(i-1)+1 .. R(i-1)+R (fresh
+    values): the node-dof row structure of a stiffness operator.  break_one: the first stripe's first
+    run gets a gap, so the bucket has no aligned runs."""
+    rng = np.random.default_rng(seed)
+    w = np.diff(B.Phi.spl)
+    cnt = np.diff(B.pos) * R
+    idx = ((B.idx[:, None] - 1) * R + np.arange(R)[None, :]).reshape(-1) + 1
+    if break_one:  # first run of the first non-empty stripe: rows r, r, r+2 (a repeated row, no run)
+        q0 = int(np.sum(cnt[:int(np.argmax(cnt > 0))]))
+        idx[q0 + 1] = idx[q0]
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)]).astype(np.int64)
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * w)]).astype(np.int64)
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + len(B.val) - int(B.ofs[-1] - 1), B.val.dtype)
+    val[:nv] = rng.uniform(-1, 1, nv).astype(B.val.dtype)
+    return V.SparseMatrix1DVBC(B.W, R * B.m, B.n, V.SplitPartition(B.Phi.spl.copy()), pos, idx.astype(np.int64),
+                               ofs, val)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("w", [3, 5, 8])
+def test_row_runs(monkeypatch, dtype, R, w):
+    """Row runs (SlotBin::run): one key and one R-wide x gather per run of R consecutive rows.  The
+    result equals the oracle bit for bit (fp64: same per-lane FMA order) and the run-free planar layout
+    (VBC_SLOT_RUNS=0); a bucket whose rows are not all in aligned runs falls back to run = 1."""
+    rng = np.random.default_rng(R * 10 + w)
+    base = V.synthetic.vbr_1dvbc(7000, 3000, 20000, w, W=8, dtype=dtype, seed=w)
+    B = expand_runs(base, R, seed=w + R)
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    x = rng.uniform(-1, 1, B.m).astype(dtype)
+    x[[5, 1234]] = [np.inf, np.nan]  # non-finite x inside runs: they land where the oracle puts them
+    outs = {}
+    for runs in ("1", "0"):
+        monkeypatch.setenv("VBC_SLOT_RUNS", runs)
+        monkeypatch.setenv("VBC_SLOT_PLANAR", "1")
+        monkeypatch.setenv("VBC_SLOTS", "1")
+        Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)  # fresh handle cache
+        inf = Bc.info(trans=True)
+        assert inf["planar_bins"] == 1 and inf["planar_run"] == (R if runs == "1" else 1)
+        y = torch.full((B.n,), 7.0, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+        V.mul_(y, Bc.T, dev(x))
+        outs[runs] = y.cpu().numpy()
+        Bc.release()
+    ref = O.mul(R64, x.astype(np.float64), np.zeros(B.n), trans=True)
+    got = outs["1"]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    if dtype == np.float64:
+        assert np.array_equal(got[fin], ref[fin])
+    else:
+        assert rel(np.nan_to_num(got[fin], posinf=0, neginf=0), np.nan_to_num(ref[fin], posinf=0, neginf=0)) <= TOL32
+    assert np.array_equal(outs["1"], outs["0"], equal_nan=True)
+
+
+def test_row_runs_fallback(monkeypatch):
+    """One stripe whose first two rows repeat an x row: not runs -> the bucket keeps run = 1."""
+    monkeypatch.setenv("VBC_SLOT_PLANAR", "1")
+    monkeypatch.setenv("VBC_SLOTS", "1")
+    base = V.synthetic.vbr_1dvbc(5000, 2000, 12000, 3, W=8, seed=3)
+    B = expand_runs(base, 3, seed=4, break_one=True)
+    assert B.info(trans=True)["planar_run"] == 1
+    rng = np.random.default_rng(6)
+    x = rng.uniform(-1, 1, B.m)
+    y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert np.array_equal(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(B.n), trans=True))
+
+
+def test_fe3d_uses_runs():
+    """The 3-dof stiffness stand-in (one stripe per node) is laid out with runs of 3."""
+    B = V.synthetic.fe_stiffness_3d_1dvbc(30000, 300000)
+    inf = B.info(trans=True)
+    assert inf["planar_bins"] == 1 and inf["planar_run"] == 3
