@@ -164,6 +164,44 @@ VBC_API int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, i
                 unsigned flags);
 
 /* ---------------------------------------------------------------------------------------------
+ * Multi-GPU (one process, several GPUs of a node; RCCL over xGMI).  SURVEY.md §8e.
+ *
+ * Replaces the reference's only parallel region, the threaded stripe loop of the transposed product
+ * (multiply_1DVBC.jl:169-177, multiply_VBC.jl:182-189), by a split of the matrix over GPUs: ranges
+ * balanced by HBM bytes, one single-GPU handle per device (vbc1d_create_ex on each slice).
+ *   VBC_SPLIT_STRIPES: GPU g owns stripes [l_g, l_g+1) (columns [c_g, c_g+1) of B; block rows of A
+ *     when B stores Aᵀ, as bin/test_table.jl:27 does).  B'x: x broadcast, y slices gathered to the
+ *     root (disjoint, bit-identical to one GPU).  Bx: x slices scattered, ncclReduce(sum) of y.
+ *   VBC_SPLIT_ROWS: GPU g owns the stored rows [r_g, r_g+1) of every stripe.  Bx: x broadcast, y slices
+ *     gathered (disjoint).  B'x: x slices, ncclReduce(sum) of y.
+ * devices: all distinct (one RCCL communicator per device, ncclCommInitAll) or all the same device
+ * (shards share it; no communicators -- oversubscription and single-GPU testing).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct vbc_sharded vbc_sharded; /* opaque */
+#define VBC_SPLIT_STRIPES 0
+#define VBC_SPLIT_ROWS 1
+
+/* Same matrix arguments as vbc1d_create_ex (types: Tv, Ti, compute eltype); `flags` as vbc1d_create
+ * (the layouts each shard builds). */
+VBC_API int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int64_t L, const void *spl,
+                                 const void *pos, const void *idx, const void *ofs, const void *val, int64_t nval,
+                                 const vbc_types *types, int ngpus, const int *devices, int split, unsigned flags);
+
+/* mul!(y, op(B), x, α, β) over all shards.  mem = VBC_MEM_DEVICE: x, y (compute eltype, contiguous) live
+ * on devices[0] and the product -- collectives included -- is ordered on `stream` (a hipStream_t of
+ * devices[0]) without host synchronisation.  mem = VBC_MEM_HOST: host x, y; returns when y is final.
+ * Products of one sharded handle are issued one at a time (an internal lock keeps every GPU's
+ * collective order identical). */
+VBC_API int vbc_sharded_mul(vbc_sharded *s, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
+                            double beta, int mem, void *stream, unsigned flags);
+
+VBC_API int vbc_sharded_destroy(vbc_sharded *s);
+VBC_API int vbc_sharded_count(const vbc_sharded *s, int *ngpus);
+/* Shard g: its single-GPU handle (owned by s), its 0-based range [lo, hi) of the split dimension
+ * (columns for VBC_SPLIT_STRIPES, rows for VBC_SPLIT_ROWS) and its device. */
+VBC_API int vbc_sharded_shard(const vbc_sharded *s, int g, vbc_handle **h, int64_t *lo, int64_t *hi, int *device);
+
+/* ---------------------------------------------------------------------------------------------
  * Introspection (for the Julia shim's size(), and for roofline accounting in bench.py)
  * ------------------------------------------------------------------------------------------- */
 typedef struct vbc_info {

@@ -19,12 +19,14 @@ VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
 VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD, VBC_CREATE_MULTI = 0x1, 0x2, 0x4
 VBC_MUL_REFERENCE_QUIRKS = 0x1
 VBC_MAT_ROWMAJOR = 0x2
+VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = 0, 1
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
     "vbc1d_create", "vbc2d_create", "vbc_csc_create", "vbc_destroy", "vbc_mul", "vbc_mul_mat",
     "vbc1d_create_ex", "vbc2d_create_ex", "vbc_csc_create_ex", "vbc_mul_ex",
     "vbc_get_info", "vbc_last_error", "vbc_version",
+    "vbc1d_create_sharded", "vbc_sharded_mul", "vbc_sharded_destroy", "vbc_sharded_count", "vbc_sharded_shard",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
     "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
     "vbcx_vbc_fill", "vbcx_transpose_pattern",
@@ -95,6 +97,11 @@ def lib():
         L.vbc_csc_create_ex.argtypes = [C.POINTER(P), I64, I64, P, P, P, T, INT, U]
         L.vbc_mul_ex.argtypes = [P, INT, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]
         L.vbc_destroy.argtypes = [P]
+        L.vbc1d_create_sharded.argtypes = [C.POINTER(P), I64, I64, I64, I64, P, P, P, P, P, I64, T, INT, P, INT, U]
+        L.vbc_sharded_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
+        L.vbc_sharded_destroy.argtypes = [P]
+        L.vbc_sharded_count.argtypes = [P, C.POINTER(INT)]
+        L.vbc_sharded_shard.argtypes = [P, INT, C.POINTER(P), C.POINTER(I64), C.POINTER(I64), C.POINTER(INT)]
         L.vbc_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
         L.vbc_mul_mat.argtypes = [P, INT, I64, P, I64, I64, P, I64, I64, D, D, INT, P, U]
         L.vbc_get_info.argtypes = [P, C.POINTER(vbc_info)]

@@ -184,3 +184,88 @@ class ShardedSparseMatrix1DVBC:
             return y
         self.local_mul(y, x, alpha, beta)
         return self._all_reduce(y)
+
+
+class MultiGPUSparseMatrix1DVBC:
+    """ONE process driving several GPUs: libvbc's sharded handle (include/vbc.h vbc1d_create_sharded,
+    RCCL over xGMI between distinct devices).  Same splits as ShardedSparseMatrix1DVBC, but the
+    exchange runs inside the library on device pointers of devices[0] (the Julia drop-in's
+    configuration: one session, x and y on one device, the other GPUs as workers).
+
+        S = MultiGPUSparseMatrix1DVBC(B, devices=[0, 1, 2, 3], split="stripes")
+        mul_(y, S.T, x)      # mul!(y, B', x): x broadcast, y slices gathered on devices[0]
+        mul_(y, S, x)        # mul!(y, B, x): x slices, ncclReduce(sum) of y
+
+    `devices` all equal (e.g. [0, 0, 0]) runs every shard on that device with no communicator."""
+
+    def __init__(self, B, devices=(0,), split="stripes", transposed=True, forward=True):
+        import ctypes as C
+        from . import _lib as _L
+        if split not in ("stripes", "rows"):
+            raise ValueError("split must be 'stripes' or 'rows'")
+        self.m, self.n, self.W = B.m, B.n, B.W
+        self.val = B.val  # eltype queries (mul_ computes in eltype(y))
+        self.split = split
+        self.devices = [int(d) for d in devices]
+        flags = (_L.VBC_CREATE_TRANSPOSED if transposed else 0) | (_L.VBC_CREATE_FORWARD if forward else 0)
+        t = _L.vbc_types(_L.dtype_code(B.val.dtype), 64, _L.compute_code(B.val.dtype), 0)
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        _L.check(_L.lib().vbc1d_create_sharded(
+            C.byref(h), B.m, B.n, B.W, len(B.Phi), B.Phi.spl.ctypes.data, B.pos.ctypes.data, B.idx.ctypes.data,
+            B.ofs.ctypes.data, B.val.ctypes.data, len(B.val), C.byref(t), len(self.devices), devs,
+            _L.VBC_SPLIT_STRIPES if split == "stripes" else _L.VBC_SPLIT_ROWS, flags), "create_sharded")
+        self._h = h
+        self.compute = t.compute_dtype
+
+    @property
+    def shape(self):
+        return (self.m, self.n)
+
+    @property
+    def T(self):
+        from .matrices import Adjoint
+        return Adjoint(self)
+
+    def shards(self):
+        """[(lo, hi, device)] per shard: its 0-based range of the split dimension (columns for
+        split='stripes', rows for split='rows')."""
+        import ctypes as C
+        from . import _lib as _L
+        out = []
+        for g in range(len(self.devices)):
+            lo, hi, dev = C.c_int64(), C.c_int64(), C.c_int()
+            _L.check(_L.lib().vbc_sharded_shard(self._h, g, None, C.byref(lo), C.byref(hi), C.byref(dev)), "shard")
+            out.append((lo.value, hi.value, dev.value))
+        return out
+
+    def _mul(self, y, x, trans, alpha, beta, stream, quirks):
+        from . import _lib as _L
+        from .multiply import _mem_device_stream, _stride
+        if len(x.shape) != 1 or len(y.shape) != 1:
+            raise _L.ArgumentError("the multi-GPU product takes vectors")
+        nx, ny = x.shape[0], y.shape[0]
+        if (nx, ny) != ((self.m, self.n) if trans else (self.n, self.m)):
+            raise _L.DimensionMismatch(f"size(A)={self.shape}, length(x)={nx}, length(y)={ny}")
+        for a in (x, y):
+            if _L.dtype_code(a.dtype) != self.compute or _stride(a) != 1:
+                raise _L.UnsupportedDtype("the multi-GPU product takes contiguous vectors of the matrix eltype")
+        mem, dev, stream = _mem_device_stream(x, y, stream)
+        if mem == _L.VBC_MEM_DEVICE and dev != self.devices[0]:
+            raise _L.ArgumentError(f"x and y must live on devices[0] = cuda:{self.devices[0]}")
+        flags = _L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0
+        _L.check(_L.lib().vbc_sharded_mul(self._h, int(trans), _L.ptr(x), nx, _L.ptr(y), ny, float(alpha),
+                                          float(beta), mem, stream, flags), "mul! (sharded)")
+        return y
+
+    def release(self):
+        from . import _lib as _L
+        if getattr(self, "_h", None):
+            _L.lib().vbc_sharded_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass

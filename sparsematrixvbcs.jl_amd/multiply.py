@@ -77,6 +77,8 @@ def mul_(y, A, x, alpha=1.0, beta=0.0, *, stream=None, quirks=False, device=None
     product computes in eltype(y) with x converted, as multiply_1DVBC.jl:102 does).  Matrix x / y go
     to mulmat_ (engine)."""
     B, trans = _unwrap(A)
+    if hasattr(B, "_mul") and not isinstance(B, _DeviceMatrix):  # distributed.MultiGPUSparseMatrix1DVBC
+        return B._mul(y, x, trans, alpha, beta, stream, quirks)
     if not isinstance(B, _DeviceMatrix):
         raise TypeError(f"mul_ expects SparseMatrix1DVBC / SparseMatrixVBC / SparseMatrixCSC, got {type(B)}")
     if len(y.shape) != 1 or len(x.shape) != 1:
