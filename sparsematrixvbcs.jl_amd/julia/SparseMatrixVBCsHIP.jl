@@ -5,11 +5,14 @@
 # syntax-reviewed only.  Every ccall signature mirrors include/vbc.h one to one; the Python mirror
 # (sparsematrixvbcs.jl_amd/*.py), which IS tested on the GPU, binds the same symbols the same way.
 #
-# Usage (after `using SparseMatrixVBCs, AMDGPU`):
+# Usage (after `using SparseMatrixVBCs`; ROCArray methods load with `using AMDGPU`, see
+# ext/SparseMatrixVBCsHIPAMDGPUExt.jl):
 #     B  = SparseMatrix1DVBC{8}(A)                 # reference constructor, unchanged
-#     Bd = HIPSparseMatrix1DVBC(B)                 # uploads once (vbc1d_create)
-#     mul!(y_dev, Bd', x_dev)                      # ROCArrays: enqueued on the task-local stream
-#     mul!(y_host, Bd', x_host)                    # Vectors: staged through HBM, synchronous
+#     Bd = HIPSparseMatrix1DVBC(B)                 # uploads once per compute eltype (vbc1d_create_ex)
+#     mul!(y, Bd', x)                              # host StridedVectors: staged through HBM
+#     mul!(y_dev, Bd', x_dev)                      # ROCVectors: enqueued on the task-local stream
+#     Bs = HIPShardedSparseMatrix1DVBC(B; devices=0:7)   # one session, 8 GPUs, RCCL over xGMI
+#     mul!(y, Bs', x)
 module SparseMatrixVBCsHIP
 
 using LinearAlgebra
@@ -20,14 +23,36 @@ const libvbc = get(ENV, "VBC_LIBRARY", joinpath(@__DIR__, "..", "libvbc.so"))
 
 const VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR,
       VBC_UNSUPPORTED_DTYPE, VBC_ASSERTION = 0, 1, 2, 3, 4, 5, 6
-const VBC_F64, VBC_F32 = Cint(0), Cint(1)
+const VBC_F64, VBC_F32, VBC_I64, VBC_I32, VBC_BOOL = Cint(0), Cint(1), Cint(2), Cint(3), Cint(4)
 const VBC_MEM_DEVICE, VBC_MEM_HOST = Cint(0), Cint(1)
 const VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD = Cuint(1), Cuint(2)
 const VBC_MUL_REFERENCE_QUIRKS = Cuint(1)
+const VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = Cint(0), Cint(1)
 
+# the eltypes the reference's tests use (runtests.jl:15-16) and their vbc_dtype codes
 vbc_dtype(::Type{Float64}) = VBC_F64
 vbc_dtype(::Type{Float32}) = VBC_F32
+vbc_dtype(::Type{Int64}) = VBC_I64
+vbc_dtype(::Type{Int32}) = VBC_I32
+vbc_dtype(::Type{Bool}) = VBC_BOOL
 vbc_dtype(::Type{T}) where {T} = throw(MethodError(vbc_dtype, (T,)))
+
+# The product computes in eltype(y) (multiply_1DVBC.jl:27,34,102): floats in themselves, integer y in
+# exact wrapping Int64 (Int32 y is stored back truncated, Julia's wraparound).
+compute_dtype(::Type{Float64}) = VBC_F64
+compute_dtype(::Type{Float32}) = VBC_F32
+compute_dtype(::Type{<:Union{Int64, Int32}}) = VBC_I64
+compute_dtype(::Type{T}) where {T} = throw(MethodError(compute_dtype, (T,)))
+
+# include/vbc.h vbc_types
+struct VbcTypes
+    val_dtype::Cint
+    index_bits::Cint
+    compute_dtype::Cint
+    reserved::Cint
+end
+vbc_types(::Type{Tv}, ::Type{Ti}, cdt::Cint) where {Tv, Ti <: Union{Int64, Int32}} =
+    VbcTypes(vbc_dtype(Tv), 8 * sizeof(Ti), cdt, 0)
 
 function last_error()
     buf = Vector{UInt8}(undef, 1024)
@@ -42,120 +67,193 @@ function check(st::Cint)
     st == VBC_DIM_MISMATCH && throw(DimensionMismatch(last_error()))
     st == VBC_INVALID_ARG && throw(ArgumentError(last_error()))
     st == VBC_ASSERTION && throw(AssertionError(last_error()))
+    st == VBC_UNSUPPORTED_DTYPE && throw(MethodError(mul!, (last_error(),)))
     throw(ErrorException(last_error()))
 end
 
 """
     HIPSparseMatrix1DVBC(B::SparseMatrix1DVBC; device=0, forward=true, transposed=true)
 
-Device-resident copy of `B` (the host struct is kept for `size`, printing and CPU fallbacks the
-caller may want).  Immutable; freed by a finalizer (`vbc_destroy`).
+Device-resident copies of `B`, one libvbc handle per compute eltype met (created on first use by
+`mul!`), freed by a finalizer (`vbc_destroy`).  Immutable.
 """
-mutable struct HIPSparseMatrix1DVBC{W, Tv}
-    host::SparseMatrix1DVBC{W, Tv, Int}
-    handle::Ptr{Cvoid}
+mutable struct HIPSparseMatrix1DVBC{W, Tv, Ti}
+    host::SparseMatrix1DVBC{W, Tv, Ti}
+    device::Int
+    flags::Cuint
+    handles::Dict{Cint, Ptr{Cvoid}}
 end
 
-function HIPSparseMatrix1DVBC(B::SparseMatrix1DVBC{W, Tv, Int}; device::Integer=0,
-                              forward::Bool=true, transposed::Bool=true) where {W, Tv}
-    h = Ref{Ptr{Cvoid}}(C_NULL)
+function HIPSparseMatrix1DVBC(B::SparseMatrix1DVBC{W, Tv, Ti}; device::Integer=0, forward::Bool=true,
+                              transposed::Bool=true) where {W, Tv, Ti}
     flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0))
-    GC.@preserve B check(ccall((:vbc1d_create, libvbc), Cint,
-        (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Int64},
-         Ptr{Int64}, Ptr{Cvoid}, Int64, Cint, Cint, Cuint),
-        h, B.m, B.n, W, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val),
-        vbc_dtype(Tv), device, flags))
-    M = HIPSparseMatrix1DVBC{W, Tv}(B, h[])
-    finalizer(M) do M
-        ccall((:vbc_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle)
-    end
+    M = HIPSparseMatrix1DVBC{W, Tv, Ti}(B, device, flags, Dict{Cint, Ptr{Cvoid}}())
+    finalizer(destroy_handles, M)
     return M
 end
 
-mutable struct HIPSparseMatrixVBC{U, W, Tv}
-    host::SparseMatrixVBC{U, W, Tv, Int}
-    handle::Ptr{Cvoid}
+function _create(B::SparseMatrix1DVBC{W, Tv, Ti}, device, flags, cdt::Cint) where {W, Tv, Ti}
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    t = Ref(vbc_types(Tv, Ti, cdt))
+    GC.@preserve B t check(ccall((:vbc1d_create_ex, libvbc), Cint,
+        (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Cvoid}, Int64,
+         Ptr{VbcTypes}, Cint, Cuint),
+        h, B.m, B.n, W, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val), t, device, flags))
+    return h[]
 end
 
-function HIPSparseMatrixVBC(B::SparseMatrixVBC{U, W, Tv, Int}; device::Integer=0,
-                            forward::Bool=true, transposed::Bool=true) where {U, W, Tv}
-    h = Ref{Ptr{Cvoid}}(C_NULL)
+mutable struct HIPSparseMatrixVBC{U, W, Tv, Ti}
+    host::SparseMatrixVBC{U, W, Tv, Ti}
+    device::Int
+    flags::Cuint
+    handles::Dict{Cint, Ptr{Cvoid}}
+end
+
+function HIPSparseMatrixVBC(B::SparseMatrixVBC{U, W, Tv, Ti}; device::Integer=0, forward::Bool=true,
+                            transposed::Bool=true) where {U, W, Tv, Ti}
     flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0))
-    GC.@preserve B check(ccall((:vbc2d_create, libvbc), Cint,
-        (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Int64, Ptr{Int64}, Int64, Ptr{Int64},
-         Ptr{Int64}, Ptr{Int64}, Ptr{Int64}, Ptr{Cvoid}, Int64, Cint, Cint, Cuint),
-        h, B.m, B.n, U, W, length(B.Π), B.Π.spl, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs,
-        B.val, length(B.val), vbc_dtype(Tv), device, flags))
-    M = HIPSparseMatrixVBC{U, W, Tv}(B, h[])
-    finalizer(M) do M
-        ccall((:vbc_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle)
-    end
+    M = HIPSparseMatrixVBC{U, W, Tv, Ti}(B, device, flags, Dict{Cint, Ptr{Cvoid}}())
+    finalizer(destroy_handles, M)
     return M
 end
 
-const HIPMatrix = Union{HIPSparseMatrix1DVBC, HIPSparseMatrixVBC}
+function _create(B::SparseMatrixVBC{U, W, Tv, Ti}, device, flags, cdt::Cint) where {U, W, Tv, Ti}
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    t = Ref(vbc_types(Tv, Ti, cdt))
+    GC.@preserve B t check(ccall((:vbc2d_create_ex, libvbc), Cint,
+        (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Int64, Ptr{Ti}, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti},
+         Ptr{Ti}, Ptr{Cvoid}, Int64, Ptr{VbcTypes}, Cint, Cuint),
+        h, B.m, B.n, U, W, length(B.Π), B.Π.spl, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val,
+        length(B.val), t, device, flags))
+    return h[]
+end
+
+# TrSpMV!(y, A::SparseMatrixCSC, x) (TrSpMV.jl:1-20) through a CSC handle (unit-width stripes).
+mutable struct HIPSparseMatrixCSC{Tv, Ti}
+    host::SparseMatrixCSC{Tv, Ti}
+    device::Int
+    flags::Cuint
+    handles::Dict{Cint, Ptr{Cvoid}}
+end
+
+function HIPSparseMatrixCSC(A::SparseMatrixCSC{Tv, Ti}; device::Integer=0) where {Tv, Ti}
+    M = HIPSparseMatrixCSC{Tv, Ti}(A, device, VBC_CREATE_TRANSPOSED, Dict{Cint, Ptr{Cvoid}}())
+    finalizer(destroy_handles, M)
+    return M
+end
+
+function _create(A::SparseMatrixCSC{Tv, Ti}, device, flags, cdt::Cint) where {Tv, Ti}
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    t = Ref(vbc_types(Tv, Ti, cdt))
+    GC.@preserve A t check(ccall((:vbc_csc_create_ex, libvbc), Cint,
+        (Ptr{Ptr{Cvoid}}, Int64, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Cvoid}, Ptr{VbcTypes}, Cint, Cuint),
+        h, size(A, 1), size(A, 2), A.colptr, A.rowval, A.nzval, t, device, flags))
+    return h[]
+end
+
+const HIPMatrix = Union{HIPSparseMatrix1DVBC, HIPSparseMatrixVBC, HIPSparseMatrixCSC}
 Base.size(A::HIPMatrix) = size(A.host)
 Base.size(A::HIPMatrix, d::Integer) = size(A.host, d)
+Base.eltype(A::HIPMatrix) = eltype(A.host)
 
-# Host vectors: staged by libvbc, synchronous.
-function _mul!(y::StridedVector{T}, A::HIPMatrix, trans::Bool, x::StridedVector{T},
-               α::Number, β::Number; quirks::Bool=false) where {T}
-    (stride(x, 1) == 1 && stride(y, 1) == 1) || throw(ArgumentError("unit-stride vectors only"))
-    GC.@preserve x y check(ccall((:vbc_mul, libvbc), Cint,
-        (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cdouble, Cdouble, Cint, Ptr{Cvoid}, Cuint),
-        A.handle, trans, x, length(x), y, length(y), Float64(α), Float64(β), VBC_MEM_HOST, C_NULL,
-        quirks ? VBC_MUL_REFERENCE_QUIRKS : Cuint(0)))
+# the handle computing in eltype(y); a Float matrix cannot run in an integer eltype (InexactError)
+function handle_for(A::HIPMatrix, ::Type{Ty}) where {Ty}
+    cdt = compute_dtype(Ty)
+    cdt == VBC_I64 && eltype(A) <: AbstractFloat && throw(InexactError(:convert, Ty, zero(eltype(A))))
+    get!(() -> _create(A.host, A.device, A.flags, cdt), A.handles, cdt)
+end
+
+function destroy_handles(A::HIPMatrix)
+    for h in values(A.handles)
+        ccall((:vbc_destroy, libvbc), Cint, (Ptr{Cvoid},), h)
+    end
+    empty!(A.handles)
+end
+
+# Host vectors (any StridedVector, any supported eltype: x converted to eltype(y) like
+# multiply_1DVBC.jl:102): vbc_mul_ex stages them through the handle's cached device buffers and
+# returns when y is final.  The eltypes travel with the pointers, so a mismatch cannot overrun.
+function _mul!(y::StridedVector{Ty}, A::HIPMatrix, trans::Bool, x::StridedVector{Tx}, α::Number, β::Number;
+               quirks::Bool=false) where {Ty, Tx}
+    h = handle_for(A, Ty)
+    GC.@preserve x y check(ccall((:vbc_mul_ex, libvbc), Cint,
+        (Ptr{Cvoid}, Cint, Ptr{Tx}, Cint, Int64, Int64, Ptr{Ty}, Cint, Int64, Int64, Cdouble, Cdouble, Cint,
+         Ptr{Cvoid}, Cuint),
+        h, trans, pointer(x), vbc_dtype(Tx), stride(x, 1), length(x), pointer(y), vbc_dtype(Ty), stride(y, 1),
+        length(y), Float64(α), Float64(β), VBC_MEM_HOST, C_NULL, quirks ? VBC_MUL_REFERENCE_QUIRKS : Cuint(0)))
     return y
 end
+
+const AdjOrTransHIP = Union{Adjoint{<:Any, <:HIPMatrix}, Transpose{<:Any, <:HIPMatrix}}
 
 # The reference's operator surface: mul!(y, B, x, α, β) and mul!(y, B', x, α, β)
 # (multiply_1DVBC.jl:9, :85; multiply_VBC.jl:3, :89) plus the 3-argument forms and Base.:*.
 LinearAlgebra.mul!(y::StridedVector, A::HIPMatrix, x::StridedVector, α::Number, β::Number) =
     _mul!(y, A, false, x, α, β)
-LinearAlgebra.mul!(y::StridedVector, adjA::Union{Adjoint{<:Any, <:HIPMatrix}, Transpose{<:Any, <:HIPMatrix}},
-                   x::StridedVector, α::Number, β::Number) = _mul!(y, parent(adjA), true, x, α, β)
+LinearAlgebra.mul!(y::StridedVector, adjA::AdjOrTransHIP, x::StridedVector, α::Number, β::Number) =
+    _mul!(y, parent(adjA), true, x, α, β)
 LinearAlgebra.mul!(y::StridedVector, A::HIPMatrix, x::StridedVector) = mul!(y, A, x, true, false)
-LinearAlgebra.mul!(y::StridedVector, adjA::Union{Adjoint{<:Any, <:HIPMatrix}, Transpose{<:Any, <:HIPMatrix}},
-                   x::StridedVector) = mul!(y, adjA, x, true, false)
-Base.:*(A::HIPMatrix, x::StridedVector{T}) where {T} = mul!(similar(x, T, size(A, 1)), A, x, true, false)
-Base.:*(adjA::Union{Adjoint{<:Any, <:HIPMatrix}, Transpose{<:Any, <:HIPMatrix}}, x::StridedVector{T}) where {T} =
-    mul!(similar(x, T, size(adjA, 1)), adjA, x, true, false)
+LinearAlgebra.mul!(y::StridedVector, adjA::AdjOrTransHIP, x::StridedVector) = mul!(y, adjA, x, true, false)
+# Base.:* (multiply_1DVBC.jl:182-185): y of promote_op(matprod, eltype(A), eltype(x))
+Base.:*(A::HIPMatrix, x::StridedVector{T}) where {T} =
+    mul!(similar(x, Base.promote_op(LinearAlgebra.matprod, eltype(A), T), size(A, 1)), A, x, true, false)
+Base.:*(adjA::AdjOrTransHIP, x::StridedVector{T}) where {T} =
+    mul!(similar(x, Base.promote_op(LinearAlgebra.matprod, eltype(parent(adjA)), T), size(adjA, 1)), adjA, x,
+         true, false)
 
-# TrSpMV!(y, A::SparseMatrixCSC, x) (TrSpMV.jl:1-20) through a CSC handle.
-mutable struct HIPSparseMatrixCSC{Tv}
-    host::SparseMatrixCSC{Tv, Int}
+TrSpMV!(y::StridedVector, A::HIPSparseMatrixCSC, x::StridedVector) = _mul!(y, A, true, x, true, false)
+
+"""
+    HIPShardedSparseMatrix1DVBC(B; devices=0:7, split=:stripes)
+
+`B` split over several GPUs of the node by byte-balanced stripe (`split=:stripes`, the block rows of
+A when B stores Aᵀ) or row (`split=:rows`) ranges, one handle per GPU, RCCL over xGMI for the exchange
+(vbc1d_create_sharded).  This replaces the reference's threaded stripe loop (multiply_1DVBC.jl:
+169-177).  Computes in Tv; host vectors or (with AMDGPU) ROCVectors on `devices[1]`.
+"""
+mutable struct HIPShardedSparseMatrix1DVBC{W, Tv, Ti}
+    host::SparseMatrix1DVBC{W, Tv, Ti}
     handle::Ptr{Cvoid}
 end
-function HIPSparseMatrixCSC(A::SparseMatrixCSC{Tv, Int}; device::Integer=0) where {Tv}
+
+function HIPShardedSparseMatrix1DVBC(B::SparseMatrix1DVBC{W, Tv, Ti}; devices=0:7, split::Symbol=:stripes,
+                                     forward::Bool=true, transposed::Bool=true) where {W, Tv, Ti}
+    split in (:stripes, :rows) || throw(ArgumentError("split must be :stripes or :rows"))
+    devs = Cint.(collect(devices))
+    flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0))
     h = Ref{Ptr{Cvoid}}(C_NULL)
-    GC.@preserve A check(ccall((:vbc_csc_create, libvbc), Cint,
-        (Ptr{Ptr{Cvoid}}, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Cvoid}, Cint, Cint, Cuint),
-        h, size(A, 1), size(A, 2), A.colptr, A.rowval, A.nzval, vbc_dtype(Tv), device, VBC_CREATE_TRANSPOSED))
-    M = HIPSparseMatrixCSC{Tv}(A, h[])
-    finalizer(M) do M
-        ccall((:vbc_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle)
-    end
+    t = Ref(vbc_types(Tv, Ti, compute_dtype(Tv <: Union{Bool, Int32} ? Int64 : Tv)))
+    GC.@preserve B t devs check(ccall((:vbc1d_create_sharded, libvbc), Cint,
+        (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Cvoid}, Int64,
+         Ptr{VbcTypes}, Cint, Ptr{Cint}, Cint, Cuint),
+        h, B.m, B.n, W, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val), t, length(devs), devs,
+        split === :stripes ? VBC_SPLIT_STRIPES : VBC_SPLIT_ROWS, flags))
+    M = HIPShardedSparseMatrix1DVBC{W, Tv, Ti}(B, h[])
+    finalizer(M -> ccall((:vbc_sharded_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle), M)
     return M
 end
-function TrSpMV!(y::Vector{T}, A::HIPSparseMatrixCSC{T}, x::Vector{T}) where {T}
-    GC.@preserve x y check(ccall((:vbc_mul, libvbc), Cint,
-        (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cdouble, Cdouble, Cint, Ptr{Cvoid}, Cuint),
-        A.handle, 1, x, length(x), y, length(y), 1.0, 0.0, VBC_MEM_HOST, C_NULL, Cuint(0)))
+
+Base.size(A::HIPShardedSparseMatrix1DVBC) = size(A.host)
+Base.size(A::HIPShardedSparseMatrix1DVBC, d::Integer) = size(A.host, d)
+
+function _mul!(y::Vector{T}, A::HIPShardedSparseMatrix1DVBC, trans::Bool, x::Vector{T}, α::Number, β::Number;
+               quirks::Bool=false) where {T}
+    GC.@preserve x y check(ccall((:vbc_sharded_mul, libvbc), Cint,
+        (Ptr{Cvoid}, Cint, Ptr{T}, Int64, Ptr{T}, Int64, Cdouble, Cdouble, Cint, Ptr{Cvoid}, Cuint),
+        A.handle, trans, x, length(x), y, length(y), Float64(α), Float64(β), VBC_MEM_HOST, C_NULL,
+        quirks ? VBC_MUL_REFERENCE_QUIRKS : Cuint(0)))
     return y
 end
 
-# Device arrays (AMDGPU.jl ROCArray): enqueue on the task-local HIP stream, no synchronisation.
-# Kept behind a package extension so the shim has no hard AMDGPU dependency:
-#
-#   function LinearAlgebra.mul!(y::ROCVector{T}, adjA::Adjoint{<:Any,<:HIPMatrix}, x::ROCVector{T},
-#                               α::Number, β::Number) where {T}
-#       check(ccall((:vbc_mul, libvbc), Cint,
-#           (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cdouble, Cdouble, Cint, Ptr{Cvoid}, Cuint),
-#           parent(adjA).handle, 1, pointer(x), length(x), pointer(y), length(y), α, β,
-#           VBC_MEM_DEVICE, AMDGPU.stream().stream, 0))
-#       return y
-#   end
+const AdjOrTransSharded = Union{Adjoint{<:Any, <:HIPShardedSparseMatrix1DVBC},
+                                Transpose{<:Any, <:HIPShardedSparseMatrix1DVBC}}
+LinearAlgebra.mul!(y::Vector, A::HIPShardedSparseMatrix1DVBC, x::Vector, α::Number, β::Number) =
+    _mul!(y, A, false, x, α, β)
+LinearAlgebra.mul!(y::Vector, adjA::AdjOrTransSharded, x::Vector, α::Number, β::Number) =
+    _mul!(y, parent(adjA), true, x, α, β)
+LinearAlgebra.mul!(y::Vector, A::HIPShardedSparseMatrix1DVBC, x::Vector) = mul!(y, A, x, true, false)
+LinearAlgebra.mul!(y::Vector, adjA::AdjOrTransSharded, x::Vector) = mul!(y, adjA, x, true, false)
 
-export HIPSparseMatrix1DVBC, HIPSparseMatrixVBC, HIPSparseMatrixCSC, TrSpMV!
+export HIPSparseMatrix1DVBC, HIPSparseMatrixVBC, HIPSparseMatrixCSC, HIPShardedSparseMatrix1DVBC, TrSpMV!
 
 end # module
