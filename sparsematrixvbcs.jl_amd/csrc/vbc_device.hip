@@ -1549,11 +1549,11 @@ static int mul_mat_device(vbc_handle *h, int trans, int64_t nrhs, const char *dX
             st = mul_dispatch(h, trans, dX + r * ldx * esz, dY + r * ldy * esz, alpha, beta, s);
         return st;
     }
-    // row-major, per column through contiguous temporaries (strided 2D copies)
+    // row-major, per column through the handle's cached contiguous temporaries (strided 2D copies);
+    // the caller holds h->mu, and the stream orders the columns -- no allocation, no synchronisation
     void *tx = nullptr, *ty = nullptr;
-    if (hipMalloc(&tx, std::max<int64_t>(nx, 1) * esz) != hipSuccess ||
-        hipMalloc(&ty, std::max<int64_t>(ny, 1) * esz) != hipSuccess)
-        st = fail(VBC_HIP_ERROR, "hipMalloc of column temporaries failed");
+    if (int e = stage_buffer(h, 2, std::max<int64_t>(nx, 1) * esz, &tx)) return e;
+    if (int e = stage_buffer(h, 3, std::max<int64_t>(ny, 1) * esz, &ty)) return e;
     for (int64_t r = 0; r < nrhs && st == VBC_OK; r++) {
         if (!copy2d(tx, esz, dX + r * esz, ldx * esz, esz, nx, hipMemcpyDeviceToDevice, s))
             st = fail(VBC_HIP_ERROR, "column gather failed");
@@ -1563,9 +1563,6 @@ static int mul_mat_device(vbc_handle *h, int trans, int64_t nrhs, const char *dX
         if (st == VBC_OK && !copy2d(dY + r * esz, ldy * esz, ty, esz, esz, ny, hipMemcpyDeviceToDevice, s))
             st = fail(VBC_HIP_ERROR, "column scatter failed");
     }
-    if (hipStreamSynchronize(s) != hipSuccess && st == VBC_OK) st = fail(VBC_HIP_ERROR, "sync failed");
-    if (tx) (void)hipFree(tx);
-    if (ty) (void)hipFree(ty);
     return st;
 }
 
@@ -1588,7 +1585,7 @@ int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, int64_t l
     if (!g.ok) return fail(VBC_HIP_ERROR, "hipSetDevice failed");
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(h->mu);  // the fused kernel's carry buffer and the staging buffers
-    ProductOrder po(h, s);
+    ProductOrder po(h, s, rowmajor);          // row-major per-column products share the column temporaries
     if (mem == VBC_MEM_DEVICE) {
         int st = po.begin();
         if (st == VBC_OK)

@@ -123,8 +123,8 @@ struct vbc_handle {
     //    previous one first waits for that one's completion event, so concurrent products on
     //    distinct streams stay correct.  Slotted / swept / panel layouts hold no scratch and skip it.
     std::mutex mu;
-    void *d_stage[2] = {nullptr, nullptr};  // x / X and y / Y staging (device)
-    size_t stage_bytes[2] = {0, 0};
+    void *d_stage[4] = {nullptr, nullptr, nullptr, nullptr};  // x / X, y / Y staging; 2, 3: column temporaries
+    size_t stage_bytes[4] = {0, 0, 0, 0};
     bool has_scratch = false;         // set at create: some launch of this handle uses carry slots
     hipEvent_t order_ev = nullptr;    // recorded after each product with scratch
     hipStream_t order_stream = nullptr;
