@@ -372,8 +372,17 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     int64_t rows = 0;
     for (int32_t c : cr) rows += c;
     const double target = planar ? (double)h->target_ranges_p : (double)h->target_ranges_s[kind];
-    int64_t nr = (int64_t)std::llround(target * (double)real / (double)std::max<int64_t>(total_entries, 1));
+    const double share = target * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    int64_t nr = (int64_t)std::llround(share);
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
+    // planar buckets with fewer chunks than wave slots: one chunk per workgroup of `split` waves
+    int split = 1;
+    if (planar && h->planar_split != 0) {
+        if (h->planar_split > 1) split = h->planar_split;
+        else
+            while (split < 8 && (double)nch * split * 2 <= share) split *= 2;
+    }
+    if (split > 1) nr = nch;
     bool affine = true;
     for (size_t q = 1; q < out.size() && affine; q++)
         affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * (out[1] - out[0]);
@@ -382,7 +391,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     for (int64_t c = 0; c < nch; c++) {
         acc += cr[c];
         // a table-mapped bin keeps <= kSlotOutEntries segments per range (their y offsets sit in LDS)
-        const bool full = !affine && (int64_t)(c + 2 - rchunk.back()) * RPI > kSlotOutEntries;
+        const bool full = split > 1 || (!affine && (int64_t)(c + 2 - rchunk.back()) * RPI > kSlotOutEntries);
         if (c + 1 < nch && (full || ((int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows))) {
             rrow.push_back((int32_t)acc);
             rchunk.push_back((int32_t)(c + 1));
@@ -405,6 +414,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.spl = slot_spl(h, kind, w);
     b.planar = planar ? 1 : 0;
     b.run = run;
+    b.split = split;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -1153,6 +1163,10 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
+    if (const char *e = getenv("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
+        const int v = atoi(e);
+        h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
+    }
     h->target_ranges_p = prop.multiProcessorCount * std::max(1, std::min(occupancy_planar(h->esz), 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) h->target_ranges_p = std::max(1, atoi(e));
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
@@ -1404,9 +1418,12 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     int32_t pl = h->has_t ? (int32_t)h->lt.pbins.size() : 0;
     info->planar_bins = pl;
     info->planar_run = 1;
+    info->planar_split = 1;
     if (h->has_t)
-        for (const auto &b : h->lt.pbins) info->planar_run = std::max<int32_t>(info->planar_run, b.run);
-    info->reserved_ = 0;
+        for (const auto &b : h->lt.pbins) {
+            info->planar_run = std::max<int32_t>(info->planar_run, b.run);
+            info->planar_split = std::max<int32_t>(info->planar_split, b.split);
+        }
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }

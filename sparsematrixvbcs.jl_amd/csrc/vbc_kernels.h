@@ -90,6 +90,9 @@ struct SlotBin {
     int32_t planar;      // 1: planar chunk rows (vbc_planar.h: one stripe per lane, column groups)
     int32_t run;         // planar: every segment's rows come in runs of `run` consecutive x rows (1 = none);
                          // keys / LAST are read from each run's first row, x gathered `run` elements wide
+    int32_t split;       // planar: > 1 = one chunk per workgroup of `split` waves, each folding a slice of
+                         // the chunk's rows, partials summed in LDS (small matrices: more waves in flight)
+    int32_t pad_;
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key

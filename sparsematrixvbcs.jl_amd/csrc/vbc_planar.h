@@ -256,4 +256,93 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
                                                                       lds_out);
 }
 
+// Split planar product (SlotBin::split = P > 1; ranges are single chunks): workgroup c = chunk c, wave k
+// folds the rows [R0 + k*S, R0 + (k+1)*S) of it (S a whole number of runs) in stored order, the P
+// partial accumulators meet in LDS and wave 0 writes y = alpha * (((p0 + p1) + p2) + ...) + beta * y.
+// For matrices with fewer chunks than the chip has wave slots (ct20stif: 273 chunks of ~48 rows),
+// where one wave per chunk leaves the product latency-bound.  Same keys, values and gathers as
+// run_planar; summation order is per slice, then across slices.
+template <typename T, int W_, bool KC, int RUN, int P>
+__global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin *__restrict__ bp, const T *__restrict__ x,
+                                                            T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const SlotBin b = *bp;
+    const int c = blockIdx.x;
+    if (c >= b.nranges) return;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int U = planar_step<T, W_, RUN>(), NR = U / RUN;
+    const int R0 = G(b.rrow)[c], R1 = G(b.rrow)[c + 1];
+    const int S = ((R1 - R0 + P - 1) / P + RUN - 1) / RUN * RUN;
+    const int a = __builtin_amdgcn_readfirstlane(min(R1, R0 + wv * S)), e = __builtin_amdgcn_readfirstlane(min(R1, a + S));
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> xg = G(x);
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;
+    const cptr bases = (cptr)b.base;
+    const cptr doffs = (cptr)b.kdoff;
+    constexpr uint32_t kPad16 = 0xFFFF8000u;
+    T acc[W_];
+#pragma unroll
+    for (int k = 0; k < W_; k++) acc[k] = T(0);
+    for (int R = a; R < e; R += U) {
+        uint32_t kk[NR], bs[NR];
+        T v[U][W_], xv[NR][RUN];
+#pragma unroll
+        for (int j = 0; j < NR; j++) {
+            const int Rk = min(R + j * RUN, e - RUN);
+            if constexpr (KC) {
+                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + lane];
+                bs[j] = bases[Rk];
+            } else {
+                kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
+                bs[j] = 0;
+            }
+#pragma unroll
+            for (int d = 0; d < RUN; d++) ld_row<T, W_, 0>(val + (size_t)min(R + j * RUN + d, e - 1) * 64 * W_, lane, v[j * RUN + d]);
+        }
+#pragma unroll
+        for (int j = 0; j < NR; j++) {
+            const uint32_t gi = KC ? (bs[j] & kSlotIdx) + (kk[j] == kPad16 ? 0u : kk[j]) : kk[j] & kSlotIdx;
+            ld_run<T, RUN>(xg + gi, xv[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NR; j++) {
+            const bool live = R + j * RUN < e;
+            const bool pad = KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0;
+#pragma unroll
+            for (int d = 0; d < RUN; d++) {
+                const T xe = pad ? T(0) : xv[j][d];
+#pragma unroll
+                for (int k = 0; k < W_; k++) {
+                    const T nv = fmadd(v[j * RUN + d][k], xe, acc[k]);
+                    acc[k] = live ? nv : acc[k];
+                }
+            }
+        }
+    }
+    __shared__ T part[P > 1 ? P - 1 : 1][64 * W_];
+    if (wv > 0) {
+#pragma unroll
+        for (int k = 0; k < W_; k++) part[wv - 1][k * 64 + lane] = acc[k];
+    }
+    __syncthreads();
+    if (wv != 0) return;
+#pragma unroll
+    for (int q = 0; q < P - 1; q++)
+#pragma unroll
+        for (int k = 0; k < W_; k++) acc[k] += part[q][k * 64 + lane];
+    const int seg = c * 64 + lane;
+    if (seg >= b.nseg) return;
+    const int o = b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
+    gptr<T> yo = G(y) + o;
+#pragma unroll
+    for (int k = 0; k < W_; k++) {
+        if (k < b.wst) {
+            T q = alpha * acc[k];
+            if (rd_i) q = fmadd(beta, yo[k], q);
+            yo[k] = q;
+        }
+    }
+}
+
 }  // namespace vbc

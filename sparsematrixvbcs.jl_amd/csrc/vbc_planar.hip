@@ -25,10 +25,36 @@ static void launch_w(const SlotBin &hb, const SlotBin *d_b, bool faste, bool sta
                            (T)alpha, (T)beta, (int)rd);
 }
 
+template <typename T, int W_, bool KC, int RUN>
+static void launch_split(const SlotBin &hb, const SlotBin *d_b, const void *x, void *y, double alpha, double beta,
+                         bool rd, hipStream_t s)
+{
+    const T *xs = static_cast<const T *>(x);
+    T *ys = static_cast<T *>(y);
+    const dim3 grid(hb.nranges);
+    switch (hb.split) {
+    case 2: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 2>), grid, dim3(128), 0, s, d_b, xs, ys, (T)alpha, (T)beta, (int)rd); break;
+    case 4: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 4>), grid, dim3(256), 0, s, d_b, xs, ys, (T)alpha, (T)beta, (int)rd); break;
+    default: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 8>), grid, dim3(512), 0, s, d_b, xs, ys, (T)alpha, (T)beta, (int)rd); break;
+    }
+}
+
 template <typename T, bool KC, int RUN>
 static int launch_r(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                     double alpha, double beta, bool rd, hipStream_t s)
 {
+    if (hb.split > 1) {
+        switch (hb.wkey) {
+        case 3: launch_split<T, 3, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        case 4: launch_split<T, 4, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        case 5: launch_split<T, 5, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        case 6: launch_split<T, 6, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        case 7: launch_split<T, 7, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        case 8: launch_split<T, 8, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        default: return (int)hipErrorInvalidValue;
+        }
+        return (int)hipGetLastError();
+    }
     switch (hb.wkey) {
     case 3: launch_w<T, 3, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;
     case 4: launch_w<T, 4, KC, RUN>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s); break;

@@ -73,6 +73,7 @@ def test_fe3d_planar_matches_oracle_bitwise(monkeypatch, stage):
     """The irregular 3D stiffness operator (w = 3): planar result equals the oracle bit for bit
     (same per-lane FMA order as multiply_1DVBC.jl:101-104), staged and direct y writes."""
     monkeypatch.setenv("VBC_SLOT_STAGE", stage)
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")  # one wave per chunk: the reference's summation order
     B = V.synthetic.fe_stiffness_3d_1dvbc(300000, 3_000_000)
     assert planar_bins(B) == 1
     rng = np.random.default_rng(3)
@@ -83,8 +84,9 @@ def test_fe3d_planar_matches_oracle_bitwise(monkeypatch, stage):
     assert np.array_equal(y.cpu().numpy(), ref)
 
 
-def test_planar_nonfinite_x():
+def test_planar_nonfinite_x(monkeypatch):
     """Inf / NaN in x land exactly where the reference puts them (padding rows take x as 0)."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
     B = V.synthetic.fe_stiffness_3d_1dvbc(30000, 300000)
     rng = np.random.default_rng(5)
     x = rng.uniform(-1, 1, B.m)
@@ -152,6 +154,7 @@ def test_row_runs(monkeypatch, dtype, R, w):
         monkeypatch.setenv("VBC_SLOT_RUNS", runs)
         monkeypatch.setenv("VBC_SLOT_PLANAR", "1")
         monkeypatch.setenv("VBC_SLOTS", "1")
+        monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
         Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)  # fresh handle cache
         inf = Bc.info(trans=True)
         assert inf["planar_bins"] == 1 and inf["planar_run"] == (R if runs == "1" else 1)
@@ -174,6 +177,7 @@ def test_row_runs_fallback(monkeypatch):
     """One stripe whose first two rows repeat an x row: not runs -> the bucket keeps run = 1."""
     monkeypatch.setenv("VBC_SLOT_PLANAR", "1")
     monkeypatch.setenv("VBC_SLOTS", "1")
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
     base = V.synthetic.vbr_1dvbc(5000, 2000, 12000, 3, W=8, seed=3)
     B = expand_runs(base, 3, seed=4, break_one=True)
     assert B.info(trans=True)["planar_run"] == 1
@@ -189,3 +193,55 @@ def test_fe3d_uses_runs():
     B = V.synthetic.fe_stiffness_3d_1dvbc(30000, 300000)
     inf = B.info(trans=True)
     assert inf["planar_bins"] == 1 and inf["planar_run"] == 3
+
+
+@pytest.mark.parametrize("P", ["2", "4", "8"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w,R", [(3, 3), (5, 1), (8, 2), (4, 1)])
+def test_split_chunks(monkeypatch, P, dtype, w, R):
+    """Split planar product (SlotBin::split): P waves per chunk, partials summed in LDS.  Random x
+    within tolerance of the oracle (normwise, 1e-12 fp64 / 1e-5 fp32), alpha / beta, affine (natural
+    order) and table-mapped (sorted) outputs; integer-valued data bit for bit."""
+    if dtype == np.float32 and w == 4:
+        pytest.skip("fp32 w = 4 is not planar")
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", P)
+    monkeypatch.setenv("VBC_SLOTS", "1")
+    rng = np.random.default_rng(int(P) * 100 + w)
+    for sort in ("0", "2"):
+        monkeypatch.setenv("VBC_SLOTS_SORT", sort)
+        base = V.synthetic.vbr_1dvbc(4000, 700, 30000, w, W=8, dtype=dtype, seed=w + int(P))
+        B = expand_runs(base, R, seed=w) if R > 1 else base
+        inf = B.info(trans=True)
+        assert inf["planar_bins"] == 1 and inf["planar_split"] == int(P) and inf["planar_run"] == R
+        R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+        x = rng.uniform(-1, 1, B.m).astype(dtype)
+        y0 = rng.uniform(-1, 1, B.n).astype(dtype)
+        tol = TOL64 if dtype == np.float64 else TOL32
+        for alpha, beta in ((1.0, 0.0), (-0.5, 3.0)):
+            y = dev(y0.copy())
+            V.mul_(y, B.T, dev(x), alpha, beta)
+            ref = O.mul(R64, x.astype(np.float64), y0.astype(np.float64), alpha, beta, trans=True, ref_semantics=False)
+            assert rel(y.cpu().numpy(), ref) <= tol, (sort, alpha)
+        # integer-valued: every partial sum exact, so any summation order gives the oracle's bits
+        Bi = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs,
+                                 rng.integers(-50, 50, len(B.val)).astype(dtype))
+        xi = rng.integers(-20, 20, B.m).astype(dtype)
+        y = torch.zeros(B.n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+        V.mul_(y, Bi.T, dev(xi))
+        refi = O.mul(O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, Bi.val.astype(np.float64)),
+                     xi.astype(np.float64), np.zeros(B.n), trans=True)
+        assert np.array_equal(y.cpu().numpy().astype(np.float64), refi)
+        B.release()
+        Bi.release()
+
+
+def test_split_auto_small_matrix():
+    """The ct20stif stand-in (17443 3-dof stripes, 273 planar chunks) picks the split product."""
+    import bench
+    B = bench.build_matrix("ct20stif", np.float64)
+    inf = B.info(trans=True)
+    assert inf["planar_bins"] >= 1 and inf["planar_split"] > 1
+    x = np.random.default_rng(1).uniform(-1, 1, B.m)
+    y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert rel(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(B.n), trans=True)) <= TOL64
