@@ -1378,6 +1378,55 @@ int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t *colptr
         if (rowval[p] < 1 || rowval[p] > m) return fail(VBC_INVALID_ARG, "rowval out of range 1:m");
         s.rows[p] = (int32_t)(rowval[p] - 1);
     }
+    // Column blocking: runs of up to 8 consecutive columns with identical row patterns (the dof
+    // columns of a node in a stiffness matrix) become one w-wide stripe, so TrSpMV! runs the blocked
+    // kernels (planar with row runs for 3-dof operators).  Each output y[j] still sums its column in
+    // stored row order (TrSpMV.jl:10-16), so the result is that of the unit-width layout, bit for bit.
+    // VBC_CSC_BLOCK=0 keeps unit stripes.
+    const char *eb = getenv("VBC_CSC_BLOCK");
+    if (!(eb && atoi(eb) == 0) && n > 1 && (dtype == VBC_F64 || dtype == VBC_F32 || dtype == VBC_I64)) {
+        std::vector<int64_t> g0;  // first column of each group
+        for (int64_t j = 0; j < n;) {
+            int64_t e = j + 1;
+            const int64_t len = colptr[j + 1] - colptr[j];
+            while (e < n && e - j < 8 && colptr[e + 1] - colptr[e] == len &&
+                   std::equal(rowval + colptr[j] - 1, rowval + colptr[j + 1] - 1, rowval + colptr[e] - 1))
+                e++;
+            g0.push_back(j);
+            j = e;
+        }
+        if ((int64_t)g0.size() < n) {
+            const int64_t L = (int64_t)g0.size();
+            const int esz = elem_size(dtype);
+            Stripes b;
+            b.m = m; b.n = n; b.L = L;
+            b.col0.resize(L); b.w.resize(L); b.rbeg.resize(L + 1); b.voff.resize(L);
+            std::vector<char> bv((size_t)std::max<int64_t>(nnz, 1) * esz);
+            const char *src = static_cast<const char *>(nzval);
+            int64_t q = 0;
+            for (int64_t l = 0; l < L; l++) {
+                const int64_t j = g0[l], w = (l + 1 < L ? g0[l + 1] : n) - j, R = colptr[j + 1] - colptr[j];
+                b.col0[l] = j;
+                b.w[l] = (int32_t)w;
+                b.rbeg[l] = q;
+                q += R;
+            }
+            b.rbeg[L] = q;
+            b.rows.resize(q);
+            int64_t v = 0;
+            for (int64_t l = 0; l < L; l++) {
+                const int64_t j = g0[l], w = b.w[l], R = colptr[j + 1] - colptr[j];
+                b.voff[l] = v;
+                for (int64_t r = 0; r < R; r++) {
+                    b.rows[b.rbeg[l] + r] = (int32_t)(rowval[colptr[j] - 1 + r] - 1);
+                    for (int64_t c = 0; c < w; c++)
+                        std::memcpy(bv.data() + (v + r * w + c) * esz, src + (colptr[j + c] - 1 + r) * esz, (size_t)esz);
+                }
+                v += R * w;
+            }
+            return create_common(out, b, bv.data(), dtype, device, flags, nnz, 0, q);
+        }
+    }
     return create_common(out, s, nzval, dtype, device, flags, nnz, 0, nnz);
 }
 

@@ -183,3 +183,47 @@ def test_north_star_full_size_vs_oracle(workload):
     ref_f = O.mul(R, xf, np.zeros(B.m))
     assert rel(yf.cpu().numpy(), ref_f) <= 1e-10
     B.release()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("ragged", [False, True])
+def test_trspmv_column_blocking(monkeypatch, dtype, ragged):
+    """vbc_csc_create groups consecutive columns with identical row patterns (a node's dof columns)
+    into one stripe.  Each y[j] still sums its column in stored row order (TrSpMV.jl:10-16): on the
+    3-dof operator every bucket is slotted / planar and TrSpMV! equals the unit-stripe layout bit for
+    bit; with a few triples broken (ragged: 1- and 2-wide groups, whose small buckets may take the
+    merge layout) it matches within tolerance.  Forward product on the blocked handle too."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")  # one wave per chunk: per-column serial order
+    A = V.synthetic.fe_stiffness_3d(90000, 2_000_000, 3, dtype).tocsc()
+    if ragged:
+        D = A.tolil()
+        D[5, 7] = 1.5
+        D[11, 300] = -2.0
+        A = D.tocsc().astype(dtype)
+    A.sort_indices()
+    m, n = A.shape
+    rng = np.random.default_rng(23)
+    x = rng.uniform(-1, 1, m).astype(dtype)
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    tol = 1e-12 if dtype == np.float64 else 1e-5
+    outs = {}
+    for blk in ("1", "0"):
+        monkeypatch.setenv("VBC_CSC_BLOCK", blk)
+        C = V.SparseMatrixCSC(A)
+        y = torch.full((n,), float("nan"), dtype=tdt, device=DEV)
+        V.TrSpMV_(y, C, dev(x))
+        outs[blk] = y.cpu().numpy()
+        assert (C.info(trans=True)["L"] < n) == (blk == "1")
+        C.release()
+    exact = O.trspmv(A.astype(np.float64), x.astype(np.float64), np.zeros(n), nthreads=threads())
+    assert rel(outs["1"], exact) <= tol
+    if ragged:
+        assert rel(outs["1"], outs["0"]) <= tol
+    else:
+        assert np.array_equal(outs["1"], outs["0"])
+    monkeypatch.setenv("VBC_CSC_BLOCK", "1")
+    C = V.SparseMatrixCSC(A)
+    xf = rng.uniform(-1, 1, n).astype(dtype)
+    yf = torch.zeros(m, dtype=tdt, device=DEV)
+    V.mul_(yf, C, dev(xf))
+    assert rel(yf.cpu().numpy(), A.astype(np.float64) @ xf.astype(np.float64)) <= tol
