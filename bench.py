@@ -45,12 +45,17 @@ WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
              "fe3d": "FE-3D-stiffness-dof3-1e7x1e7-1e8nnz-w3 (irregular: random 18-neighbour subsets)",
              "c5": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS (costs.jl:200-220 generator)",
              "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
-             "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)"}
+             "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)",
+             "ldoor-csc": "C4 TrSpMV!(y, A, x) on the GHS_psdef/ldoor stand-in (CSC, 952203^2, 42.5M nnz)"}
 
 
 def algorithmic_bytes(B, esz, ti=4, nrhs=1):
     """SURVEY.md §8d, transposed: Tv·|val| + Ti·q + Ti·(3L+3) + Tx·m + Ty·n; 2D adds Ti·(K+1);
-    k right-hand sides multiply the x and y terms by k."""
+    k right-hand sides multiply the x and y terms by k.  CSC (TrSpMV!): Tv·nnz + Ti·nnz + Ti·(n+1)
+    + Tx·m + Ty·n."""
+    if not hasattr(B, "ofs"):  # SparseMatrixCSC
+        A = B.A
+        return (esz + ti) * int(A.nnz) + ti * (A.shape[1] + 1) + esz * (A.shape[0] + A.shape[1])
     nval = int(B.ofs[-1] - 1)
     q = int(B.pos[-1] - 1)
     L = len(B.Phi)
@@ -79,12 +84,16 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
         return V.synthetic.fe_stiffness_3d_1dvbc(n, int(round(1e8 * scale)), 3, dtype=dtype, seed=seed)
     if workload == "c5":
         return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
-    if workload in ("ldoor", "ct20stif"):
-        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif"}[workload]
+    if workload in ("ldoor", "ct20stif", "ldoor-csc"):
+        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ldoor-csc": "GHS_psdef/ldoor"}[workload]
         try:
             A = V.io.mdopen(name, dtype=dtype).A
         except FileNotFoundError:
             A = V.synthetic.standin(name, dtype=dtype, seed=seed)
+        if workload == "ldoor-csc":  # TrSpMV!(y, A, x) = A'x on the CSC itself (TrSpMV.jl:1-20)
+            C = V.SparseMatrixCSC(A.tocsc())
+            C.A = A.tocsc()  # the scipy operand, for the byte count and the oracle
+            return C
         # bin/test_table.jl:27 stores A = permutedims(A): B'x multiplies the original matrix
         return V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
     return V.synthetic.north_star(dtype=dtype, scale=scale, seed=seed, mixed=(workload == "ns-mixed"))
@@ -95,7 +104,11 @@ def kernel_name(B, local, k):
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     inf = B.info(local, True)
     if inf["planar_bins"] > 0:
-        return "vbc::spmv_planar<T, W, FASTE, NB, KC> (planar slotted chunks, csrc/vbc_planar.h)"
+        if inf["planar_split"] > 1:
+            return (f"vbc::spmv_planar_split<T, W, KC, RUN={inf['planar_run']}, P={inf['planar_split']}> "
+                    "(split planar chunks, csrc/vbc_planar.h)")
+        return (f"vbc::spmv_planar<T, W, FASTE, NB, KC, RUN={inf['planar_run']}> "
+                "(planar slotted chunks, csrc/vbc_planar.h)")
     if inf["sweep_bins"] > 0:
         return "vbc::spmv_sweep<T, TB> (row-swept tiles, csrc/vbc_sweep.hip)"
     if inf["slot_bins"] > 0:
@@ -147,6 +160,15 @@ def parity(B, x_host, y_dev, k=1, cols=(0,)):
     from oracle import oracle as O
     from oracle import simd as S
     th = S.host_threads()
+    if not hasattr(B, "ofs"):  # TrSpMV! on a CSC: orc_trspmv (TrSpMV.jl:1-20)
+        t0 = time.perf_counter()
+        ref = O.trspmv(B.A, x_host, np.zeros(B.n, B.A.dtype), nthreads=th)
+        g = y_dev.cpu().numpy()
+        err = float(np.linalg.norm(g.astype(np.float64) - ref) / max(np.linalg.norm(ref), 1e-300))
+        tol = PARITY_TOL[np.dtype(B.A.dtype)]
+        return {"rel_err": float(f"{err:.3e}"), "tol": tol, "pass": bool(err <= tol),
+                "bitwise_equal": bool(np.array_equal(g, ref)), "oracle": "oracle/vbc_oracle.c orc_trspmv (TrSpMV.jl:1-20)",
+                "columns": None, "oracle_s": round(time.perf_counter() - t0, 2)}
     if hasattr(B, "Pi"):
         R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
     else:
@@ -214,23 +236,29 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     esz = np.dtype(dtype).itemsize
     t_build = time.perf_counter()
     B = build_matrix(workload, dtype, args.scale)
+    csc = not hasattr(B, "ofs")
     rng = np.random.default_rng(0xC0FFEE)
     k = args.nrhs if workload == "c5" else 1
     x_host = rng.uniform(-1, 1, (B.m, k) if k > 1 else B.m).astype(dtype)
     x = torch.from_numpy(x_host).to(device)  # k > 1: row-major X (right-hand sides interleaved)
     y = torch.empty((B.n, k) if k > 1 else B.n, dtype=x.dtype, device=device)
     Bt = B.T
+
+    def step():
+        if csc:
+            V.TrSpMV_(y, B, x)
+        else:
+            V.mul_(y, Bt, x)
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
         B.handle(local, True, multi=k > 1)  # build the HBM layout outside the timed region
         t_build = time.perf_counter() - t_build
         for _ in range(args.warmup):
-            V.mul_(y, Bt, x)
+            step()
     torch.cuda.synchronize(device)
-    elapsed, kernel_ms, graphed = timed_products(lambda: V.mul_(y, Bt, x), steps, device, stream, 1,
-                                                 graph=not args.eager)
+    elapsed, kernel_ms, graphed = timed_products(step, steps, device, stream, 1, graph=not args.eager)
     bytes_launch = algorithmic_bytes(B, esz, nrhs=k)
-    nnz = int(np.count_nonzero(B.val))
+    nnz = int(B.A.nnz) if csc else int(np.count_nonzero(B.val))
     ms_per_step = elapsed / steps * 1e3
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload, "f64" if dtype == np.float64 else "f32")
@@ -246,10 +274,12 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
         },
         "config": {
             "workload": WORKLOADS[workload] + (f"-scale{args.scale}" if args.scale != 1.0 else ""),
-            "op": ("mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if k == 1 else
+            "op": ("TrSpMV!(y, A, x) -- CSC transposed product (TrSpMV.jl:1-20)" if csc else
+                   "mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if k == 1 else
                    f"Y = B'X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:89-192 per column), "
                    "matrix-core panel kernel"),
-            "m": B.m, "n": B.n, "stripes": len(B.Phi), "row_blocks": int(B.pos[-1] - 1), "nnz": nnz, "W": B.W,
+            "m": B.m, "n": B.n, "stripes": B.n if csc else len(B.Phi),
+            "row_blocks": nnz if csc else int(B.pos[-1] - 1), "nnz": nnz, "W": 1 if csc else B.W,
             "index_bytes": 4, "nrhs": k, "launch": "hipGraph of K products" if graphed else "eager",
             "build_s": round(t_build, 1),
         },
@@ -409,7 +439,8 @@ def main():
             out["rel_err"] = p["parity"]["rel_err"]
         if not args.no_secondary:
             sec = {}
-            for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32)):
+            for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("ct20stif", np.float64),
+                           ("ldoor", np.float64), ("ldoor-csc", np.float32)):
                 if wl == args.workload:
                     continue
                 s = measure(args, wl, dt, device, local, with_cpu=False, with_parity=not args.no_parity)

@@ -19,7 +19,7 @@ case "$step" in
   bench) timeout -k 10 900 python -u bench.py "$@" > gpurun_out/${tag}_bench.log 2>&1; rc=$?
          tail -c 3000 gpurun_out/${tag}_bench.log; exit $rc ;;
   prof)  rm -rf gpurun_out/${tag}_prof
-         timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run -- python -u bench.py "$@" \
+         timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof -o run -- python -u bench.py "$@" \
            > gpurun_out/${tag}_prof.log 2>&1; rc=$?; tail -c 2000 gpurun_out/${tag}_prof.log; exit $rc ;;
   ab)    timeout -k 10 900 python -u tools/ab.py "$@" > gpurun_out/${tag}_ab.log 2>&1; rc=$?
          tail -40 gpurun_out/${tag}_ab.log; exit $rc ;;
