@@ -227,10 +227,11 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
 }
 
 // Rows per pipeline step: about 24 values per lane per stage (fp64 w = 3: 8 rows), whole runs.
-// Values per lane per stage: fp64 24 (36 / 48 measured the same on ldoor and fe3d), fp32 36 (ldoor
-// stand-in 49.5 -> 44.7 us against 24; 48 the same).  A/B builds: -DVBC_PLANAR_VALS=...
+// Values per lane per stage: fp64 24 (36 / 48 measured the same on ldoor and fe3d), fp32 with row
+// runs 36 (ldoor stand-in 49.5 -> 44.7 us against 24; 48 the same; without runs 36 spills SGPRs:
+// one scalar base per row).  A/B builds: -DVBC_PLANAR_VALS=...
 #ifndef VBC_PLANAR_VALS
-#define VBC_PLANAR_VALS (sizeof(T) == 8 ? 24 : 36)
+#define VBC_PLANAR_VALS (sizeof(T) == 8 || RUN == 1 ? 24 : 36)
 #endif
 template <typename T, int W_, int RUN>
 __host__ __device__ constexpr int planar_step()
