@@ -45,12 +45,13 @@ def main():
     ap.add_argument("--extra", default="")
     ap.add_argument("--counters", default="", help="extra counter passes, ';'-separated groups")
     ap.add_argument("--kernel", default=KERNEL, help="kernel name substring to attribute counters to")
+    ap.add_argument("--tag", default="", help="suffix of the output file name (ablation runs)")
     ap.add_argument("--read-factor", type=float, default=2.0,
                     help="FETCH_SIZE correction: 2 for 16-B/lane streaming reads (gfx950 half-count), 1 for "
                          "dword loads and gathers")
     args = ap.parse_args()
     out = ROOT / "gpurun_out" / "pmc"
-    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--workload", args.workload,
+    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--no-parity", "--workload", args.workload,
                   "--dtype", args.dtype] + args.extra.split()
     res = {}
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"]] + [g.split(",") for g in args.counters.split(";") if g]
@@ -76,7 +77,18 @@ def main():
         "raw_bytes_per_launch": int(fetch_kb * 1024 + write_kb * 1024),
         "counters": res,
     }
-    p = ROOT / "profiles" / f"pmc_{args.workload}_{args.dtype}.json"
+    if "TCC_EA0_RDREQ_sum" in res:
+        rq = res["TCC_EA0_RDREQ_sum"]["mean"]
+        bub = res.get("TCC_BUBBLE_sum", {}).get("mean", 0.0)
+        r32 = res.get("TCC_EA0_RDREQ_32B_sum", {}).get("mean", 0.0)
+        summary["rdreq_per_launch"] = {"all": rq, "bubble_128B": bub, "32B": r32,
+                                       "dram": res.get("TCC_EA0_RDREQ_DRAM_sum", {}).get("mean")}
+    if "TCC_HIT_sum" in res and "TCC_MISS_sum" in res:
+        h, m = res["TCC_HIT_sum"]["mean"], res["TCC_MISS_sum"]["mean"]
+        summary["l2_hit_rate"] = h / max(h + m, 1.0)
+    if os.environ.get("VBC_PANEL_DIAG") or os.environ.get("VBC_DIAG"):
+        summary["ablation_env"] = {k: v for k, v in os.environ.items() if k.startswith("VBC_")}
+    p = ROOT / "profiles" / f"pmc_{args.workload}_{args.dtype}{args.tag}.json"
     p.write_text(json.dumps(summary, indent=1) + "\n")
     (ROOT / "gpurun_out" / p.name).write_text(json.dumps(summary, indent=1) + "\n")
     print(json.dumps(summary, indent=1))
