@@ -304,7 +304,8 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
 
     esz = np.dtype(dtype).itemsize
     B = build_matrix(workload, dtype, args.scale)  # same seed on every rank: one matrix
-    S = V.distributed.ShardedSparseMatrix1DVBC(B, rank, world, split="stripes")
+    S = V.distributed.ShardedSparseMatrix1DVBC(B, rank, world, split="stripes",
+                                               comm="cpu" if args.backend == "gloo" else "device")
     bytes_total = algorithmic_bytes(B, esz)
     bytes_local = algorithmic_bytes(S.local, esz)
     nnz_total = int(np.count_nonzero(B.val[:B.ofs[-1] - 1]))
@@ -359,7 +360,8 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
         dist.barrier()
         fwd = fwd_elapsed
 
-    stats = torch.tensor([elapsed, kernel_ms, e2e_elapsed, fwd or 0.0], dtype=torch.float64, device=device)
+    stats = torch.tensor([elapsed, kernel_ms, e2e_elapsed, fwd or 0.0], dtype=torch.float64,
+                         device=device if args.backend == "nccl" else "cpu")
     mx = stats.clone()
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     mn = stats.clone()
@@ -409,6 +411,11 @@ def main():
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of one graph replay")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 process group: nccl = RCCL over xGMI (the measurement); gloo = rehearsal of the "
+                         "multi-rank code path with host-side collectives")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank on cuda:0 (a one-GPU box; needs --backend gloo)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary workloads")
@@ -422,6 +429,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.same_device:
+        if args.backend != "gloo":
+            raise SystemExit("--same-device needs --backend gloo (RCCL refuses two ranks on one GPU)")
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dtype = np.float64 if args.dtype == "f64" else np.float32
@@ -454,7 +465,10 @@ def main():
                     sec[wl]["parity_pass"] = s["parity"]["pass"]
             out["secondary"] = sec
     else:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
         p = measure_sharded(args, args.workload, dtype, world, rank, local, device)
         out = dict(head, value=p["value"], unit=p["unit"], ms_per_step=p["ms_per_step"], scaling="strong",
                    dtype=p["dtype"], config=p["config"], gflops=p["gflops"], roofline=p["roofline"], e2e=p["e2e"],
