@@ -2,14 +2,18 @@
 //
 // The builders produce the exact field arrays of the reference's constructors
 // (constructors_1DVBC.jl:9-92, constructors_VBC.jl:15-133) but by a different algorithm: instead of
-// the reference's w-way column merge, each stripe's distinct rows (or block rows) are collected with
-// a stamp array, sorted, given slots, and the stripe's entries are scattered into their slots.  The
-// oracle (oracle/vbc_oracle.c) restates the merge line by line; tests require both to agree
-// exactly, which pins this implementation.
+// the reference's w-way column merge, each stripe's distinct rows (or block rows) are collected,
+// sorted and deduplicated, given slots, and the stripe's entries are placed by a merge walk of each
+// (sorted) column against the slots.  1DVBC stripes are independent, so count and fill run over
+// stripe ranges on host threads (VBC_HOST_THREADS, default min(hardware threads, 16)).  The oracle
+// (oracle/vbc_oracle.c) restates the merge line by line; tests require both to agree exactly, which
+// pins this implementation.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <thread>
 #include <vector>
 
 #include "vbc_host.h"
@@ -19,20 +23,54 @@ using vbc::fail;
 
 namespace {
 
+// Host threads for the builders: VBC_HOST_THREADS, else min(hardware threads, 16).
+int host_threads()
+{
+    if (const char *e = std::getenv("VBC_HOST_THREADS")) return std::max(1, std::atoi(e));
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
+}
+
+// f(lo, hi, status&) over [0, n) in contiguous chunks on host threads; the first nonzero status wins.
+template <typename F>
+int parallel_ranges(int64_t n, int64_t work, F f)
+{
+    const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, work / 200000));
+    if (nt <= 1 || n < 2 * nt) {
+        int st = VBC_OK;
+        f((int64_t)0, n, st);
+        return st;
+    }
+    std::vector<int> sts(nt, VBC_OK);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt, sts[t]); });
+    for (auto &x : th) x.join();
+    for (int st : sts)
+        if (st) return st;
+    return VBC_OK;
+}
+
+
 int check_csc(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval)
 {
     if (m < 0 || n < 0) return fail(VBC_INVALID_ARG, "number of rows/columns must be >= 0");
     if (!colptr) return fail(VBC_INVALID_ARG, "colptr is NULL");
     if (colptr[0] != 1) return fail(VBC_INVALID_ARG, "colptr[1] must be 1");
-    for (int64_t j = 0; j < n; j++) {
+    for (int64_t j = 0; j < n; j++)
         if (colptr[j + 1] < colptr[j]) return fail(VBC_INVALID_ARG, "colptr must be non-decreasing");
-        for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
-            const int64_t i = rowval[p];
-            if (i < 1 || i > m) return fail(VBC_INVALID_ARG, "rowval out of range 1:m");
-            if (p > colptr[j] - 1 && rowval[p - 1] >= i)
-                return fail(VBC_INVALID_ARG, "rowval must be strictly increasing within a column");
-        }
-    }
+    if (colptr[n] > 1 && !rowval) return fail(VBC_INVALID_ARG, "rowval is NULL");
+    // 1: a row index out of 1:m, 2: rows not strictly increasing within a column (worst of all columns)
+    const int bad = parallel_ranges(n, colptr[n] - 1, [&](int64_t j0, int64_t j1, int &st) {
+        for (int64_t j = j0; j < j1; j++)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t i = rowval[p];
+                if (i < 1 || i > m) st = std::max(st, 1);
+                else if (p > colptr[j] - 1 && rowval[p - 1] >= i) st = std::max(st, 2);
+            }
+    });
+    if (bad == 1) return fail(VBC_INVALID_ARG, "rowval out of range 1:m");
+    if (bad) return fail(VBC_INVALID_ARG, "rowval must be strictly increasing within a column");
     return VBC_OK;
 }
 
@@ -48,36 +86,67 @@ int check_spl(int64_t n, int64_t L, const int64_t *spl, int64_t W, bool assert_w
     return VBC_OK;
 }
 
+// Sorted distinct 0-based rows of columns [j0, j1) (each column's rows ascending): a merge of the
+// sorted columns with duplicates dropped; columns whose pattern equals the first's (every column of a
+// StrictChunker stripe) are skipped.
+inline void stripe_rows(const int64_t *colptr, const int64_t *rowval, int64_t j0, int64_t j1,
+                        std::vector<int64_t> &rows, std::vector<int64_t> &tmp)
+{
+    rows.clear();
+    const int64_t *a = rowval + colptr[j0] - 1;
+    const int64_t na = colptr[j0 + 1] - colptr[j0];
+    for (int64_t p = 0; p < na; p++) rows.push_back(a[p] - 1);
+    for (int64_t j = j0 + 1; j < j1; j++) {
+        const int64_t *b = rowval + colptr[j] - 1;
+        const int64_t nb = colptr[j + 1] - colptr[j];
+        if (nb == na && std::equal(a, a + na, b)) continue;
+        tmp.clear();
+        size_t s = 0;
+        for (int64_t p = 0; p < nb; p++) {
+            const int64_t i = b[p] - 1;
+            while (s < rows.size() && rows[s] < i) tmp.push_back(rows[s++]);
+            if (s < rows.size() && rows[s] == i) s++;
+            tmp.push_back(i);
+        }
+        while (s < rows.size()) tmp.push_back(rows[s++]);
+        rows.swap(tmp);
+    }
+}
+
 template <typename T>
 int fill_1d(int64_t m, int64_t W, const int64_t *colptr, const int64_t *rowval, const T *nzval,
             int64_t L, const int64_t *spl, const int64_t *pos, const int64_t *ofs, int64_t *idx,
             T *val, int64_t pad)
 {
-    std::vector<int64_t> stamp(m, 0), slot(m, 0), rows;
+    (void)m;
     const int64_t nv = ofs[L] - 1;
-    std::fill(val, val + nv + pad, T(0));
-    for (int64_t l = 0; l < L; l++) {
-        const int64_t j0 = spl[l] - 1, j1 = spl[l + 1] - 1, w = j1 - j0;
-        if (w > W) return fail(VBC_ASSERTION, "AssertionError: w <= W");
-        rows.clear();
-        for (int64_t j = j0; j < j1; j++)
-            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
-                const int64_t i = rowval[p] - 1;
-                if (stamp[i] != l + 1) { stamp[i] = l + 1; rows.push_back(i); }
+    std::fill(val + nv, val + nv + pad, T(0));
+    for (int64_t l = 0; l < L; l++)
+        if (spl[l + 1] - spl[l] > W) return fail(VBC_ASSERTION, "AssertionError: w <= W");
+    const int status = parallel_ranges(L, colptr[spl[L] - 1] - 1, [&](int64_t l0, int64_t l1, int &st) {
+        std::vector<int64_t> rows, tmp;
+        for (int64_t l = l0; l < l1 && st == VBC_OK; l++) {
+            const int64_t j0 = spl[l] - 1, j1 = spl[l + 1] - 1, w = j1 - j0;
+            stripe_rows(colptr, rowval, j0, j1, rows, tmp);
+            if ((int64_t)rows.size() != pos[l + 1] - pos[l]) {
+                st = VBC_INVALID_ARG;
+                continue;
             }
-        std::sort(rows.begin(), rows.end());
-        if ((int64_t)rows.size() != pos[l + 1] - pos[l])
-            return fail(VBC_INVALID_ARG, "pos inconsistent with A and spl");
-        for (size_t s = 0; s < rows.size(); s++) {
-            slot[rows[s]] = (int64_t)s;
-            idx[pos[l] - 1 + (int64_t)s] = rows[s] + 1;
+            for (size_t s = 0; s < rows.size(); s++) idx[pos[l] - 1 + (int64_t)s] = rows[s] + 1;
+            T *seg = val + (ofs[l] - 1);
+            std::fill(seg, seg + (int64_t)rows.size() * w, T(0));
+            for (int64_t j = j0; j < j1; j++) {  // merge walk: the column's rows against the slots
+                size_t s = 0;
+                for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                    const int64_t i = rowval[p] - 1;
+                    while (rows[s] != i) s++;
+                    seg[(int64_t)s * w + (j - j0)] = nzval[p];
+                }
+            }
         }
-        T *seg = val + (ofs[l] - 1);
-        for (int64_t j = j0; j < j1; j++)
-            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++)
-                seg[slot[rowval[p] - 1] * w + (j - j0)] = nzval[p];
-    }
-    return VBC_OK;
+    });
+    // the message is set here: the last-error string is per thread
+    return status ? fail(status, "pos inconsistent with A and spl") : VBC_OK;
 }
 
 template <typename T>
@@ -250,16 +319,19 @@ int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t 
 {
     if (int st = check_csc(m, n, colptr, rowval)) return st;
     if (int st = check_spl(n, L, spl, 0, false)) return st;
-    std::vector<int64_t> stamp(m, 0);
+    // distinct rows per stripe (pos / ofs hold the counts until the prefix sum)
+    int st = parallel_ranges(L, colptr[n] - 1, [&](int64_t l0, int64_t l1, int &) {
+        std::vector<int64_t> rows, tmp;
+        for (int64_t l = l0; l < l1; l++) {
+            stripe_rows(colptr, rowval, spl[l] - 1, spl[l + 1] - 1, rows, tmp);
+            pos[l + 1] = (int64_t)rows.size();
+        }
+    });
+    if (st) return st;
     pos[0] = 1;
     ofs[0] = 1;
     for (int64_t l = 0; l < L; l++) {
-        int64_t rows = 0;
-        for (int64_t j = spl[l] - 1; j < spl[l + 1] - 1; j++)
-            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
-                const int64_t i = rowval[p] - 1;
-                if (stamp[i] != l + 1) { stamp[i] = l + 1; rows++; }
-            }
+        const int64_t rows = pos[l + 1];
         pos[l + 1] = pos[l] + rows;
         ofs[l + 1] = ofs[l] + rows * (spl[l + 1] - spl[l]);
     }

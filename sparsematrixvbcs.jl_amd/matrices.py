@@ -34,13 +34,10 @@ def _value_dtype(A):
 
 
 def _csc_fields(A):
-    A = sp.csc_matrix(A)
-    A.sum_duplicates()
-    A.sort_indices()
-    colptr = np.ascontiguousarray(A.indptr, dtype=np.int64) + 1
-    rowval = np.ascontiguousarray(A.indices, dtype=np.int64) + 1
-    nzval = np.ascontiguousarray(A.data, dtype=_value_dtype(A))
-    return A.shape, colptr, rowval, nzval
+    from .partition import CSCFields
+    F = A if isinstance(A, CSCFields) else CSCFields(A)
+    nzval = np.ascontiguousarray(F.A.data, dtype=_value_dtype(F.A))
+    return F.shape, F.colptr, F.rowval, nzval
 
 
 class _Handles:
@@ -153,6 +150,8 @@ class SparseMatrix1DVBC(_DeviceMatrix):
     def from_csc(cls, W, A, method=None, dtype=None):
         if method is None:
             method = DynamicTotalChunker(model_SparseMatrix1DVBC_memory(np.float64, np.int64), W)
+        from .partition import CSCFields
+        A = CSCFields(A)  # one conversion for the partitioner and the builder
         Phi = method if isinstance(method, SplitPartition) else pack_stripe(A, method)
         (m, n), colptr, rowval, nzval = _csc_fields(A)
         if dtype is not None:

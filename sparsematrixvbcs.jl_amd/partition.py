@@ -35,13 +35,27 @@ class SplitPartition:
         return isinstance(other, SplitPartition) and np.array_equal(self.spl, other.spl)
 
 
+class CSCFields:
+    """A CSC matrix with its 1-based Int64 index arrays (the Julia SparseMatrixCSC fields), converted
+    once and shared by the partitioner and the constructor (matrices.from_csc)."""
+
+    def __init__(self, A):
+        import scipy.sparse as sp
+        A = sp.csc_matrix(A)
+        if not A.has_canonical_format:
+            A = A.copy()
+            A.sum_duplicates()  # also sorts the indices
+        self.A = A
+        self.shape = A.shape
+        self.colptr = np.add(A.indptr, 1, dtype=np.int64)
+        self.rowval = np.add(A.indices, 1, dtype=np.int64)
+
+
 def _csc(A):
-    A = A.tocsc()
-    if not A.has_sorted_indices:
-        A = A.sorted_indices()
-    colptr = np.ascontiguousarray(A.indptr, dtype=np.int64) + 1
-    rowval = np.ascontiguousarray(A.indices, dtype=np.int64) + 1
-    return A, colptr, rowval
+    if isinstance(A, CSCFields):
+        return A.A, A.colptr, A.rowval
+    F = CSCFields(A)
+    return F.A, F.colptr, F.rowval
 
 
 # --- cost models (costs.jl:8-10) ------------------------------------------------------------
