@@ -37,19 +37,34 @@ def gpu_time(B, x, y, reps):
     return float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e-3
 
 
-def cpu_time(R, x, n, reps=5, trsp=None):
+def cpu_time(R, x, n, reps=5, trsp=None, B=None):
+    """CPU time of the same product: the reference's SIMD kernel (oracle/vbc_simd.c) for 1DVBC B'x on
+    all host threads with the reference's one-stripe grabs (multiply_1DVBC.jl:169-177) and on 1 core,
+    its serial TrSpMV! for the CSC row; the scalar oracle for 2D VBC (no SIMD port).  Returns
+    (seconds all threads, threads, seconds 1 core, kind)."""
     from oracle import oracle as O
-    th = max(1, min(16, os.cpu_count() or 1))
+    from oracle import simd as S
+    th = S.host_threads()
     y = np.zeros(n, dtype=x.dtype)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        if trsp is not None:
-            O.trspmv(trsp, x, y, nthreads=th)
-        else:
-            O.mul(R, x, y, trans=True, nthreads=th)
-        ts.append(time.perf_counter() - t0)
-    return float(np.median(ts)), th
+
+    def med(f):
+        f()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+    if trsp is not None:
+        cp = np.add(trsp.indptr, 1, dtype=np.int64)
+        rv = np.add(trsp.indices, 1, dtype=np.int64)
+        t1 = med(lambda: S.trspmv(cp, rv, trsp.data, trsp.shape[0], trsp.shape[1], x, y))
+        return t1, 1, t1, "simd (serial, TrSpMV.jl)"
+    if B is not None and not hasattr(B, "Pi"):
+        return (med(lambda: S.mul_t(B, x, y, th, 1)), th, med(lambda: S.mul_t(B, x, y, 1, 1)),
+                "simd (multiply_1DVBC.jl:90-180)")
+    t = med(lambda: O.mul(R, x, y, trans=True, nthreads=th))
+    return t, th, med(lambda: O.mul(R, x, y, trans=True, nthreads=1)), "scalar oracle"
 
 
 def main():
@@ -88,10 +103,11 @@ def main():
     def record(name, setup, mem, B=None, R=None, trsp=None):
         t_gpu = gpu_time(B, x, y, args.reps)
         err = float(np.linalg.norm(y.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref))
-        t_cpu, th = cpu_time(R, xh, n, trsp=trsp)
+        t_cpu, th, t_cpu1, kind = cpu_time(R, xh, n, trsp=trsp, B=B)
         bytes_ = B.info()["bytes_t"] if hasattr(B, "info") else None
         row = dict(method=name, setup_s=round(setup, 4), memory=int(mem), gpu_us=round(t_gpu * 1e6, 2),
-                   cpu_us=round(t_cpu * 1e6, 1), cpu_threads=th, speedup=round(t_cpu / t_gpu, 1),
+                   cpu_us=round(t_cpu * 1e6, 1), cpu_threads=th, cpu_1core_us=round(t_cpu1 * 1e6, 1), cpu_kind=kind,
+                   speedup=round(t_cpu / t_gpu, 1),
                    gpu_GBs=round(bytes_ / t_gpu / 1e9, 1) if bytes_ else None, rel_err=err)
         rows.append(row)
         print(f"{name:22s} setup {setup:8.3f}s  mem {mem:12d}  gpu {t_gpu * 1e6:9.2f} us  cpu {t_cpu * 1e6:10.1f} us"
