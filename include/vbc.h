@@ -225,6 +225,8 @@ typedef struct vbc_info {
     int32_t planar_bins;    /* B'x buckets laid out planar (vbc_planar.h) */
     int32_t planar_run;     /* longest row run of those buckets (1 = none; 2, 3: one x gather per run) */
     int32_t planar_split;   /* waves per chunk of the split planar product (1 = one wave per range) */
+    int32_t planar_pair;    /* 1: fp64 3-wide runs laid out for lane pairs (one 16-B gather per lane) */
+    int32_t reserved2_;
 } vbc_info;
 
 VBC_API int vbc_get_info(const vbc_handle *h, vbc_info *info);

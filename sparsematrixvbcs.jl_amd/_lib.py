@@ -63,7 +63,8 @@ class vbc_info(C.Structure):
                 ("bytes_t", C.c_int64), ("bytes_f", C.c_int64), ("bins_m", C.c_int32),
                 ("slot_bins", C.c_int32), ("bytes_m", C.c_int64),
                 ("sweep_bins", C.c_int32), ("planar_bins", C.c_int32),
-                ("planar_run", C.c_int32), ("planar_split", C.c_int32)]
+                ("planar_run", C.c_int32), ("planar_split", C.c_int32),
+                ("planar_pair", C.c_int32), ("reserved2_", C.c_int32)]
 
 
 _lib = None

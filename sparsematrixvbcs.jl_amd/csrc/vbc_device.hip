@@ -352,7 +352,6 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
                        const std::vector<int64_t> &order = {})
 {
     const int esz = h->esz;
-    const int RPI = slot_rpi(h, kind, w);
     // segment q of the layout is input segment order[q] (natural order when `order` is empty)
     const std::vector<int64_t> sbeg = order.empty() ? sbeg0 : permuted_sbeg(sbeg0, order);
     std::vector<int64_t> pstart(sbeg.size() - 1);
@@ -366,22 +365,38 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     const int64_t real = sbeg[nseg] - sbeg[0];
     const bool planar = slot_planar(h, kind, w);
     const int run = planar ? slot_runs(h, ents, sbeg0) : 1;  // sbeg0: the input order ents is in
-    std::vector<int32_t> cr = chunk_rows(sbeg, RPI);
-    for (int32_t &c : cr) c = (c + run - 1) / run * run;  // whole runs (an empty chunk: one padding run)
-    const int64_t nch = (int64_t)cr.size();
-    int64_t rows = 0;
-    for (int32_t c : cr) rows += c;
+    // pair layout (vbc_planar.h run_pair): fp64 3-wide stripes with runs of 3, a lane pair per stripe
+    // (for long segments: FE-3D's ~3 runs per stripe measured slower with 32-stripe chunks, 304 -> 315
+    // us, ldoor's ~15 faster, 92 -> 81 us)
+    bool pair = planar && run == 3 && esz == 8 && w == 3 && wsrc == 3 && h->planar_pair != 0 &&
+                (h->planar_pair == 2 || real >= 3 * 8 * std::max<int64_t>(nseg, 1));
+    int RPI = 0, split = 1;
+    std::vector<int32_t> cr;
+    int64_t nch = 0, rows = 0;
     const double target = planar ? (double)h->target_ranges_p : (double)h->target_ranges_s[kind];
     const double share = target * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        RPI = pair ? 32 : slot_rpi(h, kind, w);
+        cr = chunk_rows(sbeg, RPI);
+        for (int32_t &c : cr) {
+            c = (c + run - 1) / run * run;  // whole runs (an empty chunk: one padding run)
+            if (pair) c /= 3;               // pair layout: rows are run-rows
+        }
+        nch = (int64_t)cr.size();
+        rows = 0;
+        for (int32_t c : cr) rows += c;
+        // planar buckets with fewer chunks than wave slots: one chunk per workgroup of `split` waves
+        split = 1;
+        if (planar && h->planar_split != 0) {
+            if (h->planar_split > 1) split = h->planar_split;
+            else
+                while (split < 8 && (double)nch * split * 2 <= share) split *= 2;
+        }
+        if (!(pair && split > 1)) break;
+        pair = false;  // the split product runs the plain planar layout
+    }
     int64_t nr = (int64_t)std::llround(share);
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
-    // planar buckets with fewer chunks than wave slots: one chunk per workgroup of `split` waves
-    int split = 1;
-    if (planar && h->planar_split != 0) {
-        if (h->planar_split > 1) split = h->planar_split;
-        else
-            while (split < 8 && (double)nch * split * 2 <= share) split *= 2;
-    }
     if (split > 1) nr = nch;
     bool affine = true;
     for (size_t q = 1; q < out.size() && affine; q++)
@@ -415,6 +430,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.planar = planar ? 1 : 0;
     b.run = run;
     b.split = split;
+    b.pair = pair ? 1 : 0;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -432,7 +448,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     const int64_t E = rows * RPI;
     ps.rows = rows;
     ps.keys.resize(E);
-    ps.o_val = ar.reserve(E * w * esz);
+    ps.o_val = ar.reserve(E * w * esz * (pair ? 3 : 1));
     ps.o_out = ar.reserve(std::max<size_t>(out.size(), 1) * 4);
     ps.o_rrow = ar.reserve(rrow.size() * 4);
     ps.o_rchunk = ar.reserve(rchunk.size() * 4);
@@ -442,7 +458,37 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     uint32_t *key = ps.keys.data();
     char *vv = ar.at<char>(ps.o_val);
     int64_t row = 0;
-    for (int64_t c = 0; c < nch; c++) {
+    if (pair) {  // run-rows of 32 stripes: segments A (64 lanes x 16 B), B, C, D (vbc_planar.h run_pair)
+        double *dv = reinterpret_cast<double *>(vv);
+        for (int64_t c = 0; c < nch; c++) {
+            for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
+                const uint32_t last = qr + 1 == cr[c] ? kLast : 0u;
+                double *blk = dv + row * 288;
+                for (int sl = 0; sl < 32; sl++) {
+                    const int64_t seg = c * 32 + sl, e = row * 32 + sl;
+                    const bool real_run = seg < nseg && sbeg[seg] + 3 * qr < sbeg[seg + 1];
+                    double v[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+                    if (real_run) {
+                        for (int d = 0; d < 3; d++)
+                            std::memcpy(v[d], val + ents[pstart[seg] + 3 * qr + d].voff * esz, 3 * sizeof(double));
+                        key[e] = ents[pstart[seg] + 3 * qr].key | last;
+                    } else {
+                        key[e] = kPad | last;
+                    }
+                    blk[4 * sl + 0] = v[0][0];
+                    blk[4 * sl + 1] = v[0][1];
+                    blk[4 * sl + 2] = v[0][2];
+                    blk[4 * sl + 3] = v[1][2];
+                    blk[128 + 2 * sl + 0] = v[1][0];
+                    blk[128 + 2 * sl + 1] = v[1][1];
+                    blk[192 + sl] = v[2][2];
+                    blk[224 + 2 * sl + 0] = v[2][0];
+                    blk[224 + 2 * sl + 1] = v[2][1];
+                }
+            }
+        }
+    }
+    for (int64_t c = 0; c < (pair ? 0 : nch); c++) {
         for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
             const uint32_t last = qr + run == cr[c] ? kLast : 0u;  // on the last run's first row
             for (int sl = 0; sl < RPI; sl++) {
@@ -1163,6 +1209,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
+    if (const char *e = getenv("VBC_PLANAR_PAIR")) h->planar_pair = atoi(e) == 0 ? 0 : atoi(e) == 2 ? 2 : 1;  // 2: always
     if (const char *e = getenv("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
@@ -1472,6 +1519,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
         for (const auto &b : h->lt.pbins) {
             info->planar_run = std::max<int32_t>(info->planar_run, b.run);
             info->planar_split = std::max<int32_t>(info->planar_split, b.split);
+            info->planar_pair = std::max<int32_t>(info->planar_pair, b.pair);
         }
     info->bytes_m = h->bytes_m;
     return VBC_OK;

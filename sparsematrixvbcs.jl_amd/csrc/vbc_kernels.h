@@ -92,7 +92,8 @@ struct SlotBin {
                          // keys / LAST are read from each run's first row, x gathered `run` elements wide
     int32_t split;       // planar: > 1 = one chunk per workgroup of `split` waves, each folding a slice of
                          // the chunk's rows, partials summed in LDS (small matrices: more waves in flight)
-    int32_t pad_;
+    int32_t pair;        // planar fp64 w = 3, run = 3: a lane pair per stripe, 32 stripes per chunk, rows =
+                         // run-rows of 288 values (vbc_planar.h run_pair)
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key

@@ -263,6 +263,184 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
                                                                       lds_out);
 }
 
+// Lane-pair planar product (SlotBin::pair: fp64, 3-wide stripes, rows in runs of 3 -- a 3-dof
+// stiffness operator).  A run's three x values are 24 B: one lane needs a dwordx4 + dwordx2 gather
+// (two requests).  Here lanes 2s and 2s+1 share stripe s: they gather x[g .. g+1] and x[g+1 .. g+2]
+// with ONE dwordx4 instruction (same 64-B line, merged by the addresser) and swap the element the
+// other one lacks over DPP.  The even lane owns columns 0 and 1, the odd lane column 2, each folding
+// its columns' three rows in stored order (multiply_1DVBC.jl:101-104), so every output is still the
+// reference's serial sum.  A chunk is 32 stripes; a row of the layout is a *run-row* (one run of every
+// stripe, 288 values, no padding): A = 64 lanes x {r0c0, r0c1 | r0c2, r1c2}, B = 32 x {r1c0, r1c1},
+// C = 32 x r2c2, D = 32 x {r2c0, r2c1}; three dwordx4 loads per lane per run-row (the odd lane's
+// second one reads C and its neighbour, its third the even partner's D line: merged requests).
+template <int NRS, bool FASTE, int NB, bool KC>
+__device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, const double *__restrict__ x,
+                                         double *__restrict__ y, double alpha, double beta, bool rd, char *lds_wave,
+                                         int *lds_out)
+{
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const int R0 = G(b.rrow)[r], R1 = G(b.rrow)[r + 1];
+    if (R0 >= R1) return;
+    int c = G(b.rchunk)[r];
+    const bool odd = (lane & 1) != 0;
+    const int ps = lane >> 1;  // stripe slot of the pair
+    const gptr<const double> val = G(static_cast<const double *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const double> xg = G(x);
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;
+    const cptr bases = (cptr)b.base;
+    const cptr doffs = (cptr)b.kdoff;
+    // per-lane element offsets of the three value loads inside a run-row
+    const int o0 = 2 * lane, o1 = odd ? 192 + ps : 128 + 2 * ps, o2 = 224 + 2 * ps;
+    auto load = [&](int R, uint32_t (&kk)[NRS], uint32_t (&bs)[NRS], d2 (&v)[NRS][3]) {
+#pragma unroll
+        for (int j = 0; j < NRS; j++) {
+            const int Rc = min(R + j, R1 - 1);
+            if constexpr (KC) {
+                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + ps];
+                bs[j] = bases[Rc];
+            } else {
+                kk[j] = key[(size_t)Rc * 32 + ps];
+                bs[j] = 0;
+            }
+            const gptr<const double> rowp = val + (size_t)Rc * 288;
+            v[j][0] = __builtin_nontemporal_load((gptr<const d2>)(rowp + o0));
+            v[j][1] = *(const __attribute__((address_space(1))) d2 *)(rowp + o1);  // 8-B aligned (odd lanes)
+            v[j][2] = __builtin_nontemporal_load((gptr<const d2>)(rowp + o2));
+        }
+    };
+    constexpr uint32_t kPad16 = 0xFFFF8000u;
+    auto gather = [&](const uint32_t (&kk)[NRS], const uint32_t (&bs)[NRS], d2 (&xv)[NRS]) {
+#pragma unroll
+        for (int j = 0; j < NRS; j++) {
+            const uint32_t gi = KC ? (bs[j] & kSlotIdx) + (kk[j] == kPad16 ? 0u : kk[j]) : kk[j] & kSlotIdx;
+            xv[j] = *(const __attribute__((address_space(1))) d2 *)(xg + gi + (odd ? 1 : 0));  // 8-B aligned
+        }
+    };
+    double acc0 = 0.0, acc1 = 0.0;  // even: columns 0, 1; odd: column 2 in acc0
+    int nbuf = 0, cfirst = c;
+    const int c0 = c;
+    if constexpr (!FASTE) {
+        if (!b.out_affine) {
+            const int n = min(kSlotOutEntries, b.nseg - c0 * 32);
+            for (int i = lane; i < n; i += 64) lds_out[i] = G(b.out)[c0 * 32 + i];
+        }
+    }
+    // staged chunks [cfirst, cfirst + nbuf) -> y: one contiguous run of 32 * 3 values per chunk
+    auto write_out = [&]() {
+        const int64_t segs = min((int64_t)nbuf * 32, (int64_t)b.nseg - (int64_t)cfirst * 32);
+        const int64_t bytes = segs * 3 * (int64_t)sizeof(double);
+        char *dst = reinterpret_cast<char *>(y + b.out_base + (int64_t)cfirst * 32 * 3);
+        if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
+                if (off + 16 <= bytes) *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                else
+                    for (int64_t q = off; q < bytes; q += 8)
+                        *(gptr<double>)(dst + q) = *reinterpret_cast<const double *>(lds_wave + q);
+            }
+        } else {
+            for (int64_t off = (int64_t)lane * 8; off < bytes; off += 512)
+                *(gptr<double>)(dst + off) = *reinterpret_cast<const double *>(lds_wave + off);
+        }
+        nbuf = 0;
+    };
+    auto flush = [&]() {
+        const int seg = c * 32 + ps;
+        if constexpr (NB > 0) {
+            double *st = reinterpret_cast<double *>(lds_wave) + ((size_t)nbuf * 32 + ps) * 3;
+            if (odd) st[2] = alpha * acc0;
+            else {
+                st[0] = alpha * acc0;
+                st[1] = alpha * acc1;
+            }
+            if (nbuf == 0) cfirst = c;
+        } else if (seg < b.nseg) {
+            const int o = (FASTE || b.out_affine) ? b.out_base + seg * b.out_stride : lds_out[(c - c0) * 32 + ps];
+            gptr<double> yo = G(y) + o;
+            if (odd) {
+                double q = alpha * acc0;
+                if (!FASTE && rd) q = fmadd(beta, yo[2], q);
+                yo[2] = q;
+            } else {
+                double q0 = alpha * acc0, q1 = alpha * acc1;
+                if (!FASTE && rd) {
+                    q0 = fmadd(beta, yo[0], q0);
+                    q1 = fmadd(beta, yo[1], q1);
+                }
+                yo[0] = q0;
+                yo[1] = q1;
+            }
+        }
+        acc0 = acc1 = 0.0;
+        c++;
+        if constexpr (NB > 0) {
+            if (++nbuf == NB) write_out();
+        }
+    };
+    int R1v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
+    auto compute = [&](int R, const uint32_t (&kk)[NRS], const uint32_t (&bs)[NRS], const d2 (&v)[NRS][3],
+                       const d2 (&xv)[NRS]) {
+#pragma unroll
+        for (int j = 0; j < NRS; j++) {
+            const bool live = R + j < R1v;
+            const bool pad = KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0;
+            // even sends x[g] (its .x), odd sends x[g+2] (its .y); each receives the element it lacks
+            const double t = odd ? xv[j].y : xv[j].x;
+            const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)tb, 0xB1, 0xF, 0xF, true);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(tb >> 32), 0xB1, 0xF, 0xF, true);
+            const double other = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+            double x0 = odd ? other : xv[j].x, x1 = odd ? xv[j].x : xv[j].y, x2 = odd ? xv[j].y : other;
+            if (pad) x0 = x1 = x2 = 0.0;
+            // even: v[0] = {r0c0, r0c1}, v[1] = {r1c0, r1c1}, v[2] = {r2c0, r2c1}
+            // odd:  v[0] = {r0c2, r1c2}, v[1].x = r2c2
+            const double n0 = odd ? fmadd(v[j][1].x, x2, fmadd(v[j][0].y, x1, fmadd(v[j][0].x, x0, acc0)))
+                                  : fmadd(v[j][2].x, x2, fmadd(v[j][1].x, x1, fmadd(v[j][0].x, x0, acc0)));
+            const double n1 = fmadd(v[j][2].y, x2, fmadd(v[j][1].y, x1, fmadd(v[j][0].y, x0, acc1)));
+            acc0 = live ? n0 : acc0;
+            acc1 = live ? n1 : acc1;
+            const uint32_t lastw = KC ? bs[j] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[j]);
+            if (R + j < R1 && (lastw & kLast)) flush();
+        }
+    };
+    uint32_t kA[NRS], kB[NRS], bA[NRS], bB[NRS];
+    d2 vA[NRS][3], vB[NRS][3], xv[NRS];
+    load(R0, kA, bA, vA);
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int R = R0; R < R1; R += 2 * NRS) {
+        gather(kA, bA, xv);
+        load(R + NRS, kB, bB, vB);
+        compute(R, kA, bA, vA, xv);
+        gather(kB, bB, xv);
+        load(R + 2 * NRS, kA, bA, vA);
+        compute(R + NRS, kB, bB, vB, xv);
+    }
+    if constexpr (NB > 0) {
+        if (nbuf > 0) write_out();
+    }
+}
+
+template <bool FASTE, int NB, bool KC>
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin *__restrict__ bp,
+                                                                  const double *__restrict__ x, double *__restrict__ y,
+                                                                  double alpha, double beta, int rd_i)
+{
+    const SlotBin b = *bp;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= b.nranges) return;
+    const int lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * 8192 : 16];
+    char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * 8192 : 0);
+    __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutEntries];
+    int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutEntries);
+#ifndef VBC_PAIR_NRS
+#define VBC_PAIR_NRS 4  // run-rows per pipeline stage (ldoor stand-in: 2 -> 82, 3 -> 80, 4 -> 77 us)
+#endif
+    run_pair<VBC_PAIR_NRS, FASTE, NB, KC>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
+}
+
 // Split planar product (SlotBin::split = P > 1; ranges are single chunks): workgroup c = chunk c, wave k
 // folds the rows [R0 + k*S, R0 + (k+1)*S) of it (S a whole number of runs) in stored order, the P
 // partial accumulators meet in LDS and wave 0 writes y = alpha * (((p0 + p1) + p2) + ...) + beta * y.

@@ -80,10 +80,34 @@ static int launch_t(const SlotBin &hb, const SlotBin *d_b, bool faste, bool stag
     }
 }
 
+template <bool KC>
+static int launch_pair(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
+                       double alpha, double beta, bool rd, hipStream_t s)
+{
+    const int grid = (hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
+    const double *xs = static_cast<const double *>(x);
+    double *ys = static_cast<double *>(y);
+    if (faste && staged)
+        hipLaunchKernelGGL((spmv_planar_pair<true, 8, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
+                           beta, (int)rd);
+    else if (faste)
+        hipLaunchKernelGGL((spmv_planar_pair<true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
+                           beta, (int)rd);
+    else
+        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
+                           beta, (int)rd);
+    return (int)hipGetLastError();
+}
+
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                   double alpha, double beta, bool rd, hipStream_t s)
 {
     if (hb.nranges <= 0) return (int)hipSuccess;
+    if (hb.pair) {  // fp64, w = 3, runs of 3: lane pairs (vbc_planar.h run_pair)
+        if (esz != 8 || hb.wkey != 3 || hb.run != 3) return (int)hipErrorInvalidValue;
+        return hb.kc ? launch_pair<true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
+                     : launch_pair<false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+    }
     if (esz == 8)
         return hb.kc ? launch_t<double, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
                      : launch_t<double, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);

@@ -245,3 +245,64 @@ def test_split_auto_small_matrix():
     y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
     V.mul_(y, B.T, dev(x))
     assert rel(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(B.n), trans=True)) <= TOL64
+
+
+@pytest.mark.parametrize("sort", ["0", "2"])
+@pytest.mark.parametrize("keys16", ["0", "1"])
+@pytest.mark.parametrize("stage", ["0", "8"])
+def test_pair_layout(monkeypatch, sort, keys16, stage):
+    """Lane-pair planar layout (SlotBin::pair: fp64, 3-wide stripes, runs of 3): one 16-B gather per
+    lane, DPP exchange, each column folded serially by one lane -> the oracle's bits, and the same
+    bits as the plain planar layout (VBC_PLANAR_PAIR=0); alpha / beta; non-finite x."""
+    monkeypatch.setenv("VBC_SLOTS", "1")
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
+    monkeypatch.setenv("VBC_SLOTS_SORT", sort)
+    monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
+    monkeypatch.setenv("VBC_SLOT_STAGE", stage)
+    base = V.synthetic.vbr_1dvbc(9000, 4000, 30000, 3, W=8, seed=31)
+    B = expand_runs(base, 3, seed=32)
+    R = ref_of(B)
+    rng = np.random.default_rng(33)
+    x = rng.uniform(-1, 1, B.m)
+    x[[4, 2001, 17000]] = [np.inf, np.nan, -np.inf]
+    y0 = rng.uniform(-1, 1, B.n)
+    outs = {}
+    for pair in ("2", "0"):
+        monkeypatch.setenv("VBC_PLANAR_PAIR", pair)
+        Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+        inf = Bc.info(trans=True)
+        assert inf["planar_bins"] == 1 and inf["planar_run"] == 3 and inf["planar_pair"] == (pair == "2")
+        y = torch.full((B.n,), 5.0, dtype=torch.float64, device=DEV)
+        V.mul_(y, Bc.T, dev(x))
+        outs[pair] = y.cpu().numpy()
+        yb = dev(y0.copy())
+        V.mul_(yb, Bc.T, dev(np.nan_to_num(x, posinf=1.0, neginf=-1.0, nan=0.5)), -0.5, 2.0)
+        outs[pair + "ab"] = yb.cpu().numpy()
+        Bc.release()
+    ref = O.mul(R, x, np.zeros(B.n), trans=True)
+    got = outs["2"]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    assert np.array_equal(got[fin], ref[fin])
+    assert np.array_equal(outs["2"], outs["0"], equal_nan=True)
+    xf = np.nan_to_num(x, posinf=1.0, neginf=-1.0, nan=0.5)
+    refab = O.mul(R, xf, y0.copy(), -0.5, 2.0, trans=True, ref_semantics=False)
+    assert rel(outs["2ab"], refab) <= TOL64
+    assert np.array_equal(outs["2ab"], outs["0ab"])
+
+
+def test_pair_auto_selection(monkeypatch):
+    """Auto selection: long 3-run segments (ldoor-like, ~15 runs per stripe) take the pair layout, also
+    as a blocked CSC (TrSpMV!); FE-3D's ~3 runs per stripe keep the plain planar layout (small
+    matrices take the split product instead; kept out here)."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
+    B = V.synthetic.fe_stiffness_3d_1dvbc(60000, 600000)
+    assert B.info(trans=True)["planar_pair"] == 0
+    A = V.synthetic.fe_stiffness_3d(60000, 2_700_000, 3, np.float64).tocsc()
+    A.sort_indices()
+    C = V.SparseMatrixCSC(A)
+    assert C.info(trans=True)["planar_pair"] == 1
+    x = np.random.default_rng(4).uniform(-1, 1, A.shape[0])
+    y = torch.zeros(A.shape[1], dtype=torch.float64, device=DEV)
+    V.TrSpMV_(y, C, dev(x))
+    assert np.array_equal(y.cpu().numpy(), O.trspmv(A, x, np.zeros(A.shape[1])))
