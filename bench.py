@@ -104,6 +104,9 @@ def kernel_name(B, local, k):
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     inf = B.info(local, True)
     if inf["planar_bins"] > 0:
+        if inf["planar_pair"]:
+            return ("vbc::spmv_planar_pair<FASTE, NB, KC> (lane pairs, fp64 3-wide runs of 3, "
+                    "csrc/vbc_planar.h)")
         if inf["planar_split"] > 1:
             return (f"vbc::spmv_planar_split<T, W, KC, RUN={inf['planar_run']}, P={inf['planar_split']}> "
                     "(split planar chunks, csrc/vbc_planar.h)")
