@@ -137,3 +137,27 @@ def test_mirror_keeps_reference_eltypes():
                 D[B.idx[Q] - 1, j:j + w] += B.val[q:q + w].astype(np.int64)
                 q += w
         assert np.array_equal(D, A.toarray().astype(np.int64))
+
+
+def test_sharded_create_validation_without_gpu():
+    """vbc1d_create_sharded / vbc_sharded_* reject bad arguments before touching a device."""
+    lib = L.lib()
+    h = C.c_void_p()
+    spl = np.array([1, 3], np.int64)
+    pos = np.array([1, 2], np.int64)
+    idx = np.array([1], np.int64)
+    ofs = np.array([1, 3], np.int64)
+    val = np.ones(2)
+    t = L.vbc_types(L.VBC_F64, 64, L.VBC_F64, 0)
+    devs = (C.c_int * 2)(0, 0)
+    args = (C.byref(h), 1, 2, 8, 1, spl.ctypes.data, pos.ctypes.data, idx.ctypes.data, ofs.ctypes.data,
+            val.ctypes.data, 2, C.byref(t))
+    assert lib.vbc1d_create_sharded(*args, 0, devs, L.VBC_SPLIT_STRIPES, 0) == L.VBC_INVALID_ARG  # no GPUs
+    assert "ngpus" in L.last_error()
+    assert lib.vbc1d_create_sharded(*args, 2, devs, 7, 0) == L.VBC_INVALID_ARG  # unknown split
+    assert lib.vbc1d_create_sharded(*args[:-1], None, 2, devs, L.VBC_SPLIT_ROWS, 0) == L.VBC_INVALID_ARG
+    assert lib.vbc_sharded_mul(None, 1, None, 0, None, 0, 1.0, 0.0, L.VBC_MEM_DEVICE, None, 0) == L.VBC_INVALID_ARG
+    n = C.c_int()
+    assert lib.vbc_sharded_count(None, C.byref(n)) == L.VBC_INVALID_ARG
+    assert lib.vbc_sharded_shard(None, 0, None, None, None, None) == L.VBC_INVALID_ARG
+    assert lib.vbc_sharded_destroy(None) == L.VBC_OK
