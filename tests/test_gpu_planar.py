@@ -306,3 +306,48 @@ def test_pair_auto_selection(monkeypatch):
     y = torch.zeros(A.shape[1], dtype=torch.float64, device=DEV)
     V.TrSpMV_(y, C, dev(x))
     assert np.array_equal(y.cpu().numpy(), O.trspmv(A, x, np.zeros(A.shape[1])))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_vbc2d_3x3_tiles_runs(monkeypatch, dtype):
+    """SparseMatrixVBC{3,3} with 3x3 tiles (multiply_VBC.jl:93-147): B'x expands each tile into its
+    three rows (constructors_VBC.jl:95-105), which are runs of 3 consecutive x rows -> the planar
+    layout with row runs (fp64: lane pairs when forced).  Equals the oracle bit for bit in fp64
+    (per-column serial order); both directions, alpha / beta."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
+    monkeypatch.setenv("VBC_SLOTS", "1")  # small and long-striped: auto would pick the merge layout
+    import scipy.sparse as sp
+    rng = np.random.default_rng(41)
+    nb = 3000
+    blocks = sp.random(nb, nb, density=0.004, random_state=rng, format="csr")
+    A = sp.kron(blocks, np.ones((3, 3))).tocsc()
+    A.data = rng.uniform(-1, 1, A.nnz)
+    A = A.astype(dtype)
+    B = V.SparseMatrixVBC[3, 3](A, V.AlternatingPacker(V.EquiChunker(3), V.EquiChunker(3)))
+    R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    for pair in ("0", "2"):
+        if pair == "2" and dtype == np.float32:
+            continue
+        monkeypatch.setenv("VBC_PLANAR_PAIR", pair)
+        Bc = V.SparseMatrixVBC(B.U, B.W, B.m, B.n, B.Pi, B.Phi, B.pos, B.idx, B.ofs, B.val)
+        inf = Bc.info(trans=True)
+        assert inf["planar_bins"] >= 1 and inf["planar_run"] == 3
+        assert inf["planar_pair"] == (1 if pair == "2" else 0)
+        x = rng.uniform(-1, 1, B.m).astype(dtype)
+        y = torch.zeros(B.n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+        V.mul_(y, Bc.T, dev(x))
+        ref = O.mul(R, x.astype(np.float64), np.zeros(B.n), trans=True)
+        if dtype == np.float64:
+            assert np.array_equal(y.cpu().numpy(), ref)
+        else:
+            assert rel(y.cpu().numpy(), ref) <= TOL32
+        y0 = rng.uniform(-1, 1, B.n).astype(dtype)
+        y = dev(y0.copy())
+        V.mul_(y, Bc.T, dev(x), 2.0, -1.0)
+        refab = O.mul(R, x.astype(np.float64), y0.astype(np.float64), 2.0, -1.0, trans=True, ref_semantics=False)
+        assert rel(y.cpu().numpy(), refab) <= (TOL64 if dtype == np.float64 else TOL32)
+        xf = rng.uniform(-1, 1, B.n).astype(dtype)
+        yf = torch.zeros(B.m, dtype=y.dtype, device=DEV)
+        V.mul_(yf, Bc, dev(xf))
+        assert rel(yf.cpu().numpy(), O.mul(R, xf.astype(np.float64), np.zeros(B.m))) <= (TOL64 if dtype == np.float64 else TOL32)
+        Bc.release()
