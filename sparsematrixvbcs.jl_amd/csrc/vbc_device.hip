@@ -771,6 +771,128 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     return VBC_OK;
 }
 
+// Forward row runs (the forward counterpart of slot_runs): the largest R in {3, 2} such that the
+// output rows come in aligned runs of R (rows R*q .. R*q+R-1, m divisible by R) with identical stripe
+// lists -- the dof rows of a node in a stiffness operator.  sbeg: every row a segment (natural order).
+static int fwd_runs(const vbc_handle *h, int w, int64_t m, const std::vector<Entry> &ents,
+                    const std::vector<int64_t> &sbeg)
+{
+    if (h->slot_runs == 0 || h->slot_planar == 0 || w < 2 || w > 4 || m <= 0) return 1;
+    for (int R = 3; R >= 2; R--) {
+        if (m % R || R * w > 12) continue;
+        bool ok = true;
+        for (int64_t q = 0; q < m && ok; q += R) {
+            const int64_t b0 = sbeg[q], len = sbeg[q + 1] - b0;
+            for (int r = 1; r < R && ok; r++) {
+                const int64_t br = sbeg[q + r];
+                if (sbeg[q + r + 1] - br != len) { ok = false; break; }
+                for (int64_t k = 0; k < len; k++)
+                    if ((ents[br + k].key & kSlotIdx) != (ents[b0 + k].key & kSlotIdx)) { ok = false; break; }
+            }
+        }
+        if (ok) return R;
+    }
+    return 1;
+}
+
+// Planar forward bin (vbc_planar.h run_planar_fwd): segment q = output rows R*q .. R*q+R-1, one per
+// lane, 64 per chunk; chunk row k = the k-th block (stripe) of each segment, its R x w values stored
+// column-group-major over the chunk (planar_off with width R*w, element r*w + c); one key per block =
+// the stripe's first column (the gathered x slice).  Natural order: y offsets affine (R*q).
+// Returns false (and builds nothing) when the padded rows exceed slots_pad x the real ones.
+static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry> &ents, const std::vector<int64_t> &sbeg,
+                           int64_t m, const char *val, Arena &ar, int &range0, PendingSlot &ps)
+{
+    const int esz = h->esz, RPI = 64, WV = R * w;
+    const int64_t nseg = m / R;
+    const int64_t nch = (nseg + RPI - 1) / RPI;
+    // run-segment lengths; natural order first, else sorted by length in windows of kSortWindow chunks
+    // (y offsets from a table then)
+    std::vector<int64_t> rb(nseg + 1, 0), order;
+    for (int64_t q = 0; q < nseg; q++) rb[q + 1] = rb[q] + sbeg[R * q + 1] - sbeg[R * q];
+    const int64_t real = rb[nseg];
+    std::vector<int32_t> cr = chunk_rows(rb, RPI);
+    int64_t rows = 0;
+    for (int32_t c : cr) rows += c;
+    if (real == 0) return false;
+    if ((double)(rows * RPI) > h->slots_pad * (double)real) {
+        if (h->slots_sort == 0) return false;
+        order = sorted_order(rb, RPI);
+        cr = chunk_rows(permuted_sbeg(rb, order), RPI);
+        rows = 0;
+        for (int32_t c : cr) rows += c;
+        if ((double)(rows * RPI) > h->slots_pad * (double)real) return false;
+    }
+    auto seg_of = [&](int64_t p) { return order.empty() ? p : order[p]; };  // layout position -> run-segment
+    const int64_t nr = std::max<int64_t>(1, std::min<int64_t>(h->target_ranges_p, nch));
+    std::vector<int32_t> rrow{0}, rchunk{0};
+    int64_t acc = 0;
+    for (int64_t c = 0; c < nch; c++) {
+        acc += cr[c];
+        if (c + 1 < nch && (int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows) {
+            rrow.push_back((int32_t)acc);
+            rchunk.push_back((int32_t)(c + 1));
+        }
+    }
+    rrow.push_back((int32_t)rows);
+    ps = PendingSlot{};
+    SlotBin &b = ps.b;
+    b.kind = 1;
+    b.wkey = w;
+    b.w = w;
+    b.wst = w;
+    b.rpi = RPI;
+    b.range0 = 0;  // its own launch
+    b.nranges = (int32_t)rchunk.size();
+    b.nseg = (int32_t)nseg;
+    b.u = h->slot_u;
+    b.diag = h->diag;
+    b.spl = 1;
+    b.planar = 1;
+    b.run = R;
+    b.split = 1;
+    b.pair = 0;
+    b.out_affine = order.empty() ? 1 : 0;
+    b.out_base = 0;
+    b.out_stride = R;
+    b.contig = b.out_affine;
+    const int64_t E = rows * RPI;
+    ps.rows = rows;
+    ps.keys.resize(E);
+    ps.o_val = ar.reserve(E * WV * esz);
+    ps.o_out = ar.reserve(std::max<int64_t>(order.size(), 1) * 4);
+    for (size_t p = 0; p < order.size(); p++) ar.at<int32_t>(ps.o_out)[p] = (int32_t)(R * order[p]);
+    ps.o_rrow = ar.reserve(rrow.size() * 4);
+    ps.o_rchunk = ar.reserve(rchunk.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_rrow), rrow.data(), rrow.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_rchunk), rchunk.data(), rchunk.size() * 4);
+    char *vv = ar.at<char>(ps.o_val);
+    int64_t row = 0;
+    for (int64_t c = 0; c < nch; c++) {
+        for (int32_t k = 0; k < cr[c]; k++, row++) {
+            const uint32_t last = k + 1 == cr[c] ? kLast : 0u;
+            char *rowp = vv + row * RPI * WV * esz;
+            for (int sl = 0; sl < RPI; sl++) {
+                const int64_t p = c * RPI + sl, e = row * RPI + sl;
+                const int64_t q = p < nseg ? seg_of(p) : 0;
+                const bool real_blk = p < nseg && sbeg[R * q] + k < sbeg[R * q + 1];
+                ps.keys[e] = real_blk ? ((ents[sbeg[R * q] + k].key & kSlotIdx) | last) : (kPad | last);
+                for (int r = 0; r < R; r++)
+                    for (int cc = 0; cc < w; cc++) {
+                        char *dst = rowp + planar_off(esz, WV, sl, r * w + cc) * esz;
+                        if (real_blk) std::memcpy(dst, val + (ents[sbeg[R * q + r] + k].voff + cc) * esz, (size_t)esz);
+                        else std::memset(dst, 0, (size_t)esz);
+                    }
+            }
+        }
+    }
+    ps.kc_ok = h->slot_keys16 != 0 && slot_keys_compressible(ps.keys, rows, RPI);
+    h->slot_rows_padded += E;
+    h->slot_rows_real += real;
+    (void)range0;
+    return true;
+}
+
 // Forward layout: per width bucket, segments = output rows with entries of that width (ascending),
 // entries = (row, stripe) blocks ordered by stripe within the row.  With a single bucket, a slotted
 // layout takes every row as a segment (affine, no fill list).
@@ -834,6 +956,23 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
                 ents[e] = {(uint32_t)s.col0[l] | (!slotted && e == cnt[i] ? kHead : 0u), s.voff[l] + (r - s.rbeg[l]) * w};
             }
         Ls.emplace_back();
+        if (single) {  // node-blocked rows: the planar forward layout with row runs
+            const int R = fwd_runs(h, w, s.m, ents, sbeg);
+            PendingSlot ps;
+            int zero = 0;
+            if (R > 1 && build_fwd_runs(h, w, R, ents, sbeg, s.m, val, ar, zero, ps)) {
+                std::vector<PendingSlot> one;
+                one.push_back(std::move(ps));
+                commit_launch_keys(h, one, ar);
+                const PendingSlot &p1 = one[0];
+                h->bytes_f += p1.rows * p1.b.rpi * (int64_t)w * R * h->esz + p1.key_bytes + s.m * h->esz;
+                std::fill(any.begin(), any.end(), 1);
+                pbs.push_back({});
+                pss.push_back(std::move(one));
+                pws.push_back({});
+                continue;
+            }
+        }
         if (slotted) {
             PendingSlot ps;
             int srange0 = 0;
@@ -1521,6 +1660,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
             info->planar_split = std::max<int32_t>(info->planar_split, b.split);
             info->planar_pair = std::max<int32_t>(info->planar_pair, b.pair);
         }
+    info->fwd_run = 1;
+    if (h->has_f)
+        for (const auto &l : h->lf)
+            for (const auto &b : l.pbins) info->fwd_run = std::max<int32_t>(info->fwd_run, b.run);
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }

@@ -263,6 +263,148 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
                                                                       lds_out);
 }
 
+// Planar forward product with row runs (SlotBin kind 1, run = R): mul!(y, B, x) for node-blocked rows.
+// A lane owns a segment of R consecutive output rows whose stripe lists are identical; per block (chunk
+// row) it loads the block's R x w values (column-group-major, planar_off width R*w), gathers the
+// stripe's w-wide x slice once (x[j .. j+w-1], multiply_1DVBC.jl:27 -- one gather for R rows instead
+// of R), and adds the R dot products to its R accumulators, blocks in stripe order as the reference's
+// serial stripe loop (:62-71).  At the LAST row the lane writes y[R*q .. R*q+R-1] (contiguous, LDS-
+// staged in runs of NB chunks when FASTE).
+template <typename T, int W_, int R, int U, bool FASTE, int NB, bool KC>
+__device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane, const T *__restrict__ x,
+                                               T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave)
+{
+    constexpr int WV = R * W_;
+    const int R0 = G(b.rrow)[r], R1 = G(b.rrow)[r + 1];
+    if (R0 >= R1) return;
+    int c = G(b.rchunk)[r];
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> xg = G(x);
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;
+    const cptr bases = (cptr)b.base;
+    const cptr doffs = (cptr)b.kdoff;
+    auto load = [&](int Rr, uint32_t (&kk)[U], uint32_t (&bs)[U], T (&v)[U][WV]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int Rc = min(Rr + u, R1 - 1);
+            if constexpr (KC) {
+                kk[u] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + lane];
+                bs[u] = bases[Rc];
+            } else {
+                kk[u] = __builtin_nontemporal_load(key + (size_t)Rc * 64 + lane);
+                bs[u] = 0;
+            }
+            ld_row<T, WV, 0>(val + (size_t)Rc * 64 * WV, lane, v[u]);
+        }
+    };
+    constexpr uint32_t kPad16 = 0xFFFF8000u;
+    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&bs)[U], T (&xv)[U][W_]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t gi = KC ? (bs[u] & kSlotIdx) + (kk[u] == kPad16 ? 0u : kk[u]) : kk[u] & kSlotIdx;
+            ld_run<T, W_>(xg + gi, xv[u]);
+        }
+    };
+    T acc[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) acc[q] = T(0);
+    int nbuf = 0, cfirst = c;
+    auto write_out = [&]() {
+        const int64_t segs = min((int64_t)nbuf * 64, (int64_t)b.nseg - (int64_t)cfirst * 64);
+        const int64_t bytes = segs * R * (int64_t)sizeof(T);
+        char *dst = reinterpret_cast<char *>(y + b.out_base + (int64_t)cfirst * 64 * R);
+        if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
+                if (off + 16 <= bytes) *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                else
+                    for (int64_t q = off; q < bytes; q += sizeof(T))
+                        *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);
+            }
+        } else {
+            for (int64_t off = (int64_t)lane * sizeof(T); off < bytes; off += 64 * sizeof(T))
+                *(gptr<T>)(dst + off) = *reinterpret_cast<const T *>(lds_wave + off);
+        }
+        nbuf = 0;
+    };
+    auto flush = [&]() {
+        const int seg = c * 64 + lane;
+        if constexpr (NB > 0) {
+            T *st = reinterpret_cast<T *>(lds_wave) + ((size_t)nbuf * 64 + lane) * R;
+#pragma unroll
+            for (int q = 0; q < R; q++) st[q] = alpha * acc[q];
+            if (nbuf == 0) cfirst = c;
+        } else if (seg < b.nseg) {  // affine (natural order) or the table of a length-sorted layout
+            gptr<T> yo = G(y) + (b.out_affine ? b.out_base + (int64_t)seg * R : (int64_t)G(b.out)[seg]);
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                T v = alpha * acc[q];
+                if (!FASTE && rd) v = fmadd(beta, yo[q], v);
+                yo[q] = v;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < R; q++) acc[q] = T(0);
+        c++;
+        if constexpr (NB > 0) {
+            if (++nbuf == NB) write_out();
+        }
+    };
+    int R1v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
+    auto compute = [&](int Rr, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const T (&v)[U][WV],
+                       const T (&xv)[U][W_]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool live = Rr + u < R1v;
+            const bool pad = KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0;
+#pragma unroll
+            for (int q = 0; q < R; q++) {  // one dot product per output row of the run
+                T d = v[u][q * W_] * xv[u][0];
+#pragma unroll
+                for (int e = 1; e < W_; e++) d = fmadd(v[u][q * W_ + e], xv[u][e], d);
+                acc[q] = (live && !pad) ? acc[q] + d : acc[q];
+            }
+            const uint32_t lastw = KC ? bs[u] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[u]);
+            if (Rr + u < R1 && (lastw & kLast)) flush();
+        }
+    };
+    uint32_t kA[U], kB[U], bA[U], bB[U];
+    T vA[U][WV], vB[U][WV], xv[U][W_];
+    load(R0, kA, bA, vA);
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int Rr = R0; Rr < R1; Rr += 2 * U) {
+        gather(kA, bA, xv);
+        load(Rr + U, kB, bB, vB);
+        compute(Rr, kA, bA, vA, xv);
+        gather(kB, bB, xv);
+        load(Rr + 2 * U, kA, bA, vA);
+        compute(Rr + U, kB, bB, vB, xv);
+    }
+    if constexpr (NB > 0) {
+        if (nbuf > 0) write_out();
+    }
+}
+
+template <typename T, int W_, int R, bool FASTE, int NB, bool KC>
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin *__restrict__ bp, const T *__restrict__ x,
+                                                                 T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const SlotBin b = *bp;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= b.nranges) return;
+    const int lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * 8192 : 16];
+    char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * 8192 : 0);
+#ifndef VBC_FWD_VALS
+#define VBC_FWD_VALS 24  // values per lane per stage (A/B builds: -DVBC_FWD_VALS=...)
+#endif
+    // blocks per stage: ~VBC_FWD_VALS values per lane (fp64 R = 3, w = 3: 2 blocks)
+    constexpr int U = (VBC_FWD_VALS / (R * W_)) < 2 ? 2 : (VBC_FWD_VALS / (R * W_));
+    run_planar_fwd<T, W_, R, U, FASTE, NB, KC>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds);
+}
+
 // Lane-pair planar product (SlotBin::pair: fp64, 3-wide stripes, rows in runs of 3 -- a 3-dof
 // stiffness operator).  A run's three x values are 24 B: one lane needs a dwordx4 + dwordx2 gather
 // (two requests).  Here lanes 2s and 2s+1 share stripe s: they gather x[g .. g+1] and x[g+1 .. g+2]

@@ -99,10 +99,47 @@ static int launch_pair(const SlotBin &hb, const SlotBin *d_b, bool faste, bool s
     return (int)hipGetLastError();
 }
 
+template <typename T, int W_, int R, bool KC>
+static void launch_fwd_wr(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
+                          double alpha, double beta, bool rd, hipStream_t s)
+{
+    const int grid = (hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
+    const T *xs = static_cast<const T *>(x);
+    T *ys = static_cast<T *>(y);
+    constexpr int NB = (8192 / (64 * R * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * R * (int)sizeof(T)));
+    if (faste && staged)
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, NB, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+                           (T)alpha, (T)beta, (int)rd);
+    else if (faste)
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+                           (T)alpha, (T)beta, (int)rd);
+    else
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+                           (T)alpha, (T)beta, (int)rd);
+}
+
+// forward row runs: w in {2, 3, 4}, R in {2, 3}
+template <typename T, bool KC>
+static int launch_fwd(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
+                      double alpha, double beta, bool rd, hipStream_t s)
+{
+#define VBC_FWD(W, RR)                                                                                      if (hb.wkey == W && hb.run == RR) {                                                                         launch_fwd_wr<T, W, RR, KC>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);                          return (int)hipGetLastError();                                                                      }
+    VBC_FWD(2, 2) VBC_FWD(2, 3) VBC_FWD(3, 2) VBC_FWD(3, 3) VBC_FWD(4, 2) VBC_FWD(4, 3)
+#undef VBC_FWD
+    return (int)hipErrorInvalidValue;
+}
+
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                   double alpha, double beta, bool rd, hipStream_t s)
 {
     if (hb.nranges <= 0) return (int)hipSuccess;
+    if (hb.kind == 1) {  // forward with row runs (vbc_planar.h run_planar_fwd)
+        if (esz == 8)
+            return hb.kc ? launch_fwd<double, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
+                         : launch_fwd<double, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+        return hb.kc ? launch_fwd<float, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
+                     : launch_fwd<float, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+    }
     if (hb.pair) {  // fp64, w = 3, runs of 3: lane pairs (vbc_planar.h run_pair)
         if (esz != 8 || hb.wkey != 3 || hb.run != 3) return (int)hipErrorInvalidValue;
         return hb.kc ? launch_pair<true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)

@@ -351,3 +351,79 @@ def test_vbc2d_3x3_tiles_runs(monkeypatch, dtype):
         V.mul_(yf, Bc, dev(xf))
         assert rel(yf.cpu().numpy(), O.mul(R, xf.astype(np.float64), np.zeros(B.m))) <= (TOL64 if dtype == np.float64 else TOL32)
         Bc.release()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w,R", [(3, 3), (2, 2), (2, 3), (3, 2), (4, 3), (4, 2)])
+@pytest.mark.parametrize("stage", ["0", "8"])
+def test_forward_row_runs(monkeypatch, dtype, w, R, stage):
+    """Forward mul!(y, B, x) with node-blocked rows (R consecutive output rows with identical stripe
+    lists): the planar forward layout, one w-wide x gather per R rows.  Against the oracle's forward
+    product (multiply_1DVBC.jl:9-83) within tolerance, alpha / beta, quirks (alpha dropped); integer
+    values bit for bit; the layout falls back when one row breaks its run."""
+    monkeypatch.setenv("VBC_SLOT_STAGE", stage)
+    rng = np.random.default_rng(100 * w + R)
+    base = V.synthetic.vbr_1dvbc(6000, 1500, 30000, w, W=8, dtype=dtype, seed=w + R)
+    # forward runs: rows of the TRANSPOSE (stripes of A^T) in runs -> build B from a blocked matrix
+    At = sp_blocked(base, R, rng, dtype)
+    B = V.SparseMatrix1DVBC[8](At, V.EquiChunker(w))
+    assert B.info(trans=False)["fwd_run"] == R
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    tol = TOL64 if dtype == np.float64 else TOL32
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    for alpha, beta in ((1.0, 0.0), (0.5, -1.5)):
+        x = rng.uniform(-1, 1, B.n).astype(dtype)
+        y0 = rng.uniform(-1, 1, B.m).astype(dtype)
+        y = dev(y0.copy())
+        V.mul_(y, B, dev(x), alpha, beta)
+        ref = O.mul(R64, x.astype(np.float64), y0.astype(np.float64), alpha, beta, ref_semantics=False)
+        assert rel(y.cpu().numpy(), ref) <= tol, (alpha, beta)
+    y = dev(y0.copy())
+    V.mul_(y, B, dev(x), 3.0, 0.0, quirks=True)  # forward quirks: alpha dropped
+    assert rel(y.cpu().numpy(), O.mul(R64, x.astype(np.float64), np.zeros(B.m))) <= tol
+    Bi = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs,
+                             rng.integers(-30, 30, len(B.val)).astype(dtype))
+    xi = rng.integers(-20, 20, B.n).astype(dtype)
+    yi = torch.zeros(B.m, dtype=tdt, device=DEV)
+    V.mul_(yi, Bi, dev(xi))
+    Ri = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, Bi.val.astype(np.float64))
+    assert np.array_equal(yi.cpu().numpy().astype(np.float64), O.mul(Ri, xi.astype(np.float64), np.zeros(B.m)))
+
+
+def sp_blocked(base, R, rng, dtype):
+    """A CSC matrix whose rows come in runs of R with identical patterns: row r of `base`'s pattern
+    (as a CSC of its m x n shape) expanded into R rows with fresh values."""
+    import scipy.sparse as sp
+    D = sp.csr_matrix(base.to_csc() if hasattr(base, "to_csc") else _to_csc(base))
+    Dk = sp.kron(D, np.ones((R, 1))).tocsc()
+    Dk.data = rng.uniform(-1, 1, Dk.nnz).astype(dtype)
+    return Dk.astype(dtype)
+
+
+def _to_csc(B):
+    import scipy.sparse as sp
+    rows, cols, vals = [], [], []
+    for l in range(len(B.Phi)):
+        j0, w = B.Phi.spl[l] - 1, B.Phi.spl[l + 1] - B.Phi.spl[l]
+        for k, Q in enumerate(range(B.pos[l] - 1, B.pos[l + 1] - 1)):
+            for c in range(w):
+                rows.append(B.idx[Q] - 1)
+                cols.append(j0 + c)
+                vals.append(1.0)
+    return sp.csc_matrix((vals, (rows, cols)), shape=(B.m, B.n))
+
+
+def test_forward_row_runs_fallback():
+    """One row outside its run's pattern: the forward product keeps the row-by-row layout."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(7)
+    A = sp.kron(sp.random(2000, 2000, density=0.003, random_state=rng, format="csr"), np.ones((3, 1))).tocsc()
+    A = A.tolil()
+    A[4, 1999] = 1.0  # row 4 (run 1) gains a column its run-mates lack
+    A = A.tocsc()
+    B = V.SparseMatrix1DVBC[8](A, V.EquiChunker(3))
+    assert B.info(trans=False)["fwd_run"] == 1
+    x = rng.uniform(-1, 1, B.n)
+    y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(y, B, dev(x))
+    assert rel(y.cpu().numpy(), A @ x) <= TOL64
