@@ -1645,7 +1645,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->bytes_f = h->bytes_f;
     info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : 0;
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too
-    for (auto &l : h->lf) sl += h->has_f ? (int32_t)l.sbins.size() : 0;
+    for (auto &l : h->lf) sl += h->has_f ? (int32_t)(l.sbins.size() + l.pbins.size()) : 0;  // + planar forward
     info->slot_bins = sl;
     int32_t sw = h->has_t ? (int32_t)h->lt.wbins.size() : 0;
     for (auto &l : h->lf) sw += h->has_f ? (int32_t)l.wbins.size() : 0;
