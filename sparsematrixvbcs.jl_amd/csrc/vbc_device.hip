@@ -389,14 +389,31 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         split = 1;
         if (planar && h->planar_split != 0) {
             if (h->planar_split > 1) split = h->planar_split;
-            else
-                while (split < 8 && (double)nch * split * 2 <= share) split *= 2;
+            else  // P waves per chunk while the grid stays within half the wave slots (ct20stif stand-in:
+                  // P = 4 10.6 us vs 8 11.2; ldoor's 1/8 stripe shard: P = 2 16.3 us vs 4 17.3, 8 18.7, 1 20.0)
+                while (split < 8 && (double)nch * split * 2 * 2 <= share) split *= 2;
         }
-        if (!(pair && split > 1)) break;
-        pair = false;  // the split product runs the plain planar layout
+        // the split product runs the plain planar layout; so does a pair layout that would fill fewer than
+        // half the wave slots, when the split product may be chosen instead (ldoor's 1/8 shard: 1250 pair
+        // chunks 21.8 us, planar split 16.3 us)
+        const bool drop = pair && (split > 1 || (h->planar_pair != 2 && h->planar_split != 0 && 2.0 * (double)nch < share));
+        if (!drop) break;
+        pair = false;
     }
     int64_t nr = (int64_t)std::llround(share);
+    // one wave per SIMD of the chip for this bucket (the target is CUs x occupancy x waves per workgroup)
+    const double quantum = share / std::max(1, planar ? h->occ_p : h->occ_s[kind]);
+    if (!planar && h->range_bytes > 0 && share >= 2 * quantum) {
+        // small slotted buckets: half the waves per SIMD, each with a longer range (FE's stripe shards:
+        // 1/2 89.7 -> 87.4 us, 1/4 49.0 -> 43.3 us, 1/8 28.1 -> 24.4 us; the full matrix keeps all)
+        const double bytes = (double)rows * RPI * (w * esz + 4);
+        if (bytes / share < (double)h->range_bytes) nr = (int64_t)std::llround(share / 2);
+    }
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
+    // fewer chunks than wave slots: whole waves per SIMD (ldoor's 1/4 shard: 2500 pair chunks as 2500
+    // ranges 33.0 us, as 2048 ranges 27.7 us)
+    const int64_t qi = (int64_t)quantum;
+    if (split == 1 && qi >= 1 && nr < (int64_t)std::llround(share) && nr > qi) nr = nr / qi * qi;
     if (split > 1) nr = nch;
     bool affine = true;
     for (size_t q = 1; q < out.size() && affine; q++)
@@ -414,6 +431,10 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     }
     rrow.push_back((int32_t)rows);
     nr = (int64_t)rchunk.size();
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] slot bin kind %d w %d planar %d pair %d run %d split %d chunks %lld rows %lld ranges %lld "
+                "(target share %.0f)\n", kind, w, (int)planar, (int)pair, run, split, (long long)nch, (long long)rows,
+                (long long)nr, share);
     ps = PendingSlot{};
     SlotBin &b = ps.b;
     b.kind = kind;
@@ -1332,9 +1353,15 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     for (int kd = 0; kd < 2; kd++)
         h->target_ranges_k[kd] = prop.multiProcessorCount * std::max(1, std::min(occ[kd], 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
-    for (int kd = 0; kd < 2; kd++)
-        h->target_ranges_s[kd] = prop.multiProcessorCount * std::max(1, std::min(occupancy_slots(h->esz, kd), 8)) * kWavesPerBlock;
-    if (const char *e = getenv("VBC_TARGET_RANGES_S")) h->target_ranges_s[0] = h->target_ranges_s[1] = std::max(1, atoi(e));
+    for (int kd = 0; kd < 2; kd++) {
+        h->occ_s[kd] = std::max(1, std::min(occupancy_slots(h->esz, kd), 8));
+        h->target_ranges_s[kd] = prop.multiProcessorCount * h->occ_s[kd] * kWavesPerBlock;
+    }
+    if (const char *e = getenv("VBC_TARGET_RANGES_S")) {  // an explicit range count is taken as is
+        h->target_ranges_s[0] = h->target_ranges_s[1] = std::max(1, atoi(e));
+        h->occ_s[0] = h->occ_s[1] = 1;
+    }
+    if (const char *e = getenv("VBC_RANGE_KB")) h->range_bytes = (int64_t)std::max(0, atoi(e)) << 10;
     if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
     if (const char *e = getenv("VBC_SLOTS_SORT")) h->slots_sort = atoi(e);
@@ -1353,8 +1380,12 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
     }
-    h->target_ranges_p = prop.multiProcessorCount * std::max(1, std::min(occupancy_planar(h->esz), 8)) * kWavesPerBlock;
-    if (const char *e = getenv("VBC_TARGET_RANGES_P")) h->target_ranges_p = std::max(1, atoi(e));
+    h->occ_p = std::max(1, std::min(occupancy_planar(h->esz), 8));
+    h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
+    if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
+        h->target_ranges_p = std::max(1, atoi(e));
+        h->occ_p = 1;
+    }
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
     if (flags & VBC_CREATE_MULTI) {
         const int om = occupancy_panel(h->esz);

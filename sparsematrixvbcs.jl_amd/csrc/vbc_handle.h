@@ -103,7 +103,11 @@ struct vbc_handle {
     double slots_pad = 1.10;          // auto: largest padded/real row ratio of a slotted bucket
     int slot_narrow = 1;              // VBC_SLOT_NARROW=0: one segment per lane slot for narrow B'x rows too
     int slots_sort = 1;               // VBC_SLOTS_SORT: 0 natural order only, 1 sort when needed, 2 always sort
-    int xcd = 0;                      // VBC_XCD=1: XCD-contiguous range order in the slotted kernel (measured slower)
+    int xcd = 1;                      // VBC_XCD=0: identity block order in the slotted kernel (XCD-contiguous ranges:
+                                      // FE 170.3 -> 169.2 us, its 1/8 stripe shard 28.1 -> 26.0 us)
+    int64_t range_bytes = 192 << 10;  // VBC_RANGE_KB: a slotted bucket with fewer layout bytes per range at full
+                                      // occupancy runs half the waves per SIMD (longer ranges)
+    int occ_s[2] = {4, 4};            // workgroups per CU of the slotted kernels (occupancy)
     int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)
     int64_t slot_rows_padded_last = 0;
     int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
@@ -115,6 +119,7 @@ struct vbc_handle {
     int planar_pair = 1;              // VBC_PLANAR_PAIR: 0 never, 1 auto (>= 8 runs per stripe), 2 always (fp64 w = 3 runs)
     int planar_split = -1;            // VBC_PLANAR_SPLIT: -1 auto (few chunks), 0 never, 2 / 4 / 8 waves per chunk
     int target_ranges_p = 4096;       // resident waves of the planar kernel
+    int occ_p = 4;                    // workgroups per CU of the planar kernel
     int sweep_mode = -1;              // VBC_SWEEP: -1 auto (no x locality), 0 never, 1 always (w <= 8)
     int sweep_tile = vbc::kSweepTileBytes;  // VBC_SWEEP_TILE=16: 16 KB of LDS accumulators per wave
 

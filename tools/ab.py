@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--trans", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--nrhs", type=int, default=0, help=">0: time the multi-RHS product (row-major X / Y)")
+    ap.add_argument("--shard", default="", help="R/N: time stripe shard R of the N-way split (distributed.stripe_split)")
     ap.add_argument("--copies", type=int, default=1,
                     help="build every variant this many times (A B .. A B ..): placement effects show as spread")
     args = ap.parse_args()
@@ -41,6 +42,10 @@ def main():
         B = V.SparseMatrixCSC(V.synthetic.standin("GHS_psdef/ldoor").T.tocsc().astype(dtype))
     else:  # fe | fe3d | ns | ns-mixed | c5 | ldoor | ct20stif: the bench's own matrices
         B = bench.build_matrix(args.workload, dtype, args.scale)
+        if args.shard:
+            r, n = (int(t) for t in args.shard.split("/"))
+            cuts = V.distributed.stripe_split(B, n)
+            B, _ = V.distributed.shard(B, int(cuts[r]), int(cuts[r + 1]))
     esz = np.dtype(dtype).itemsize
     trans = bool(args.trans)
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
