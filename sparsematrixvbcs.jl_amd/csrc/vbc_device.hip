@@ -447,6 +447,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.nseg = (int32_t)nseg;
     b.u = h->slot_u;
     b.diag = h->diag;
+    b.xcd = planar ? h->xcd_p : 0;
     b.spl = slot_spl(h, kind, w);
     b.planar = planar ? 1 : 0;
     b.run = run;
@@ -868,6 +869,7 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
     b.nseg = (int32_t)nseg;
     b.u = h->slot_u;
     b.diag = h->diag;
+    b.xcd = h->xcd_p;
     b.spl = 1;
     b.planar = 1;
     b.run = R;
@@ -1367,6 +1369,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOTS_SORT")) h->slots_sort = atoi(e);
     if (const char *e = getenv("VBC_SLOT_NARROW")) h->slot_narrow = atoi(e) != 0;
     if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
+    if (const char *e = getenv("VBC_XCD_P")) h->xcd_p = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
     if (const char *e = getenv("VBC_SLOT_DEDUP")) h->slot_dedup = atoi(e) != 0;
     if (const char *e = getenv("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;

@@ -94,6 +94,7 @@ struct SlotBin {
                          // the chunk's rows, partials summed in LDS (small matrices: more waves in flight)
     int32_t pair;        // planar fp64 w = 3, run = 3: a lane pair per stripe, 32 stripes per chunk, rows =
                          // run-rows of 288 values (vbc_planar.h run_pair)
+    int32_t xcd;         // planar: XCD-contiguous workgroup order (xcd_block)
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key
@@ -102,6 +103,15 @@ struct SlotBin {
     const int32_t *rrow;   // per range: first row, nranges + 1 entries
     const int32_t *rchunk; // per range: first chunk
 };
+
+// XCD-aware workgroup order: the hardware deals workgroups round-robin over the 8 XCDs, so logical
+// block xcd * (nb / 8) + i -- a contiguous run of ranges, whose x gathers overlap -- is given to the
+// workgroups of one XCD, which share its L2.  Blocks past the last full round keep their index.
+__device__ __forceinline__ int xcd_block(int blk, int nb)
+{
+    const int full = nb & ~7;
+    return blk < full ? (blk & 7) * (full >> 3) + (blk >> 3) : blk;
+}
 
 __device__ __forceinline__ int out_of_slots(const SlotBin &b, int seg)
 {

@@ -252,7 +252,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
 {
     const SlotBin b = *bp;
-    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
     const int lane = threadIdx.x & 63;
     __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * 8192 : 16];
@@ -392,7 +393,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin *
                                                                  T *__restrict__ y, T alpha, T beta, int rd_i)
 {
     const SlotBin b = *bp;
-    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
     const int lane = threadIdx.x & 63;
     __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * 8192 : 16];
@@ -570,7 +572,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin 
                                                                   double alpha, double beta, int rd_i)
 {
     const SlotBin b = *bp;
-    const int rg = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
     const int lane = threadIdx.x & 63;
     __shared__ __attribute__((aligned(16))) char stage[NB > 0 ? kWavesPerBlock * 8192 : 16];
@@ -594,7 +597,7 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin *__res
                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
 {
     const SlotBin b = *bp;
-    const int c = blockIdx.x;
+    const int c = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     if (c >= b.nranges) return;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     constexpr int U = planar_step<T, W_, RUN>(), NR = U / RUN;
