@@ -447,7 +447,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.nseg = (int32_t)nseg;
     b.u = h->slot_u;
     b.diag = h->diag;
-    b.xcd = planar ? h->xcd_p : 0;
+    b.xcd = (planar && split == 1) ? h->xcd_p : 0;  // split grids are small (one chunk per workgroup)
     b.spl = slot_spl(h, kind, w);
     b.planar = planar ? 1 : 0;
     b.run = run;

@@ -107,7 +107,8 @@ struct vbc_handle {
                                       // FE 170.3 -> 169.2 us, its 1/8 stripe shard 28.1 -> 26.0 us)
     int64_t range_bytes = 192 << 10;  // VBC_RANGE_KB: a slotted bucket with fewer layout bytes per range at full
                                       // occupancy runs half the waves per SIMD (longer ranges)
-    int xcd_p = 0;                    // VBC_XCD_P=1: XCD-contiguous workgroup order in the planar kernels
+    int xcd_p = 1;                    // VBC_XCD_P=0: identity workgroup order in the planar kernels (XCD-contiguous:
+                                      // ldoor stand-in fp64 76.8 -> 70.2 us, fp32 44.6 -> 39.8, TrSpMV! 44.6 -> 39.3)
     int occ_s[2] = {4, 4};            // workgroups per CU of the slotted kernels (occupancy)
     int64_t slot_rows_padded = 0, slot_rows_real = 0;  // entries of slotted buckets (with / without padding)
     int64_t slot_rows_padded_last = 0;
