@@ -592,6 +592,21 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin 
 // For matrices with fewer chunks than the chip has wave slots (ct20stif: 273 chunks of ~48 rows),
 // where one wave per chunk leaves the product latency-bound.  Same keys, values and gathers as
 // run_planar; summation order is per slice, then across slices.
+// Rows per step of the split product: planar_step's, unless an A/B build sets -DVBC_SPLIT_VALS
+// (values per lane per step; 72 -- usually the whole slice in one step -- measured slower: ct20stif
+// stand-in fp64 10.8 -> 13.2 us, ldoor's 1/8 shard 16.3 -> 20.1 us).
+template <typename T, int W_, int RUN>
+__host__ __device__ constexpr int planar_split_step()
+{
+#ifdef VBC_SPLIT_VALS
+    constexpr int cap = 8 * RUN;  // <= 8 runs: their scalar key bases stay in SGPRs
+    constexpr int u = (VBC_SPLIT_VALS / W_) / RUN * RUN;
+    return u < RUN ? RUN : (u > cap ? cap / RUN * RUN : u);
+#else
+    return planar_step<T, W_, RUN>();
+#endif
+}
+
 template <typename T, int W_, bool KC, int RUN, int P>
 __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin *__restrict__ bp, const T *__restrict__ x,
                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
@@ -600,7 +615,7 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin *__res
     const int c = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     if (c >= b.nranges) return;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int U = planar_step<T, W_, RUN>(), NR = U / RUN;
+    constexpr int U = planar_split_step<T, W_, RUN>(), NR = U / RUN;
     const int R0 = G(b.rrow)[c], R1 = G(b.rrow)[c + 1];
     const int S = ((R1 - R0 + P - 1) / P + RUN - 1) / RUN * RUN;
     const int a = __builtin_amdgcn_readfirstlane(min(R1, R0 + wv * S)), e = __builtin_amdgcn_readfirstlane(min(R1, a + S));
