@@ -64,7 +64,8 @@ class vbc_info(C.Structure):
                 ("slot_bins", C.c_int32), ("bytes_m", C.c_int64),
                 ("sweep_bins", C.c_int32), ("planar_bins", C.c_int32),
                 ("planar_run", C.c_int32), ("planar_split", C.c_int32),
-                ("planar_pair", C.c_int32), ("fwd_run", C.c_int32)]
+                ("planar_pair", C.c_int32), ("fwd_run", C.c_int32),
+                ("planar_mask", C.c_int32)]
 
 
 _lib = None

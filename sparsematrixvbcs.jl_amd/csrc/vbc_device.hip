@@ -155,7 +155,7 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
 
 struct PendingSlot {
     SlotBin b;
-    size_t o_key, o_val, o_out, o_rrow, o_rchunk, o_base = 0, o_doff = 0;
+    size_t o_key, o_val, o_out, o_rrow, o_rchunk, o_base = 0, o_doff = 0, o_nlive = 0;
     int64_t key_bytes = 0;       // index bytes as stored (keys, deltas, bases, delta offsets)
     std::vector<uint32_t> keys;  // full keys until commit_slot_keys picks the stored form
     int64_t rows = 0;
@@ -294,15 +294,36 @@ static std::vector<int64_t> permuted_sbeg(const std::vector<int64_t> &sbeg, cons
 // count within slots_pad of the real one and chunks short enough to balance over the ranges, first
 // in the natural segment order (affine y map), then sorted by length (y offsets from the table).
 // Returns 0 (merge layout), 1 (slotted, natural order) or 2 (slotted, `order`).
-static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
-                      int64_t total_entries, int64_t gather_limit, std::vector<int64_t> &order)
+// Chunk-local length order (SlotBin::mask): the RPI segments of each natural chunk by decreasing
+// length -- the chunk keeps its segments (x locality of the natural order), its live lanes at every
+// chunk row are a prefix, so the kernel can point the dead lanes at lane 0's lines.
+static std::vector<int64_t> chunk_sorted_order(const std::vector<int64_t> &sbeg, int RPI)
 {
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    std::vector<int64_t> ord(nseg);
+    for (int64_t i = 0; i < nseg; i++) ord[i] = i;
+    for (int64_t a = 0; a < nseg; a += RPI)
+        std::stable_sort(ord.begin() + a, ord.begin() + std::min(nseg, a + RPI), [&](int64_t p, int64_t q) {
+            return sbeg[p + 1] - sbeg[p] > sbeg[q + 1] - sbeg[q];
+        });
+    return ord;
+}
+
+// Padded / real rows a masked planar bucket may carry: padding costs instructions, not lines.
+constexpr double kMaskPad = 3.0;
+
+static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
+                      int64_t total_entries, int64_t gather_limit, std::vector<int64_t> &order,
+                      bool *mask = nullptr)
+{
+    if (mask) *mask = false;
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     const int64_t real = nseg > 0 ? sbeg[nseg] - sbeg[0] : 0;
     order.clear();
     if (h->slots_mode == 0 || real == 0 || gather_limit >= (int64_t)kSlotIdxLimit) return 0;
     if (nseg >= (int64_t(1) << 31)) return 0;
     const int RPI = slot_rpi(h, kind, w);
+    double pad_limit = 0;
     auto fits = [&](const std::vector<int64_t> &sb, bool force) {
         const std::vector<int32_t> cr = chunk_rows(sb, RPI);
         int64_t rows = 0, longest = 0;
@@ -312,10 +333,22 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
         const double ratio = (double)(rows * RPI) / (double)real;
         const double share = (double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1);
         const double rows_per_range = (double)rows / std::max(1.0, share);
-        return ratio <= h->slots_pad && (double)longest <= std::max(64.0, 0.5 * rows_per_range);
+        return ratio <= (pad_limit > 0 ? pad_limit : h->slots_pad) && (double)longest <= std::max(64.0, 0.5 * rows_per_range);
     };
     if (h->slots_sort != 2 && fits(sbeg, h->slots_mode == 1)) return 1;
     if (h->slots_sort == 0) return 0;
+    // (not for buckets small enough for the split product, which folds every padding row: build_slots)
+    const double share_p = (double)h->target_ranges_p * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    const bool split_likely = h->planar_split != 0 && (double)((nseg + RPI - 1) / RPI) * 4 <= share_p;
+    if (mask && kind == 0 && h->planar_mask != 0 && slot_planar(h, 0, w) && !split_likely) {
+        order = chunk_sorted_order(sbeg, RPI);
+        pad_limit = kMaskPad;
+        if (fits(permuted_sbeg(sbeg, order), h->slots_mode == 1)) {
+            *mask = true;
+            return 2;
+        }
+        pad_limit = 0;
+    }
     order = sorted_order(sbeg, RPI);
     if (fits(permuted_sbeg(sbeg, order), h->slots_mode == 1)) return 2;
     order.clear();
@@ -349,7 +382,7 @@ static int slot_runs(const vbc_handle *h, const std::vector<Entry> &ents, const 
 static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vector<Entry> &ents,
                        const std::vector<int64_t> &sbeg0, const std::vector<int32_t> &out0, int64_t total_entries,
                        const char *val, Arena &ar, int &range0, PendingSlot &ps,
-                       const std::vector<int64_t> &order = {})
+                       const std::vector<int64_t> &order = {}, bool mask = false)
 {
     const int esz = h->esz;
     // segment q of the layout is input segment order[q] (natural order when `order` is empty)
@@ -453,6 +486,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.run = run;
     b.split = split;
     b.pair = pair ? 1 : 0;
+    b.mask = (mask && planar && !pair && split == 1) ? 1 : 0;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -474,6 +508,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     ps.o_out = ar.reserve(std::max<size_t>(out.size(), 1) * 4);
     ps.o_rrow = ar.reserve(rrow.size() * 4);
     ps.o_rchunk = ar.reserve(rchunk.size() * 4);
+    if (b.mask) ps.o_nlive = ar.reserve((size_t)rows * 4);
     std::memcpy(ar.at<int32_t>(ps.o_out), out.data(), out.size() * 4);
     std::memcpy(ar.at<int32_t>(ps.o_rrow), rrow.data(), rrow.size() * 4);
     std::memcpy(ar.at<int32_t>(ps.o_rchunk), rchunk.data(), rchunk.size() * 4);
@@ -513,6 +548,17 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     for (int64_t c = 0; c < (pair ? 0 : nch); c++) {
         for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
             const uint32_t last = qr + run == cr[c] ? kLast : 0u;  // on the last run's first row
+            if (b.mask) {  // live lanes of this chunk row: a prefix in chunk-local length order
+                uint32_t nl = 0;
+                for (int sl = 0; sl < RPI; sl++) {
+                    const int64_t seg = c * RPI + sl;
+                    if (seg < nseg && sbeg[seg] + qr < sbeg[seg + 1]) {
+                        if (nl != (uint32_t)sl) return fail(VBC_INVALID_ARG, "masked planar chunk: live lanes not a prefix");
+                        nl++;
+                    }
+                }
+                ar.at<uint32_t>(ps.o_nlive)[row] = nl;
+            }
             for (int sl = 0; sl < RPI; sl++) {
                 const int64_t seg = c * RPI + sl, e = row * RPI + sl;
                 const bool real_row = seg < nseg && sbeg[seg] + qr < sbeg[seg + 1];
@@ -749,7 +795,8 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         const int wps = slot_planar(h, 0, w) ? w : (h->esz == 8 && w == 3 && !getenv("VBC_PAD")) ? 3 : wp;
         std::vector<int64_t> sbeg{0}, order;
         for (int64_t l : kv.second) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
-        if (want_slots(h, 0, wps, sbeg, total, s.m, order)) {
+        bool mask = false;
+        if (want_slots(h, 0, wps, sbeg, total, s.m, order, &mask)) {
             std::vector<Entry> ents;
             std::vector<int32_t> out;
             ents.reserve(sbeg.back());
@@ -759,7 +806,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                     ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
             }
             PendingSlot ps;
-            if (int st = build_slots(h, 0, wps, w, ents, sbeg, out, total, val, ar, srange0, ps, order)) return st;
+            if (int st = build_slots(h, 0, wps, w, ents, sbeg, out, total, val, ar, srange0, ps, order, mask)) return st;
             pss.push_back(std::move(ps));
             continue;
         }
@@ -1212,6 +1259,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.rchunk = reinterpret_cast<const int32_t *>(base + ps.o_rchunk);
         b.base = reinterpret_cast<const uint32_t *>(base + ps.o_base);
         b.kdoff = reinterpret_cast<const uint32_t *>(base + ps.o_doff);
+        b.nlive = reinterpret_cast<const uint32_t *>(base + ps.o_nlive);
         (b.planar ? L.pbins : L.sbins).push_back(b);
     }
     if (!L.pbins.empty()) {
@@ -1379,6 +1427,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
     if (const char *e = getenv("VBC_PLANAR_PAIR")) h->planar_pair = atoi(e) == 0 ? 0 : atoi(e) == 2 ? 2 : 1;  // 2: always
+    if (const char *e = getenv("VBC_PLANAR_MASK")) h->planar_mask = atoi(e) != 0;
     if (const char *e = getenv("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
@@ -1693,6 +1742,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
             info->planar_run = std::max<int32_t>(info->planar_run, b.run);
             info->planar_split = std::max<int32_t>(info->planar_split, b.split);
             info->planar_pair = std::max<int32_t>(info->planar_pair, b.pair);
+            info->planar_mask = std::max<int32_t>(info->planar_mask, b.mask);
         }
     info->fwd_run = 1;
     if (h->has_f)

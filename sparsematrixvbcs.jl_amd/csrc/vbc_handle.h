@@ -119,6 +119,8 @@ struct vbc_handle {
     int slot_planar = -1;             // VBC_SLOT_PLANAR: -1 auto (B'x, w = 3..8 wider than a lane vector), 0 never, 1 w >= 3
     int slot_runs = 1;                // VBC_SLOT_RUNS=0: no row-run gathers in planar buckets
     int planar_pair = 1;              // VBC_PLANAR_PAIR: 0 never, 1 auto (>= 8 runs per stripe), 2 always (fp64 w = 3 runs)
+    int planar_mask = 1;              // VBC_PLANAR_MASK: planar B'x buckets whose natural order pads > slots_pad: 1 masked
+                                      // chunk-local length order (SlotBin::mask), 0 length-sorted windows of 32 chunks
     int planar_split = -1;            // VBC_PLANAR_SPLIT: -1 auto (few chunks), 0 never, 2 / 4 / 8 waves per chunk
     int target_ranges_p = 4096;       // resident waves of the planar kernel
     int occ_p = 4;                    // workgroups per CU of the planar kernel

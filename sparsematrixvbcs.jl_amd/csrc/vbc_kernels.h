@@ -95,6 +95,9 @@ struct SlotBin {
     int32_t pair;        // planar fp64 w = 3, run = 3: a lane pair per stripe, 32 stripes per chunk, rows =
                          // run-rows of 288 values (vbc_planar.h run_pair)
     int32_t xcd;         // planar: XCD-contiguous workgroup order (xcd_block)
+    int32_t mask;        // planar: chunk-local length order (lanes of a chunk by decreasing length, the chunk's
+                         // 64 stripes kept) and nlive[row] = live lanes of the chunk row; dead lanes read
+                         // lane 0's key and values (no extra lines fetched) and fold nothing (vbc_planar.h)
     const uint32_t *key;   // rows * rpi: PAD | LAST | gather index  (kc: int16 deltas, INT16_MIN = PAD)
     const uint32_t *base;  // kc: per row, LAST | base gather index
     const uint32_t *kdoff; // kc: per row, offset (int16 units) of its delta pattern in key
@@ -102,6 +105,7 @@ struct SlotBin {
     const int32_t *out;    // per segment (when not affine)
     const int32_t *rrow;   // per range: first row, nranges + 1 entries
     const int32_t *rchunk; // per range: first chunk
+    const uint32_t *nlive; // mask: per row, live lanes (a prefix: lanes are in decreasing length order)
 };
 
 // XCD-aware workgroup order: the hardware deals workgroups round-robin over the 8 XCDs, so logical

@@ -88,7 +88,9 @@ __device__ __forceinline__ void ld_run(gptr<const T> p, T (&r)[RUN])
 // row only, and the run's x values are one RUN-wide gather.
 // FASTE: affine y map and beta = 0 (no loads on the write path); NB > 0 (FASTE, contiguous chunk
 // outputs): NB finished chunks staged in LDS and written as one run of 16-B stores.
-template <typename T, int W_, int U, bool FASTE, int NB, bool KC, int RUN>
+// MASK (SlotBin::mask): lanes >= nlive[row] are padding; they read lane 0's key and values (lines lane 0
+// fetches anyway) and fold nothing, so a chunk's padding rows cost no memory lines.
+template <typename T, int W_, int U, bool FASTE, int NB, bool KC, int RUN, bool MASK = false>
 __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, const T *__restrict__ x,
                                            T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave, int *lds_out)
 {
@@ -101,23 +103,29 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     typedef __attribute__((address_space(4))) const uint32_t *cptr;
     const cptr bases = (cptr)b.base;
     const cptr doffs = (cptr)b.kdoff;
+    const cptr nlive = (cptr)b.nlive;
     constexpr int NR = U / RUN;  // runs per step (ranges start and end on run boundaries)
     static_assert(NR * RUN == U, "a step holds whole runs");
-    auto load = [&](int R, uint32_t (&kk)[NR], uint32_t (&bs)[NR], T (&v)[U][W_]) {
+    auto load = [&](int R, uint32_t (&kk)[NR], uint32_t (&bs)[NR], int (&nl)[NR], T (&v)[U][W_]) {
 #pragma unroll
         for (int j = 0; j < NR; j++) {
             const int Rk = min(R + j * RUN, R1 - RUN);  // the run's first row (clamped: rows past the range)
+            int ln = lane;
+            if constexpr (MASK) {
+                nl[j] = (int)nlive[Rk];
+                ln = lane < nl[j] ? lane : 0;
+            }
             if constexpr (KC) {
-                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + lane];
+                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + ln];
                 bs[j] = bases[Rk];
             } else {
-                kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
+                kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + ln);
                 bs[j] = 0;
             }
 #pragma unroll
             for (int d = 0; d < RUN; d++) {
                 const int Rc = min(R + j * RUN + d, R1 - 1);
-                ld_row<T, W_, 0>(val + (size_t)Rc * 64 * W_, lane, v[j * RUN + d]);
+                ld_row<T, W_, 0>(val + (size_t)Rc * 64 * W_, ln, v[j * RUN + d]);
             }
         }
     };
@@ -190,12 +198,12 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     };
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
-    auto compute = [&](int R, const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], const T (&v)[U][W_],
-                       const T (&xv)[NR][RUN]) {
+    auto compute = [&](int R, const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], const int (&nl)[NR],
+                       const T (&v)[U][W_], const T (&xv)[NR][RUN]) {
 #pragma unroll
         for (int j = 0; j < NR; j++) {
-            const bool live = R + j * RUN < R1v;
-            const bool pad = KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0;
+            const bool pad = MASK ? lane >= nl[j] : (KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0);
+            const bool live = R + j * RUN < R1v && !(MASK && pad);  // MASK: lane 0's values, never folded
 #pragma unroll
             for (int d = 0; d < RUN; d++) {  // the run's rows in stored (reference) order
                 const T xe = pad ? T(0) : xv[j][d];
@@ -210,16 +218,17 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
         }
     };
     uint32_t kA[NR], kB[NR], bA[NR], bB[NR];
+    int nA[NR], nB[NR];
     T vA[U][W_], vB[U][W_], xv[NR][RUN];
-    load(R0, kA, bA, vA);
+    load(R0, kA, bA, nA, vA);
     __builtin_amdgcn_s_waitcnt(0);
     for (int R = R0; R < R1; R += 2 * U) {
         gather(kA, bA, xv);
-        load(R + U, kB, bB, vB);
-        compute(R, kA, bA, vA, xv);
+        load(R + U, kB, bB, nB, vB);
+        compute(R, kA, bA, nA, vA, xv);
         gather(kB, bB, xv);
-        load(R + 2 * U, kA, bA, vA);
-        compute(R + U, kB, bB, vB, xv);
+        load(R + 2 * U, kA, bA, nA, vA);
+        compute(R + U, kB, bB, nB, vB, xv);
     }
     if constexpr (NB > 0) {
         if (nbuf > 0) write_out();
@@ -247,7 +256,7 @@ __host__ __device__ constexpr int planar_nb()
     return (8192 / (64 * W_ * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * W_ * (int)sizeof(T)));
 }
 
-template <typename T, int W_, bool FASTE, int NB, bool KC, int RUN>
+template <typename T, int W_, bool FASTE, int NB, bool KC, int RUN, bool MASK = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__restrict__ bp, const T *__restrict__ x,
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
 {
@@ -260,8 +269,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
     char *lds = stage + (NB > 0 ? (threadIdx.x >> 6) * 8192 : 0);
     __shared__ int outs[FASTE ? 1 : kWavesPerBlock * kSlotOutEntries];
     int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutEntries);
-    run_planar<T, W_, planar_step<T, W_, RUN>(), FASTE, NB, KC, RUN>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds,
-                                                                      lds_out);
+    run_planar<T, W_, planar_step<T, W_, RUN>(), FASTE, NB, KC, RUN, MASK>(b, rg, lane, x, y, alpha, beta, rd_i != 0,
+                                                                            lds, lds_out);
 }
 
 // Planar forward product with row runs (SlotBin kind 1, run = R): mul!(y, B, x) for node-blocked rows.

@@ -14,7 +14,10 @@ static void launch_w(const SlotBin &hb, const SlotBin *d_b, bool faste, bool sta
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
     constexpr int NB = planar_nb<T, W_>();
-    if (faste && staged)
+    if (hb.mask)  // chunk-local length order: a y-offset table, never the affine write path
+        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC, RUN, true>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs,
+                           ys, (T)alpha, (T)beta, (int)rd);
+    else if (faste && staged)
         hipLaunchKernelGGL((spmv_planar<T, W_, true, NB, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else if (faste)

@@ -427,3 +427,51 @@ def test_forward_row_runs_fallback():
     y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
     V.mul_(y, B, dev(x))
     assert rel(y.cpu().numpy(), A @ x) <= TOL64
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w,R", [(3, 3), (5, 1), (6, 3)])
+@pytest.mark.parametrize("keys16", ["0", "1"])
+def test_masked_chunk_order(monkeypatch, dtype, w, R, keys16):
+    """Masked planar layout (SlotBin::mask): each natural chunk's 64 stripes in decreasing length
+    order, dead lanes of a chunk row reading lane 0's lines and folding nothing.  Every stripe still
+    folds its rows serially in stored order, so the result equals the length-sorted layout
+    (VBC_PLANAR_MASK=0) bit for bit and, in fp64, the oracle bit for bit -- Inf/NaN in x land where
+    the reference's loop puts them; alpha / beta."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
+    monkeypatch.setenv("VBC_PLANAR_PAIR", "0")
+    monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
+    base = V.synthetic.vbr_1dvbc(7000, 5000, 20000, w, W=8, dtype=dtype, seed=71 + w)
+    B = expand_runs(base, R, seed=72) if R > 1 else base
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    rng = np.random.default_rng(73)
+    x = rng.uniform(-1, 1, B.m).astype(dtype)
+    x[[3, 1500, B.m - 2]] = [np.inf, np.nan, -np.inf]
+    xf = np.nan_to_num(x, posinf=1.0, neginf=-1.0, nan=0.5)
+    y0 = rng.uniform(-1, 1, B.n).astype(dtype)
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    outs = {}
+    for mk in ("1", "0"):
+        monkeypatch.setenv("VBC_PLANAR_MASK", mk)
+        Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+        inf = Bc.info(trans=True)
+        assert inf["planar_bins"] == 1 and inf["planar_run"] == R and inf["planar_mask"] == int(mk)
+        y = torch.full((B.n,), 7.0, dtype=tdt, device=DEV)
+        V.mul_(y, Bc.T, dev(x))
+        outs[mk] = y.cpu().numpy()
+        yb = dev(y0.copy())
+        V.mul_(yb, Bc.T, dev(xf), 1.5, -0.5)
+        outs[mk + "ab"] = yb.cpu().numpy()
+        Bc.release()
+    assert np.array_equal(outs["1"], outs["0"], equal_nan=True)
+    assert np.array_equal(outs["1ab"], outs["0ab"])
+    ref = O.mul(R64, x.astype(np.float64), np.zeros(B.n), trans=True)
+    got = outs["1"].astype(np.float64)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    if dtype == np.float64:
+        assert np.array_equal(got[fin], ref[fin])
+    else:
+        assert np.array_equal(np.isinf(got[fin]), np.isinf(ref[fin]))
+    refab = O.mul(R64, xf.astype(np.float64), y0.astype(np.float64), 1.5, -0.5, trans=True, ref_semantics=False)
+    assert rel(outs["1ab"].astype(np.float64), refab) <= (TOL64 if dtype == np.float64 else TOL32)
