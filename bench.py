@@ -110,6 +110,9 @@ def kernel_name(B, local, k):
         if inf["planar_split"] > 1:
             return (f"vbc::spmv_planar_split<T, W, KC, RUN={inf['planar_run']}, P={inf['planar_split']}> "
                     "(split planar chunks, csrc/vbc_planar.h)")
+        if inf["planar_mask"]:
+            return (f"vbc::spmv_planar<T, W, false, 0, KC, RUN={inf['planar_run']}, MASK=true> "
+                    "(masked planar chunks, chunk-local length order, csrc/vbc_planar.h)")
         return (f"vbc::spmv_planar<T, W, FASTE, NB, KC, RUN={inf['planar_run']}> "
                 "(planar slotted chunks, csrc/vbc_planar.h)")
     if inf["sweep_bins"] > 0:

@@ -159,6 +159,7 @@ struct PendingSlot {
     int64_t key_bytes = 0;       // index bytes as stored (keys, deltas, bases, delta offsets)
     std::vector<uint32_t> keys;  // full keys until commit_slot_keys picks the stored form
     int64_t rows = 0;
+    int64_t real = 0;            // entries without padding
     bool kc_ok = false;          // every row's keys fit base + int16 deltas
 };
 
@@ -294,16 +295,18 @@ static std::vector<int64_t> permuted_sbeg(const std::vector<int64_t> &sbeg, cons
 // count within slots_pad of the real one and chunks short enough to balance over the ranges, first
 // in the natural segment order (affine y map), then sorted by length (y offsets from the table).
 // Returns 0 (merge layout), 1 (slotted, natural order) or 2 (slotted, `order`).
-// Chunk-local length order (SlotBin::mask): the RPI segments of each natural chunk by decreasing
-// length -- the chunk keeps its segments (x locality of the natural order), its live lanes at every
-// chunk row are a prefix, so the kernel can point the dead lanes at lane 0's lines.
-static std::vector<int64_t> chunk_sorted_order(const std::vector<int64_t> &sbeg, int RPI)
+// Chunk-local length order (SlotBin::mask): the segments of each window of `win` consecutive natural
+// segments (mask_window chunks) by decreasing length -- the window keeps its segments (most of the
+// x locality of the natural order: the sort over windows of 32 chunks lost it, FE-3D's x is fetched
+// ~10x), and every chunk row's live lanes are a prefix, so the kernel points the dead lanes at lane
+// 0's lines.
+static std::vector<int64_t> chunk_sorted_order(const std::vector<int64_t> &sbeg, int win)
 {
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     std::vector<int64_t> ord(nseg);
     for (int64_t i = 0; i < nseg; i++) ord[i] = i;
-    for (int64_t a = 0; a < nseg; a += RPI)
-        std::stable_sort(ord.begin() + a, ord.begin() + std::min(nseg, a + RPI), [&](int64_t p, int64_t q) {
+    for (int64_t a = 0; a < nseg; a += win)
+        std::stable_sort(ord.begin() + a, ord.begin() + std::min(nseg, a + win), [&](int64_t p, int64_t q) {
             return sbeg[p + 1] - sbeg[p] > sbeg[q + 1] - sbeg[q];
         });
     return ord;
@@ -341,7 +344,7 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
     const double share_p = (double)h->target_ranges_p * (double)real / (double)std::max<int64_t>(total_entries, 1);
     const bool split_likely = h->planar_split != 0 && (double)((nseg + RPI - 1) / RPI) * 4 <= share_p;
     if (mask && kind == 0 && h->planar_mask != 0 && slot_planar(h, 0, w) && !split_likely) {
-        order = chunk_sorted_order(sbeg, RPI);
+        order = chunk_sorted_order(sbeg, RPI * h->mask_window);
         pad_limit = kMaskPad;
         if (fits(permuted_sbeg(sbeg, order), h->slots_mode == 1)) {
             *mask = true;
@@ -503,6 +506,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     else range0 += (int)nr;
     const int64_t E = rows * RPI;
     ps.rows = rows;
+    ps.real = real;
     ps.keys.resize(E);
     ps.o_val = ar.reserve(E * w * esz * (pair ? 3 : 1));
     ps.o_out = ar.reserve(std::max<size_t>(out.size(), 1) * 4);
@@ -829,8 +833,14 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         pbs.push_back(pb);
     }
     commit_launch_keys(h, pss, ar);
-    for (const PendingSlot &ps : pss)  // slotted bins: padded rows x (index bytes + values)
-        h->bytes_t += ps.rows * ps.b.rpi * (int64_t)ps.b.w * h->esz + ps.key_bytes;
+    for (const PendingSlot &ps : pss) {  // slotted bins: padded rows x (index bytes + values)
+        if (ps.b.mask) {  // masked: padding lanes fetch nothing; + the per-row live counts
+            const double f = (double)ps.real / (double)std::max<int64_t>(1, ps.rows * ps.b.rpi);
+            h->bytes_t += ps.real * (int64_t)ps.b.w * h->esz + (int64_t)(f * (double)ps.key_bytes) + ps.rows * 4;
+        } else {
+            h->bytes_t += ps.rows * ps.b.rpi * (int64_t)ps.b.w * h->esz + ps.key_bytes;
+        }
+    }
     L.total_ranges = range0;
     L.slot_ranges = srange0;
     L.sweep_tiles = tile0;
@@ -1428,6 +1438,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
     if (const char *e = getenv("VBC_PLANAR_PAIR")) h->planar_pair = atoi(e) == 0 ? 0 : atoi(e) == 2 ? 2 : 1;  // 2: always
     if (const char *e = getenv("VBC_PLANAR_MASK")) h->planar_mask = atoi(e) != 0;
+    if (const char *e = getenv("VBC_MASK_WINDOW")) h->mask_window = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;

@@ -431,8 +431,8 @@ def test_forward_row_runs_fallback():
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("w,R", [(3, 3), (5, 1), (6, 3)])
-@pytest.mark.parametrize("keys16", ["0", "1"])
-def test_masked_chunk_order(monkeypatch, dtype, w, R, keys16):
+@pytest.mark.parametrize("keys16,win", [("0", "1"), ("1", "2"), ("1", "3")])
+def test_masked_chunk_order(monkeypatch, dtype, w, R, keys16, win):
     """Masked planar layout (SlotBin::mask): each natural chunk's 64 stripes in decreasing length
     order, dead lanes of a chunk row reading lane 0's lines and folding nothing.  Every stripe still
     folds its rows serially in stored order, so the result equals the length-sorted layout
@@ -441,6 +441,7 @@ def test_masked_chunk_order(monkeypatch, dtype, w, R, keys16):
     monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
     monkeypatch.setenv("VBC_PLANAR_PAIR", "0")
     monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
+    monkeypatch.setenv("VBC_MASK_WINDOW", win)  # stripes sorted by length inside windows of `win` chunks
     base = V.synthetic.vbr_1dvbc(7000, 5000, 20000, w, W=8, dtype=dtype, seed=71 + w)
     B = expand_runs(base, R, seed=72) if R > 1 else base
     R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
