@@ -489,7 +489,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.run = run;
     b.split = split;
     b.pair = pair ? 1 : 0;
-    b.mask = (mask && planar && !pair && split == 1) ? 1 : 0;
+    b.mask = (mask && planar && split == 1 && (!pair || h->planar_mask_pair)) ? 1 : 0;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -525,6 +525,17 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
                 const uint32_t last = qr + 1 == cr[c] ? kLast : 0u;
                 double *blk = dv + row * 288;
+                if (b.mask) {  // live stripe slots of this run-row: a prefix in chunk-local length order
+                    uint32_t nl = 0;
+                    for (int sl = 0; sl < 32; sl++) {
+                        const int64_t seg = c * 32 + sl;
+                        if (seg < nseg && sbeg[seg] + 3 * qr < sbeg[seg + 1]) {
+                            if (nl != (uint32_t)sl) return fail(VBC_INVALID_ARG, "masked pair chunk: live slots not a prefix");
+                            nl++;
+                        }
+                    }
+                    ar.at<uint32_t>(ps.o_nlive)[row] = nl;
+                }
                 for (int sl = 0; sl < 32; sl++) {
                     const int64_t seg = c * 32 + sl, e = row * 32 + sl;
                     const bool real_run = seg < nseg && sbeg[seg] + 3 * qr < sbeg[seg + 1];
@@ -1438,6 +1449,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
     if (const char *e = getenv("VBC_PLANAR_PAIR")) h->planar_pair = atoi(e) == 0 ? 0 : atoi(e) == 2 ? 2 : 1;  // 2: always
     if (const char *e = getenv("VBC_PLANAR_MASK")) h->planar_mask = atoi(e) != 0;
+    if (const char *e = getenv("VBC_PLANAR_MASK_PAIR")) h->planar_mask_pair = atoi(e) != 0;
     if (const char *e = getenv("VBC_MASK_WINDOW")) h->mask_window = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
         const int v = atoi(e);

@@ -121,6 +121,7 @@ struct vbc_handle {
     int planar_pair = 1;              // VBC_PLANAR_PAIR: 0 never, 1 auto (>= 8 runs per stripe), 2 always (fp64 w = 3 runs)
     int planar_mask = 1;              // VBC_PLANAR_MASK: planar B'x buckets whose natural order pads > slots_pad: 1 masked
                                       // chunk-local length order (SlotBin::mask), 0 length-sorted windows of 32 chunks
+    int planar_mask_pair = 1;         // VBC_PLANAR_MASK_PAIR=0: the lane-pair kernel folds its padding rows (no nlive)
     int mask_window = 2;              // VBC_MASK_WINDOW: chunks per length-sort window of the masked order (a prefix
                                       // of live lanes holds in every chunk of a window sorted by decreasing length;
                                       // fe3d fp64 1 / 2 / 4 / 8: 284 / 276 / 284 / 287 us, fp32 145 / 145 / 152 / 159,

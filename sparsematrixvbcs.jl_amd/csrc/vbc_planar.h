@@ -426,7 +426,9 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin *
 // stripe, 288 values, no padding): A = 64 lanes x {r0c0, r0c1 | r0c2, r1c2}, B = 32 x {r1c0, r1c1},
 // C = 32 x r2c2, D = 32 x {r2c0, r2c1}; three dwordx4 loads per lane per run-row (the odd lane's
 // second one reads C and its neighbour, its third the even partner's D line: merged requests).
-template <int NRS, bool FASTE, int NB, bool KC>
+// MASK (SlotBin::mask): stripe slots >= nlive[run-row] are padding; their lanes read pair 0's keys and
+// values (lane parity kept) and fold nothing.
+template <int NRS, bool FASTE, int NB, bool KC, bool MASK = false>
 __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, const double *__restrict__ x,
                                          double *__restrict__ y, double alpha, double beta, bool rd, char *lds_wave,
                                          int *lds_out)
@@ -443,23 +445,33 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
     typedef __attribute__((address_space(4))) const uint32_t *cptr;
     const cptr bases = (cptr)b.base;
     const cptr doffs = (cptr)b.kdoff;
+    const cptr nlive = (cptr)b.nlive;
     // per-lane element offsets of the three value loads inside a run-row
     const int o0 = 2 * lane, o1 = odd ? 192 + ps : 128 + 2 * ps, o2 = 224 + 2 * ps;
-    auto load = [&](int R, uint32_t (&kk)[NRS], uint32_t (&bs)[NRS], d2 (&v)[NRS][3]) {
+    auto load = [&](int R, uint32_t (&kk)[NRS], uint32_t (&bs)[NRS], int (&nl)[NRS], d2 (&v)[NRS][3]) {
 #pragma unroll
         for (int j = 0; j < NRS; j++) {
             const int Rc = min(R + j, R1 - 1);
+            int mps = ps, m0 = o0, m1 = o1, m2 = o2;
+            if constexpr (MASK) {  // dead pairs: pair 0's addresses (lane parity kept)
+                nl[j] = (int)nlive[Rc];
+                const bool dead = ps >= nl[j];
+                mps = dead ? 0 : ps;
+                m0 = dead ? (odd ? 1 : 0) * 2 : o0;
+                m1 = dead ? (odd ? 192 : 128) : o1;
+                m2 = dead ? 224 : o2;
+            }
             if constexpr (KC) {
-                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + ps];
+                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + mps];
                 bs[j] = bases[Rc];
             } else {
-                kk[j] = key[(size_t)Rc * 32 + ps];
+                kk[j] = key[(size_t)Rc * 32 + mps];
                 bs[j] = 0;
             }
             const gptr<const double> rowp = val + (size_t)Rc * 288;
-            v[j][0] = __builtin_nontemporal_load((gptr<const d2>)(rowp + o0));
-            v[j][1] = *(const __attribute__((address_space(1))) d2 *)(rowp + o1);  // 8-B aligned (odd lanes)
-            v[j][2] = __builtin_nontemporal_load((gptr<const d2>)(rowp + o2));
+            v[j][0] = __builtin_nontemporal_load((gptr<const d2>)(rowp + m0));
+            v[j][1] = *(const __attribute__((address_space(1))) d2 *)(rowp + m1);  // 8-B aligned (odd lanes)
+            v[j][2] = __builtin_nontemporal_load((gptr<const d2>)(rowp + m2));
         }
     };
     constexpr uint32_t kPad16 = 0xFFFF8000u;
@@ -533,12 +545,12 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
     };
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
-    auto compute = [&](int R, const uint32_t (&kk)[NRS], const uint32_t (&bs)[NRS], const d2 (&v)[NRS][3],
-                       const d2 (&xv)[NRS]) {
+    auto compute = [&](int R, const uint32_t (&kk)[NRS], const uint32_t (&bs)[NRS], const int (&nl)[NRS],
+                       const d2 (&v)[NRS][3], const d2 (&xv)[NRS]) {
 #pragma unroll
         for (int j = 0; j < NRS; j++) {
-            const bool live = R + j < R1v;
-            const bool pad = KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0;
+            const bool pad = MASK ? ps >= nl[j] : (KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0);
+            const bool live = R + j < R1v && !(MASK && pad);  // MASK: pair 0's values, never folded
             // even sends x[g] (its .x), odd sends x[g+2] (its .y); each receives the element it lacks
             const double t = odd ? xv[j].y : xv[j].x;
             const uint64_t tb = __builtin_bit_cast(uint64_t, t);
@@ -559,23 +571,24 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
         }
     };
     uint32_t kA[NRS], kB[NRS], bA[NRS], bB[NRS];
+    int nA[NRS], nB[NRS];
     d2 vA[NRS][3], vB[NRS][3], xv[NRS];
-    load(R0, kA, bA, vA);
+    load(R0, kA, bA, nA, vA);
     __builtin_amdgcn_s_waitcnt(0);
     for (int R = R0; R < R1; R += 2 * NRS) {
         gather(kA, bA, xv);
-        load(R + NRS, kB, bB, vB);
-        compute(R, kA, bA, vA, xv);
+        load(R + NRS, kB, bB, nB, vB);
+        compute(R, kA, bA, nA, vA, xv);
         gather(kB, bB, xv);
-        load(R + 2 * NRS, kA, bA, vA);
-        compute(R + NRS, kB, bB, vB, xv);
+        load(R + 2 * NRS, kA, bA, nA, vA);
+        compute(R + NRS, kB, bB, nB, vB, xv);
     }
     if constexpr (NB > 0) {
         if (nbuf > 0) write_out();
     }
 }
 
-template <bool FASTE, int NB, bool KC>
+template <bool FASTE, int NB, bool KC, bool MASK = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin *__restrict__ bp,
                                                                   const double *__restrict__ x, double *__restrict__ y,
                                                                   double alpha, double beta, int rd_i)
@@ -592,7 +605,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin 
 #ifndef VBC_PAIR_NRS
 #define VBC_PAIR_NRS 4  // run-rows per pipeline stage (ldoor stand-in: 2 -> 82, 3 -> 80, 4 -> 77 us)
 #endif
-    run_pair<VBC_PAIR_NRS, FASTE, NB, KC>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
+    run_pair<VBC_PAIR_NRS, FASTE, NB, KC, MASK>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
 }
 
 // Split planar product (SlotBin::split = P > 1; ranges are single chunks): workgroup c = chunk c, wave k

@@ -90,7 +90,10 @@ static int launch_pair(const SlotBin &hb, const SlotBin *d_b, bool faste, bool s
     const int grid = (hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const double *xs = static_cast<const double *>(x);
     double *ys = static_cast<double *>(y);
-    if (faste && staged)
+    if (hb.mask)
+        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+                           alpha, beta, (int)rd);
+    else if (faste && staged)
         hipLaunchKernelGGL((spmv_planar_pair<true, 8, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
                            beta, (int)rd);
     else if (faste)

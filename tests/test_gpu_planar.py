@@ -476,3 +476,50 @@ def test_masked_chunk_order(monkeypatch, dtype, w, R, keys16, win):
         assert np.array_equal(np.isinf(got[fin]), np.isinf(ref[fin]))
     refab = O.mul(R64, xf.astype(np.float64), y0.astype(np.float64), 1.5, -0.5, trans=True, ref_semantics=False)
     assert rel(outs["1ab"].astype(np.float64), refab) <= (TOL64 if dtype == np.float64 else TOL32)
+
+
+@pytest.mark.parametrize("keys16", ["0", "1"])
+@pytest.mark.parametrize("win", ["1", "2"])
+def test_masked_pair_layout(monkeypatch, keys16, win):
+    """Lane-pair layout (fp64, 3-wide stripes, runs of 3) in the masked chunk-local order: padding
+    stripe slots of a run-row read pair 0's lines and fold nothing.  Same bits as the unmasked pair
+    kernel on the same order (VBC_PLANAR_MASK_PAIR=0), as the plain planar layout, and as the oracle;
+    Inf/NaN in x; alpha / beta."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
+    monkeypatch.setenv("VBC_PLANAR_PAIR", "2")
+    monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
+    monkeypatch.setenv("VBC_MASK_WINDOW", win)
+    base = V.synthetic.vbr_1dvbc(9000, 4000, 16000, 3, W=8, seed=81)  # ~4 runs per stripe: pads naturally
+    B = expand_runs(base, 3, seed=82)
+    R = ref_of(B)
+    rng = np.random.default_rng(83)
+    x = rng.uniform(-1, 1, B.m)
+    x[[5, 3001, 20000]] = [np.inf, np.nan, -np.inf]
+    xf = np.nan_to_num(x, posinf=1.0, neginf=-1.0, nan=0.5)
+    y0 = rng.uniform(-1, 1, B.n)
+    outs = {}
+    for tag, env in (("mask", {}), ("nomask", {"VBC_PLANAR_MASK_PAIR": "0"}), ("plain", {"VBC_PLANAR_PAIR": "0"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+        inf = Bc.info(trans=True)
+        assert inf["planar_pair"] == (tag != "plain") and inf["planar_mask"] == (tag != "nomask")
+        y = torch.full((B.n,), 3.0, dtype=torch.float64, device=DEV)
+        V.mul_(y, Bc.T, dev(x))
+        outs[tag] = y.cpu().numpy()
+        yb = dev(y0.copy())
+        V.mul_(yb, Bc.T, dev(xf), 0.75, -1.25)
+        outs[tag + "ab"] = yb.cpu().numpy()
+        Bc.release()
+        for k in env:
+            monkeypatch.delenv(k)
+    ref = O.mul(R, x, np.zeros(B.n), trans=True)
+    got = outs["mask"]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    assert np.array_equal(got[fin], ref[fin])
+    for t in ("nomask", "plain"):
+        assert np.array_equal(outs[t], got, equal_nan=True)
+        assert np.array_equal(outs[t + "ab"], outs["maskab"])
+    refab = O.mul(R, xf, y0.copy(), 0.75, -1.25, trans=True, ref_semantics=False)
+    assert rel(outs["maskab"], refab) <= TOL64
