@@ -105,8 +105,8 @@ def kernel_name(B, local, k):
     inf = B.info(local, True)
     if inf["planar_bins"] > 0:
         if inf["planar_pair"]:
-            return ("vbc::spmv_planar_pair<FASTE, NB, KC> (lane pairs, fp64 3-wide runs of 3, "
-                    "csrc/vbc_planar.h)")
+            return ("vbc::spmv_planar_pair<FASTE, NB, KC, MASK> (lane pairs, fp64 3-wide runs of 3"
+                    + (", masked chunk-local order" if inf["planar_mask"] else "") + ", csrc/vbc_planar.h)")
         if inf["planar_split"] > 1:
             return (f"vbc::spmv_planar_split<T, W, KC, RUN={inf['planar_run']}, P={inf['planar_split']}> "
                     "(split planar chunks, csrc/vbc_planar.h)")
