@@ -227,7 +227,8 @@ typedef struct vbc_info {
     int32_t planar_split;   /* waves per chunk of the split planar product (1 = one wave per range) */
     int32_t planar_pair;    /* 1: fp64 3-wide runs laid out for lane pairs (one 16-B gather per lane) */
     int32_t fwd_run;        /* forward product: output rows in runs of fwd_run share one x-slice gather */
-    int32_t planar_mask;    /* 1: a B'x planar bucket in masked chunk-local length order (padding lanes fetch nothing) */
+    int32_t planar_mask;    /* bit 0: a B'x planar bucket, bit 1: the forward planar bucket, in masked chunk-local
+                               length order (padding lanes fetch nothing) */
 } vbc_info;
 
 VBC_API int vbc_get_info(const vbc_handle *h, vbc_info *info);

@@ -905,13 +905,23 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
     int64_t rows = 0;
     for (int32_t c : cr) rows += c;
     if (real == 0) return false;
+    bool mask = false;
     if ((double)(rows * RPI) > h->slots_pad * (double)real) {
         if (h->slots_sort == 0) return false;
-        order = sorted_order(rb, RPI);
-        cr = chunk_rows(permuted_sbeg(rb, order), RPI);
-        rows = 0;
-        for (int32_t c : cr) rows += c;
-        if ((double)(rows * RPI) > h->slots_pad * (double)real) return false;
+        if (h->planar_mask != 0) {  // masked chunk-local length order (SlotBin::mask, as the B'x planar bins)
+            order = chunk_sorted_order(rb, RPI * h->mask_window);
+            cr = chunk_rows(permuted_sbeg(rb, order), RPI);
+            rows = 0;
+            for (int32_t c : cr) rows += c;
+            mask = (double)(rows * RPI) <= kMaskPad * (double)real;
+        }
+        if (!mask) {
+            order = sorted_order(rb, RPI);
+            cr = chunk_rows(permuted_sbeg(rb, order), RPI);
+            rows = 0;
+            for (int32_t c : cr) rows += c;
+            if ((double)(rows * RPI) > h->slots_pad * (double)real) return false;
+        }
     }
     auto seg_of = [&](int64_t p) { return order.empty() ? p : order[p]; };  // layout position -> run-segment
     const int64_t nr = std::max<int64_t>(1, std::min<int64_t>(h->target_ranges_p, nch));
@@ -943,12 +953,15 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
     b.run = R;
     b.split = 1;
     b.pair = 0;
+    b.mask = mask ? 1 : 0;
     b.out_affine = order.empty() ? 1 : 0;
     b.out_base = 0;
     b.out_stride = R;
     b.contig = b.out_affine;
     const int64_t E = rows * RPI;
     ps.rows = rows;
+    ps.real = real;
+    if (mask) ps.o_nlive = ar.reserve((size_t)rows * 4);
     ps.keys.resize(E);
     ps.o_val = ar.reserve(E * WV * esz);
     ps.o_out = ar.reserve(std::max<int64_t>(order.size(), 1) * 4);
@@ -963,6 +976,17 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
         for (int32_t k = 0; k < cr[c]; k++, row++) {
             const uint32_t last = k + 1 == cr[c] ? kLast : 0u;
             char *rowp = vv + row * RPI * WV * esz;
+            if (mask) {  // live lanes of this chunk row: a prefix in chunk-local length order
+                uint32_t nl = 0;
+                for (int sl = 0; sl < RPI; sl++) {
+                    const int64_t p = c * RPI + sl;
+                    if (p < nseg && sbeg[R * seg_of(p)] + k < sbeg[R * seg_of(p) + 1]) {
+                        if (nl != (uint32_t)sl) return false;
+                        nl++;
+                    }
+                }
+                ar.at<uint32_t>(ps.o_nlive)[row] = nl;
+            }
             for (int sl = 0; sl < RPI; sl++) {
                 const int64_t p = c * RPI + sl, e = row * RPI + sl;
                 const int64_t q = p < nseg ? seg_of(p) : 0;
@@ -1770,7 +1794,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->fwd_run = 1;
     if (h->has_f)
         for (const auto &l : h->lf)
-            for (const auto &b : l.pbins) info->fwd_run = std::max<int32_t>(info->fwd_run, b.run);
+            for (const auto &b : l.pbins) {
+                info->fwd_run = std::max<int32_t>(info->fwd_run, b.run);
+                if (b.mask) info->planar_mask |= 2;
+            }
     info->bytes_m = h->bytes_m;
     return VBC_OK;
 }

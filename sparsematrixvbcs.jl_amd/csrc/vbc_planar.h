@@ -280,7 +280,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
 // of R), and adds the R dot products to its R accumulators, blocks in stripe order as the reference's
 // serial stripe loop (:62-71).  At the LAST row the lane writes y[R*q .. R*q+R-1] (contiguous, LDS-
 // staged in runs of NB chunks when FASTE).
-template <typename T, int W_, int R, int U, bool FASTE, int NB, bool KC>
+// MASK (SlotBin::mask): lanes >= nlive[row] read lane 0's key and values and add nothing.
+template <typename T, int W_, int R, int U, bool FASTE, int NB, bool KC, bool MASK = false>
 __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane, const T *__restrict__ x,
                                                T *__restrict__ y, T alpha, T beta, bool rd, char *lds_wave)
 {
@@ -294,18 +295,24 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
     typedef __attribute__((address_space(4))) const uint32_t *cptr;
     const cptr bases = (cptr)b.base;
     const cptr doffs = (cptr)b.kdoff;
-    auto load = [&](int Rr, uint32_t (&kk)[U], uint32_t (&bs)[U], T (&v)[U][WV]) {
+    const cptr nlive = (cptr)b.nlive;
+    auto load = [&](int Rr, uint32_t (&kk)[U], uint32_t (&bs)[U], int (&nl)[U], T (&v)[U][WV]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int Rc = min(Rr + u, R1 - 1);
+            int ln = lane;
+            if constexpr (MASK) {
+                nl[u] = (int)nlive[Rc];
+                ln = lane < nl[u] ? lane : 0;
+            }
             if constexpr (KC) {
-                kk[u] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + lane];
+                kk[u] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rc] + ln];
                 bs[u] = bases[Rc];
             } else {
-                kk[u] = __builtin_nontemporal_load(key + (size_t)Rc * 64 + lane);
+                kk[u] = __builtin_nontemporal_load(key + (size_t)Rc * 64 + ln);
                 bs[u] = 0;
             }
-            ld_row<T, WV, 0>(val + (size_t)Rc * 64 * WV, lane, v[u]);
+            ld_row<T, WV, 0>(val + (size_t)Rc * 64 * WV, ln, v[u]);
         }
     };
     constexpr uint32_t kPad16 = 0xFFFF8000u;
@@ -363,12 +370,12 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
     };
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
-    auto compute = [&](int Rr, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const T (&v)[U][WV],
-                       const T (&xv)[U][W_]) {
+    auto compute = [&](int Rr, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const int (&nl)[U],
+                       const T (&v)[U][WV], const T (&xv)[U][W_]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const bool live = Rr + u < R1v;
-            const bool pad = KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0;
+            const bool pad = MASK ? lane >= nl[u] : (KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0);
 #pragma unroll
             for (int q = 0; q < R; q++) {  // one dot product per output row of the run
                 T d = v[u][q * W_] * xv[u][0];
@@ -381,23 +388,24 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
         }
     };
     uint32_t kA[U], kB[U], bA[U], bB[U];
+    int nA[U], nB[U];
     T vA[U][WV], vB[U][WV], xv[U][W_];
-    load(R0, kA, bA, vA);
+    load(R0, kA, bA, nA, vA);
     __builtin_amdgcn_s_waitcnt(0);
     for (int Rr = R0; Rr < R1; Rr += 2 * U) {
         gather(kA, bA, xv);
-        load(Rr + U, kB, bB, vB);
-        compute(Rr, kA, bA, vA, xv);
+        load(Rr + U, kB, bB, nB, vB);
+        compute(Rr, kA, bA, nA, vA, xv);
         gather(kB, bB, xv);
-        load(Rr + 2 * U, kA, bA, vA);
-        compute(Rr + U, kB, bB, vB, xv);
+        load(Rr + 2 * U, kA, bA, nA, vA);
+        compute(Rr + U, kB, bB, nB, vB, xv);
     }
     if constexpr (NB > 0) {
         if (nbuf > 0) write_out();
     }
 }
 
-template <typename T, int W_, int R, bool FASTE, int NB, bool KC>
+template <typename T, int W_, int R, bool FASTE, int NB, bool KC, bool MASK = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin *__restrict__ bp, const T *__restrict__ x,
                                                                  T *__restrict__ y, T alpha, T beta, int rd_i)
 {
@@ -413,7 +421,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin *
 #endif
     // blocks per stage: ~VBC_FWD_VALS values per lane (fp64 R = 3, w = 3: 2 blocks)
     constexpr int U = (VBC_FWD_VALS / (R * W_)) < 2 ? 2 : (VBC_FWD_VALS / (R * W_));
-    run_planar_fwd<T, W_, R, U, FASTE, NB, KC>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds);
+    run_planar_fwd<T, W_, R, U, FASTE, NB, KC, MASK>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds);
 }
 
 // Lane-pair planar product (SlotBin::pair: fp64, 3-wide stripes, rows in runs of 3 -- a 3-dof

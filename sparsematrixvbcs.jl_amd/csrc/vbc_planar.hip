@@ -113,7 +113,10 @@ static void launch_fwd_wr(const SlotBin &hb, const SlotBin *d_b, bool faste, boo
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
     constexpr int NB = (8192 / (64 * R * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * R * (int)sizeof(T)));
-    if (faste && staged)
+    if (hb.mask)
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs,
+                           ys, (T)alpha, (T)beta, (int)rd);
+    else if (faste && staged)
         hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, NB, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else if (faste)

@@ -523,3 +523,48 @@ def test_masked_pair_layout(monkeypatch, keys16, win):
         assert np.array_equal(outs[t + "ab"], outs["maskab"])
     refab = O.mul(R, xf, y0.copy(), 0.75, -1.25, trans=True, ref_semantics=False)
     assert rel(outs["maskab"], refab) <= TOL64
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w,R", [(3, 3), (2, 2)])
+def test_forward_masked_order(monkeypatch, dtype, w, R):
+    """Forward planar product with row runs in the masked chunk-local order (rows with uneven block
+    counts): same bits as the length-sorted layout (VBC_PLANAR_MASK=0) -- each output row still sums
+    its blocks in stripe order -- and the oracle's forward product (multiply_1DVBC.jl:9-83); integer
+    data bit for bit."""
+    rng = np.random.default_rng(90 + w + R)
+    base = V.synthetic.vbr_1dvbc(6000, 1500, 9000, w, W=8, dtype=dtype, seed=91 + w)
+    At = sp_blocked(base, R, rng, dtype)
+    B = V.SparseMatrix1DVBC[8](At, V.EquiChunker(w))
+    vi = rng.integers(-30, 30, len(B.val)).astype(dtype)
+    x = rng.uniform(-1, 1, B.n).astype(dtype)
+    xi = rng.integers(-20, 20, B.n).astype(dtype)
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    outs = {}
+    for mk in ("1", "0"):
+        monkeypatch.setenv("VBC_PLANAR_MASK", mk)
+        Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+        inf = Bc.info(trans=False)
+        assert ((inf["planar_mask"] >> 1) & 1) == int(mk)
+        if mk == "1":
+            assert inf["fwd_run"] == R
+        runs0 = inf["fwd_run"] == R  # mk = 0: the sorted run layout, or the row-by-row fallback
+        y = torch.zeros(B.m, dtype=tdt, device=DEV)
+        V.mul_(y, Bc, dev(x))
+        outs[mk] = y.cpu().numpy()
+        Bc.release()
+        Bi = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, vi)
+        yi = torch.zeros(B.m, dtype=tdt, device=DEV)
+        V.mul_(yi, Bi, dev(xi))
+        outs[mk + "i"] = yi.cpu().numpy()
+        Bi.release()
+    if runs0:  # same per-row block order and per-block dot product
+        assert np.array_equal(outs["1"], outs["0"])
+    assert np.array_equal(outs["1i"], outs["0i"])
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    assert rel(outs["0"].astype(np.float64), O.mul(R64, x.astype(np.float64), np.zeros(B.m))) <= \
+        (TOL64 if dtype == np.float64 else TOL32)
+    assert rel(outs["1"].astype(np.float64), O.mul(R64, x.astype(np.float64), np.zeros(B.m))) <= \
+        (TOL64 if dtype == np.float64 else TOL32)
+    Ri = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, vi.astype(np.float64))
+    assert np.array_equal(outs["1i"].astype(np.float64), O.mul(Ri, xi.astype(np.float64), np.zeros(B.m)))
