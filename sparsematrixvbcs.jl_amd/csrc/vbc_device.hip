@@ -342,7 +342,9 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
     if (h->slots_sort == 0) return 0;
     // (not for buckets small enough for the split product, which folds every padding row: build_slots)
     const double share_p = (double)h->target_ranges_p * (double)real / (double)std::max<int64_t>(total_entries, 1);
-    const bool split_likely = h->planar_split != 0 && (double)((nseg + RPI - 1) / RPI) * 4 <= share_p;
+    // (P >= 4; a masked bucket skips P = 2: ldoor's 1/8 stripe shard, 615 chunks, masked lane pairs
+    // 15.3 us vs split P = 2 16.3 us; the ct20stif stand-in, 273 chunks, keeps P = 4: 10.9 vs 12.8 us)
+    const bool split_likely = h->planar_split != 0 && (double)((nseg + RPI - 1) / RPI) * 8 <= share_p;
     if (mask && kind == 0 && h->planar_mask != 0 && slot_planar(h, 0, w) && !split_likely) {
         order = chunk_sorted_order(sbeg, RPI * h->mask_window);
         pad_limit = kMaskPad;
@@ -428,11 +430,12 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             else  // P waves per chunk while the grid stays within half the wave slots (ct20stif stand-in:
                   // P = 4 10.6 us vs 8 11.2; ldoor's 1/8 stripe shard: P = 2 16.3 us vs 4 17.3, 8 18.7, 1 20.0)
                 while (split < 8 && (double)nch * split * 2 * 2 <= share) split *= 2;
+            if (mask && split == 2 && h->planar_split < 0) split = 1;  // masked: P = 2 measured slower
         }
         // the split product runs the plain planar layout; so does a pair layout that would fill fewer than
         // half the wave slots, when the split product may be chosen instead (ldoor's 1/8 shard: 1250 pair
         // chunks 21.8 us, planar split 16.3 us)
-        const bool drop = pair && (split > 1 || (h->planar_pair != 2 && h->planar_split != 0 && 2.0 * (double)nch < share));
+        const bool drop = pair && (split > 1 || (!mask && h->planar_pair != 2 && h->planar_split != 0 && 2.0 * (double)nch < share));
         if (!drop) break;
         pair = false;
     }
