@@ -36,6 +36,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
 METRIC = "1DVBC SpMV effective GB/s (and GFLOP/s) vs HBM roofline, 1/2/4/8 GPU"
 PARITY_TOL = {np.dtype(np.float64): 1e-10, np.dtype(np.float32): 1e-5}  # normwise rel-err (BASELINE)
 
@@ -272,8 +273,11 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     ms_per_step = elapsed / steps * 1e3
     achieved = bytes_roof / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload, "f64" if dtype == np.float64 else "f32")
+    layout_bytes = int(B.info(local, True, multi=k > 1)["device_bytes"])
     out = {
-        "value": round(bytes_launch * steps / elapsed / 1e9, 2),
+        # TrSpMV! on a CSC: priced on the bytes its blocked layout moves, so `value` is a bandwidth
+        # (the CSC byte formula divided by the same time is reported apart as `csc_equivalent_GBs`)
+        "value": round(bytes_roof * steps / elapsed / 1e9, 2),
         "unit": "GB/s",
         "ms_per_step": round(ms_per_step, 5),
         "gflops": round(2.0 * nnz * k * steps / elapsed / 1e9, 2),
@@ -291,14 +295,18 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
             "m": B.m, "n": B.n, "stripes": B.n if csc else len(B.Phi),
             "row_blocks": nnz if csc else int(B.pos[-1] - 1), "nnz": nnz, "W": 1 if csc else B.W,
             "index_bytes": 4, "nrhs": k, "launch": "hipGraph of K products" if graphed else "eager",
-            "build_s": round(t_build, 1),
+            "build_s": round(t_build, 1), "layout_bytes": layout_bytes,
+            "cache": ("warm, matrix < MALL: the layout fits the 256 MB Infinity Cache, so back-to-back "
+                      "products may be served partly from it rather than HBM") if layout_bytes < MALL_BYTES
+                     else "matrix > MALL: every product streams the layout from HBM",
         },
         "dtype": "f64" if dtype == np.float64 else "f32",
     }
     if csc:
         out["roofline"]["bytes_csc_formula"] = bytes_launch
+        out["csc_equivalent_GBs"] = round(bytes_launch * steps / elapsed / 1e9, 2)
     if with_parity:
-        out["parity"] = parity(B, x_host, y, k, cols=(0, k - 1) if k > 1 else (0,))
+        out["parity"] = parity(B, x_host, y, k, cols=tuple(range(k)) if k > 1 else (0,))
     if with_cpu:
         out["cpu_baseline"] = cpu_baseline(B, x_host, esz)
     B.release()
@@ -413,6 +421,37 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
     return out
 
 
+def launch_ranks(n):
+    """Run this script as ranks 0..n-1 (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, as
+    torch.distributed.run sets them) in child processes; returns the first nonzero exit status."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    while True:  # a rank that fails would leave the others waiting in a collective: stop them
+        codes = [p.poll() for p in procs]
+        bad = next((c for c in codes if c not in (None, 0)), None)
+        if bad is not None:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            return bad
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(0.2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -432,6 +471,12 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary workloads")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: start the N ranks ourselves, one process per GPU (what
+        # torchrun does), before this process touches a GPU; rank 0 prints the line, we exit with
+        # the worst status
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -471,7 +516,10 @@ def main():
                            "ms_per_step": s["ms_per_step"], "gflops": s["gflops"], "dtype": s["dtype"],
                            "roofline_frac": s["roofline"]["frac"], "kernel": s["roofline"]["kernel"],
                            "kernel_us": round(s["roofline"]["avg_launch_ms"] * 1e3, 1),
-                           "bytes_per_launch": s["roofline"]["bytes_per_launch"], "op": s["config"]["op"]}
+                           "bytes_per_launch": s["roofline"]["bytes_per_launch"], "op": s["config"]["op"],
+                           "cache": s["config"]["cache"]}
+                if "csc_equivalent_GBs" in s:
+                    sec[wl]["csc_equivalent_GBs"] = s["csc_equivalent_GBs"]
                 if "parity" in s:
                     sec[wl]["rel_err"] = s["parity"]["rel_err"]
                     sec[wl]["parity_pass"] = s["parity"]["pass"]

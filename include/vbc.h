@@ -21,6 +21,12 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* ABI version (major*10000 + minor*100 + patch), returned by vbc_version().  A binding checks the major
+ * version at load time: 3.x changed vbc_info (VBC_INFO_SIZE bytes, written whole by vbc_get_info) and
+ * added the I64 / I32 / BOOL eltypes, the sharded 2D handle and the *_ex sharded product. */
+#define VBC_VERSION 30000
+#define VBC_INFO_SIZE 152
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -59,6 +65,11 @@ typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
                                       Y = α·B'X + β·Y on matrix cores (vbc_mul_mat, trans = 1,
                                       any operand layout; stripes wider than 16 are cut into
                                       16-column pieces).  Independent of the SpMV layouts. */
+#define VBC_CREATE_SERIAL 0x8u     /* keep the reference's serial per-stripe summation order in every
+                                      B'x layout (multiply_1DVBC.jl:101-104): no split planar product
+                                      (vbc_info.planar_split stays 1), so every output is bit-identical
+                                      to the oracle whatever the matrix size.  Default: small matrices
+                                      may fold a chunk's rows in P slices (rounding differs ~1 ulp). */
 
 /* mul flags */
 #define VBC_MAT_ROWMAJOR 0x2u         /* vbc_mul_mat: X, Y row-major (right-hand sides interleaved,
@@ -136,7 +147,9 @@ VBC_API int vbc_csc_create_ex(vbc_handle **out, int64_t m, int64_t n, const void
  * work.  mem = VBC_MEM_DEVICE: x, y are device pointers on the handle's device, and the product is
  * enqueued on `stream` (a hipStream_t; NULL = null stream) without synchronising.
  * mem = VBC_MEM_HOST: x, y are host pointers; the call stages them and returns when y is final.
- * x and y must not alias (the reference has the same precondition). */
+ * x and y must not alias (the reference has the same precondition).  x and y are contiguous vectors of
+ * the handle's compute eltype: this is the fast path for callers that know it (the Python mirror after
+ * its own eltype check); a binding that cannot guarantee it calls vbc_mul_ex, which carries them. */
 VBC_API int vbc_mul(vbc_handle *h, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
             double beta, int mem, void *stream, unsigned flags);
 
@@ -163,6 +176,13 @@ VBC_API int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, i
                 void *Y, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
                 unsigned flags);
 
+/* vbc_mul_mat with the eltypes of X and Y carried along: both must be the handle's compute eltype
+ * (VBC_UNSUPPORTED_DTYPE otherwise -- never read as another type); a binding with other eltypes runs
+ * vbc_mul_ex column by column, as the reference's per-column semantics allows. */
+VBC_API int vbc_mul_mat_ex(vbc_handle *h, int trans, int64_t nrhs, const void *X, int X_dtype, int64_t ldx,
+                           int64_t nx, void *Y, int Y_dtype, int64_t ldy, int64_t ny, double alpha, double beta,
+                           int mem, void *stream, unsigned flags);
+
 /* ---------------------------------------------------------------------------------------------
  * Multi-GPU (one process, several GPUs of a node; RCCL over xGMI).  SURVEY.md §8e.
  *
@@ -171,7 +191,10 @@ VBC_API int vbc_mul_mat(vbc_handle *h, int trans, int64_t nrhs, const void *X, i
  * balanced by HBM bytes, one single-GPU handle per device (vbc1d_create_ex on each slice).
  *   VBC_SPLIT_STRIPES: GPU g owns stripes [l_g, l_g+1) (columns [c_g, c_g+1) of B; block rows of A
  *     when B stores Aᵀ, as bin/test_table.jl:27 does).  B'x: x broadcast, y slices gathered to the
- *     root (disjoint, bit-identical to one GPU).  Bx: x slices scattered, ncclReduce(sum) of y.
+ *     root (disjoint; each stripe summed in stored row order, bit-identical to one GPU and to the
+ *     reference, unless a shard's layout runs the split planar product -- vbc_info.planar_split > 1,
+ *     small shards only -- which sums a chunk's rows in P slices; VBC_CREATE_SERIAL forbids it).
+ *     Bx: x slices scattered, ncclReduce(sum) of y.
  *   VBC_SPLIT_ROWS: GPU g owns the stored rows [r_g, r_g+1) of every stripe.  Bx: x broadcast, y slices
  *     gathered (disjoint).  B'x: x slices, ncclReduce(sum) of y.
  * devices: all distinct (one RCCL communicator per device, ncclCommInitAll) or all the same device
@@ -187,13 +210,35 @@ VBC_API int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_
                                  const void *pos, const void *idx, const void *ofs, const void *val, int64_t nval,
                                  const vbc_types *types, int ngpus, const int *devices, int split, unsigned flags);
 
-/* mul!(y, op(B), x, α, β) over all shards.  mem = VBC_MEM_DEVICE: x, y (compute eltype, contiguous) live
- * on devices[0] and the product -- collectives included -- is ordered on `stream` (a hipStream_t of
- * devices[0]) without host synchronisation.  mem = VBC_MEM_HOST: host x, y; returns when y is final.
- * Products of one sharded handle are issued one at a time (an internal lock keeps every GPU's
- * collective order identical). */
+/* SparseMatrixVBC{U,W,Tv,Ti} split the same way (its transposed product is threaded like the 1D one,
+ * multiply_VBC.jl:182-189).  Same matrix arguments as vbc2d_create_ex.
+ *   VBC_SPLIT_STRIPES: GPU g owns stripes [l_g, l_g+1) (Π kept whole);
+ *   VBC_SPLIT_ROWS:    GPU g owns the block rows [k_g, k_g+1) of Π (rows Π.spl[k_g]-1 ..), i.e. the
+ *                      tiles of every stripe whose block-row id falls in that range, stored order kept. */
+VBC_API int vbc2d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K,
+                                 const void *pspl, int64_t L, const void *spl, const void *pos, const void *idx,
+                                 const void *ofs, const void *val, int64_t nval, const vbc_types *types, int ngpus,
+                                 const int *devices, int split, unsigned flags);
+
+/* mul!(y, op(B), x, α, β) over all shards, operands of the compute eltype: the fast path for a caller
+ * that already holds contiguous x, y of that eltype (a binding that cannot guarantee it calls
+ * vbc_sharded_mul_ex, which carries the eltypes).  mem = VBC_MEM_DEVICE: x, y live on devices[0] and the
+ * product -- collectives included -- is ordered on `stream` (a hipStream_t of devices[0]) without host
+ * synchronisation.  mem = VBC_MEM_HOST: host x, y; returns when y is final.  Products of one sharded
+ * handle are issued one at a time (an internal lock keeps every GPU's collective order identical).
+ * A failure after the first collective of a product was enqueued leaves the handle FAILED: the
+ * communicators may hold a half-issued exchange, so every later product returns VBC_RCCL_ERROR
+ * (destroy and re-create the handle). */
 VBC_API int vbc_sharded_mul(vbc_sharded *s, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
                             double beta, int mem, void *stream, unsigned flags);
+
+/* mul!(y::StridedVector, op(B), x::StridedVector, α, β) on a sharded handle: eltypes and strides as
+ * vbc_mul_ex (x converted to the compute eltype, multiply_1DVBC.jl:9,85,102; y the compute eltype or
+ * Int32 on an integer handle; a mismatched eltype is converted or refused, never read as another
+ * type).  Non-contiguous or converted operands go through root staging buffers (device) or host copies. */
+VBC_API int vbc_sharded_mul_ex(vbc_sharded *s, int trans, const void *x, int x_dtype, int64_t incx, int64_t nx,
+                               void *y, int y_dtype, int64_t incy, int64_t ny, double alpha, double beta, int mem,
+                               void *stream, unsigned flags);
 
 VBC_API int vbc_sharded_destroy(vbc_sharded *s);
 VBC_API int vbc_sharded_count(const vbc_sharded *s, int *ngpus);
@@ -231,6 +276,8 @@ typedef struct vbc_info {
                                length order (padding lanes fetch nothing) */
 } vbc_info;
 
+/* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /
+ * 10000 == VBC_VERSION / 10000). */
 VBC_API int vbc_get_info(const vbc_handle *h, vbc_info *info);
 
 /* Copies the thread's last error message (NUL-terminated, truncated to n). Returns its length. */

@@ -16,7 +16,9 @@ VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR, VBC_UN
     VBC_ASSERTION = range(7)
 VBC_F64, VBC_F32, VBC_I64, VBC_I32, VBC_BOOL = range(5)
 VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
-VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD, VBC_CREATE_MULTI = 0x1, 0x2, 0x4
+VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD, VBC_CREATE_MULTI, VBC_CREATE_SERIAL = 0x1, 0x2, 0x4, 0x8
+VBC_VERSION_MAJOR = 3  # include/vbc.h VBC_VERSION / 10000: the vbc_info layout below is that version's
+VBC_INFO_SIZE = 152
 VBC_MUL_REFERENCE_QUIRKS = 0x1
 VBC_MAT_ROWMAJOR = 0x2
 VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = 0, 1
@@ -24,9 +26,10 @@ VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = 0, 1
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
     "vbc1d_create", "vbc2d_create", "vbc_csc_create", "vbc_destroy", "vbc_mul", "vbc_mul_mat",
-    "vbc1d_create_ex", "vbc2d_create_ex", "vbc_csc_create_ex", "vbc_mul_ex",
+    "vbc1d_create_ex", "vbc2d_create_ex", "vbc_csc_create_ex", "vbc_mul_ex", "vbc_mul_mat_ex",
     "vbc_get_info", "vbc_last_error", "vbc_version",
-    "vbc1d_create_sharded", "vbc_sharded_mul", "vbc_sharded_destroy", "vbc_sharded_count", "vbc_sharded_shard",
+    "vbc1d_create_sharded", "vbc2d_create_sharded", "vbc_sharded_mul", "vbc_sharded_mul_ex", "vbc_sharded_destroy",
+    "vbc_sharded_count", "vbc_sharded_shard",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
     "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
     "vbcx_vbc_fill", "vbcx_transpose_pattern",
@@ -88,6 +91,10 @@ def lib():
         except ImportError:
             pass
         L = C.CDLL(str(LIB_PATH))
+        ver = L.vbc_version()
+        if ver // 10000 != VBC_VERSION_MAJOR or C.sizeof(vbc_info) != VBC_INFO_SIZE:
+            raise ImportError(f"libvbc ABI {ver} does not match this binding (major {VBC_VERSION_MAJOR}, "
+                              f"vbc_info {C.sizeof(vbc_info)} bytes); rebuild it")
         P, I64, INT, U, D = C.c_void_p, C.c_int64, C.c_int, C.c_uint, C.c_double
         L.vbc1d_create.argtypes = [C.POINTER(P), I64, I64, I64, I64, P, P, P, P, P, I64, INT, INT, U]
         L.vbc2d_create.argtypes = [C.POINTER(P), I64, I64, I64, I64, I64, P, I64, P, P, P, P, P, I64,
@@ -100,12 +107,16 @@ def lib():
         L.vbc_mul_ex.argtypes = [P, INT, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]
         L.vbc_destroy.argtypes = [P]
         L.vbc1d_create_sharded.argtypes = [C.POINTER(P), I64, I64, I64, I64, P, P, P, P, P, I64, T, INT, P, INT, U]
+        L.vbc2d_create_sharded.argtypes = [C.POINTER(P), I64, I64, I64, I64, I64, P, I64, P, P, P, P, P, I64, T, INT,
+                                           P, INT, U]
         L.vbc_sharded_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
+        L.vbc_sharded_mul_ex.argtypes = [P, INT, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]
         L.vbc_sharded_destroy.argtypes = [P]
         L.vbc_sharded_count.argtypes = [P, C.POINTER(INT)]
         L.vbc_sharded_shard.argtypes = [P, INT, C.POINTER(P), C.POINTER(I64), C.POINTER(I64), C.POINTER(INT)]
         L.vbc_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
         L.vbc_mul_mat.argtypes = [P, INT, I64, P, I64, I64, P, I64, I64, D, D, INT, P, U]
+        L.vbc_mul_mat_ex.argtypes = [P, INT, I64, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]
         L.vbc_get_info.argtypes = [P, C.POINTER(vbc_info)]
         L.vbc_last_error.argtypes = [C.c_char_p, C.c_size_t]
         L.vbcx_partition_equi.argtypes = [I64, I64, P, P]

@@ -1482,6 +1482,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
     }
+    if (flags & VBC_CREATE_SERIAL) h->planar_split = 0;  // every stripe summed serially in stored row order
     h->occ_p = std::max(1, std::min(occupancy_planar(h->esz), 8));
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
@@ -1564,7 +1565,9 @@ using namespace vbc;
 
 extern "C" {
 
-int vbc_version(void) { return 100; }
+static_assert(sizeof(vbc_info) == VBC_INFO_SIZE, "vbc_info layout changed: bump VBC_VERSION and VBC_INFO_SIZE");
+
+int vbc_version(void) { return VBC_VERSION; }
 
 int vbc_last_error(char *buf, size_t n)
 {
@@ -2018,22 +2021,6 @@ extern "C++" {  // helpers of the typed entry points (templates need C++ linkage
 static bool is_float(int dt) { return dt == VBC_F64 || dt == VBC_F32; }
 static bool known_dtype(int dt) { return dt >= VBC_F64 && dt <= VBC_BOOL; }
 
-template <typename To>
-static void host_convert(const void *src, int dt, int64_t n, int64_t inc, To *dst)
-{
-    const char *p = static_cast<const char *>(src);
-    for (int64_t i = 0; i < n; i++) {
-        const char *e = p + i * inc * elem_size(dt);
-        switch (dt) {
-        case VBC_F64: dst[i] = (To) * reinterpret_cast<const double *>(e); break;
-        case VBC_F32: dst[i] = (To) * reinterpret_cast<const float *>(e); break;
-        case VBC_I64: dst[i] = (To) * reinterpret_cast<const int64_t *>(e); break;
-        case VBC_I32: dst[i] = (To) * reinterpret_cast<const int32_t *>(e); break;
-        default: dst[i] = (To) * reinterpret_cast<const uint8_t *>(e); break;
-        }
-    }
-}
-
 // Values converted to the compute eltype (empty when no conversion is needed: use `val` as is).
 static int convert_values(const void *val, int64_t nval, const vbc_types *t, std::vector<char> &out)
 {
@@ -2156,26 +2143,12 @@ int vbc_mul_ex(vbc_handle *h, int trans, const void *x, int x_dtype, int64_t inc
         const void *xp = x;
         if (!direct_x) {
             xs.resize((size_t)std::max<int64_t>(nx, 1) * esz);
-            if (cdt == VBC_F64) host_convert(x, x_dtype, nx, incx, reinterpret_cast<double *>(xs.data()));
-            else if (cdt == VBC_F32) host_convert(x, x_dtype, nx, incx, reinterpret_cast<float *>(xs.data()));
-            else host_convert(x, x_dtype, nx, incx, reinterpret_cast<int64_t *>(xs.data()));
+            host_convert_to(x, x_dtype, nx, incx, xs.data(), cdt);
             xp = xs.data();
         }
-        if (beta != 0.0) {
-            if (cdt == VBC_F64) host_convert(y, y_dtype, ny, incy, reinterpret_cast<double *>(ys.data()));
-            else if (cdt == VBC_F32) host_convert(y, y_dtype, ny, incy, reinterpret_cast<float *>(ys.data()));
-            else host_convert(y, y_dtype, ny, incy, reinterpret_cast<int64_t *>(ys.data()));
-        }
+        if (beta != 0.0) host_convert_to(y, y_dtype, ny, incy, ys.data(), cdt);
         if (int st = vbc_mul(h, trans, xp, nx, ys.data(), ny, alpha, beta, mem, stream, flags)) return st;
-        char *yp = static_cast<char *>(y);
-        const int yesz = elem_size(y_dtype);
-        for (int64_t i = 0; i < ny; i++) {
-            char *e = yp + i * incy * yesz;
-            if (y_dtype == VBC_F64) *reinterpret_cast<double *>(e) = reinterpret_cast<const double *>(ys.data())[i];
-            else if (y_dtype == VBC_F32) *reinterpret_cast<float *>(e) = reinterpret_cast<const float *>(ys.data())[i];
-            else if (y_dtype == VBC_I64) *reinterpret_cast<int64_t *>(e) = reinterpret_cast<const int64_t *>(ys.data())[i];
-            else *reinterpret_cast<int32_t *>(e) = (int32_t)reinterpret_cast<const int64_t *>(ys.data())[i];
-        }
+        host_store(ys.data(), cdt, ny, y, y_dtype, incy);
         return VBC_OK;
     }
     // device operands: conversion kernels into / out of the handle's staging buffers
@@ -2204,6 +2177,18 @@ int vbc_mul_ex(vbc_handle *h, int trans, const void *x, int x_dtype, int64_t inc
         if (int st = convert_scatter(dy, cdt, y, y_dtype, incy, ny, s)) return st;
     }
     return po.end();
+}
+
+int vbc_mul_mat_ex(vbc_handle *h, int trans, int64_t nrhs, const void *X, int X_dtype, int64_t ldx, int64_t nx,
+                   void *Y, int Y_dtype, int64_t ldy, int64_t ny, double alpha, double beta, int mem, void *stream,
+                   unsigned flags)
+{
+    if (!h) return fail(VBC_INVALID_ARG, "NULL handle");
+    if (!known_dtype(X_dtype) || !known_dtype(Y_dtype)) return fail(VBC_UNSUPPORTED_DTYPE, "unknown eltype");
+    if (X_dtype != h->dtype || Y_dtype != h->dtype)
+        return fail(VBC_UNSUPPORTED_DTYPE, "the matrix product takes X and Y of the handle's compute eltype "
+                                           "(other eltypes: vbc_mul_ex column by column)");
+    return vbc_mul_mat(h, trans, nrhs, X, ldx, nx, Y, ldy, ny, alpha, beta, mem, stream, flags);
 }
 
 }  // extern "C"

@@ -1,4 +1,5 @@
-// libvbc multi-GPU handles (include/vbc.h: vbc1d_create_sharded, vbc_sharded_mul): ONE process
+// libvbc multi-GPU handles (include/vbc.h: vbc1d_create_sharded, vbc2d_create_sharded,
+// vbc_sharded_mul, vbc_sharded_mul_ex): ONE process
 // driving several GPUs of a node -- the configuration a Julia session with AMDGPU.jl has -- with RCCL
 // over xGMI for the exchange steps.  (One process per GPU with torch.distributed is the other
 // configuration; sparsematrixvbcs.jl_amd/distributed.py builds it on top of the single-GPU handles.)
@@ -14,8 +15,17 @@
 //                      each stripe's summation order is the reference's)
 //       B x: x replicated, y[r_g : r_g+1) per GPU, gathered on the root -- no reduction;
 //       B'x: x[r_g : r_g+1) per GPU, partial y, ncclReduce(sum).
-// Disjoint outputs are bit-identical to the single-GPU product; reduced ones differ only in the
-// order the partial sums are added.
+// A SparseMatrixVBC (multiply_VBC.jl:182-189 threads its transposed product the same way) splits the
+// same two ways; its row split cuts Π's block rows, so every u×w tile stays whole on one GPU.  The
+// code below treats a 1DVBC as the 2D format with unit block rows (K = m, Π.spl = 1:m+1).
+// Disjoint outputs are bit-identical to the single-GPU product (unless a shard runs the split planar
+// product, see vbc.h VBC_CREATE_SERIAL); reduced ones differ only in the order the partial sums are
+// added.
+//
+// Error discipline: a product that fails after its first collective was enqueued leaves the
+// communicators with a half-issued exchange (other GPUs may already wait in it), so the handle is
+// marked FAILED and refuses every later product; inside an ncclGroupStart / ncclGroupEnd pair the
+// first error stops further calls, and the group is always closed.
 //
 // When every shard is on the SAME device (devices = {d, d, ...}: oversubscription, or the tests of a
 // one-GPU box) the exchange needs no communication at all: shards read x and write y through pointer
@@ -29,7 +39,14 @@
 #include <mutex>
 #include <vector>
 
+#include <cmath>
+
 #include "vbc_internal.h"
+
+namespace vbc {  // vbc_generic.hip: strided eltype conversion kernels (vbc_mul_ex uses the same)
+int convert_gather(const void *src, int src_dtype, int64_t inc, void *dst, int dst_dtype, int64_t n, hipStream_t s);
+int convert_scatter(const void *src, int src_dtype, void *dst, int dst_dtype, int64_t inc, int64_t n, hipStream_t s);
+}  // namespace vbc
 
 using vbc::fail;
 
@@ -37,6 +54,7 @@ struct vbc_sharded {
     int64_t m = 0, n = 0;
     int ngpus = 0, split = 0, cdt = 0, esz = 8;
     bool local = false;              // all shards on one device: no communicators
+    bool failed = false;             // a product failed mid-exchange: refuse further products
     std::vector<int> dev;
     std::vector<vbc_handle *> h;
     std::vector<int64_t> cut;        // ngpus+1 0-based cuts of the split dimension (columns or rows)
@@ -45,7 +63,9 @@ struct vbc_sharded {
     std::vector<hipEvent_t> done;    // per shard: end of its part of a product
     hipEvent_t start = nullptr;      // root stream: start of a product
     std::vector<void *> xb, yb;      // per non-root shard: x / y buffers (max(m, n) elements each)
-    void *hx = nullptr, *hy = nullptr;  // root: host-pointer staging
+    void *hx = nullptr, *hy = nullptr;  // root: staging of host / converted / strided operands
+    hipEvent_t stage_ev = nullptr;   // recorded after the last product that used hx / hy
+    bool stage_used = false;
     std::mutex mu;                   // products are issued one at a time (collective order, buffers)
 };
 
@@ -71,11 +91,35 @@ int nccl_fail(ncclResult_t r, const char *what)
     return VBC_RCCL_ERROR;
 }
 
-#define VBC_NCCL(call)                                                                            \
-    do {                                                                                          \
-        ncclResult_t r_ = (call);                                                                 \
-        if (r_ != ncclSuccess) return nccl_fail(r_, #call);                                       \
-    } while (0)
+// One ncclGroupStart / ncclGroupEnd pair: after the first failing call no further call is issued
+// (ok() turns false), and end() always closes the group, returning the first error.
+class NcclGroup {
+  public:
+    NcclGroup() { note(ncclGroupStart(), "ncclGroupStart"); opened_ = first_ == ncclSuccess; }
+    ~NcclGroup() { if (opened_) (void)ncclGroupEnd(); }
+    bool ok() const { return first_ == ncclSuccess; }
+    void note(ncclResult_t r, const char *what)
+    {
+        if (first_ == ncclSuccess && r != ncclSuccess) {
+            first_ = r;
+            what_ = what;
+        }
+    }
+    int end()
+    {
+        if (opened_) {
+            opened_ = false;
+            note(ncclGroupEnd(), "ncclGroupEnd");
+        }
+        return first_ == ncclSuccess ? VBC_OK : nccl_fail(first_, what_);
+    }
+
+  private:
+    ncclResult_t first_ = ncclSuccess;
+    const char *what_ = "";
+    bool opened_ = false;
+};
+
 #define VBC_HIPS(call)                                                                            \
     do {                                                                                          \
         hipError_t e_ = (call);                                                                   \
@@ -93,6 +137,7 @@ ncclDataType_t nccl_type(int cdt)
 std::vector<int64_t> as64(const void *p, int bits, int64_t n)
 {
     std::vector<int64_t> v((size_t)std::max<int64_t>(n, 0));
+    if (!p) return v;
     if (bits == 64) std::memcpy(v.data(), p, v.size() * 8);
     else
         for (size_t i = 0; i < v.size(); i++) v[i] = static_cast<const int32_t *>(p)[i];
@@ -123,6 +168,10 @@ void destroy_all(vbc_sharded *s)
         DevGuard dg(s->dev[g]);
         if (s->st[g]) (void)hipStreamSynchronize(s->st[g]);
     }
+    if (s->stage_ev) {
+        DevGuard dg(s->dev[0]);
+        (void)hipEventSynchronize(s->stage_ev);
+    }
     for (ncclComm_t c : s->comm)
         if (c) (void)ncclCommDestroy(c);
     for (size_t g = 0; g < s->dev.size(); g++) {
@@ -133,6 +182,7 @@ void destroy_all(vbc_sharded *s)
         if (g < s->st.size() && s->st[g]) (void)hipStreamDestroy(s->st[g]);
         if (g == 0) {
             if (s->start) (void)hipEventDestroy(s->start);
+            if (s->stage_ev) (void)hipEventDestroy(s->stage_ev);
             if (s->hx) (void)hipFree(s->hx);
             if (s->hy) (void)hipFree(s->hy);
         }
@@ -142,9 +192,10 @@ void destroy_all(vbc_sharded *s)
     delete s;
 }
 
-// One product on device operands of the root (devices[0]), enqueued on the root stream s0.
+// One product on device operands of the root (devices[0]), enqueued on the root stream s0.  Sets
+// *issued once a collective may have been enqueued (the caller then marks the handle failed on error).
 int mul_device(vbc_sharded *s, int trans, const char *x, int64_t nx, char *y, int64_t ny, double alpha,
-               double beta, hipStream_t s0)
+               double beta, hipStream_t s0, bool *issued)
 {
     const int G = s->ngpus;
     const int64_t esz = s->esz;
@@ -173,25 +224,27 @@ int mul_device(vbc_sharded *s, int trans, const char *x, int64_t nx, char *y, in
     auto stream = [&](int g) { return g == 0 ? s0 : s->st[g]; };
     // 1. x to the shards: broadcast (replicated x) or one slice each
     if (!s->comm.empty()) {
-        VBC_NCCL(ncclGroupStart());
-        for (int g = 0; g < G; g++) {
+        *issued = true;
+        NcclGroup grp;
+        for (int g = 0; g < G && grp.ok(); g++) {
             if (disj) {
-                VBC_NCCL(ncclBroadcast(x, g == 0 ? (void *)x : s->xb[g], (size_t)nx, dt, 0, s->comm[g], stream(g)));
+                grp.note(ncclBroadcast(x, g == 0 ? (void *)x : s->xb[g], (size_t)nx, dt, 0, s->comm[g], stream(g)),
+                         "ncclBroadcast(x)");
             } else if (g > 0 && len(g) > 0) {
-                VBC_NCCL(ncclSend(x + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0));
-                VBC_NCCL(ncclRecv(s->xb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]));
+                grp.note(ncclSend(x + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0), "ncclSend(x)");
+                if (grp.ok()) grp.note(ncclRecv(s->xb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]), "ncclRecv(x)");
             }
         }
-        VBC_NCCL(ncclGroupEnd());
+        if (int st = grp.end()) return st;
         // β y of a disjoint slice lives on the root: send it to its shard first
         if (disj && beta != 0.0) {
-            VBC_NCCL(ncclGroupStart());
-            for (int g = 1; g < G; g++) {
+            NcclGroup gb;
+            for (int g = 1; g < G && gb.ok(); g++) {
                 if (len(g) == 0) continue;
-                VBC_NCCL(ncclSend(y + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0));
-                VBC_NCCL(ncclRecv(s->yb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]));
+                gb.note(ncclSend(y + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0), "ncclSend(y)");
+                if (gb.ok()) gb.note(ncclRecv(s->yb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]), "ncclRecv(y)");
             }
-            VBC_NCCL(ncclGroupEnd());
+            if (int st = gb.end()) return st;
         }
     }
     // 2. the shards' products
@@ -210,18 +263,18 @@ int mul_device(vbc_sharded *s, int trans, const char *x, int64_t nx, char *y, in
     }
     // 3. y to the root: the slices, or the sum of the partials (in place on the root)
     if (!s->comm.empty()) {
-        VBC_NCCL(ncclGroupStart());
-        for (int g = 0; g < G; g++) {
+        NcclGroup grp;
+        for (int g = 0; g < G && grp.ok(); g++) {
             if (disj) {
                 if (g == 0 || len(g) == 0) continue;
-                VBC_NCCL(ncclSend(s->yb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]));
-                VBC_NCCL(ncclRecv(y + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0));
+                grp.note(ncclSend(s->yb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]), "ncclSend(y)");
+                if (grp.ok()) grp.note(ncclRecv(y + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0), "ncclRecv(y)");
             } else {
                 void *buf = g == 0 ? (void *)y : s->yb[g];
-                VBC_NCCL(ncclReduce(buf, buf, (size_t)ny, dt, ncclSum, 0, s->comm[g], stream(g)));
+                grp.note(ncclReduce(buf, buf, (size_t)ny, dt, ncclSum, 0, s->comm[g], stream(g)), "ncclReduce(y)");
             }
         }
-        VBC_NCCL(ncclGroupEnd());
+        if (int st = grp.end()) return st;
     }
     // 4. the root stream waits for every shard
     for (int g = 1; g < G; g++) {
@@ -235,48 +288,159 @@ int mul_device(vbc_sharded *s, int trans, const char *x, int64_t nx, char *y, in
     return VBC_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int64_t L, const void *spl,
-                         const void *pos, const void *idx, const void *ofs, const void *val, int64_t nval,
-                         const vbc_types *types, int ngpus, const int *devices, int split, unsigned flags)
+// mul_device with the failed-state bookkeeping.
+int mul_checked(vbc_sharded *s, int trans, const char *x, int64_t nx, char *y, int64_t ny, double alpha,
+                double beta, hipStream_t s0)
 {
-    if (!out) return fail(VBC_INVALID_ARG, "NULL out");
+    bool issued = false;
+    const int st = mul_device(s, trans, x, nx, y, ny, alpha, beta, s0, &issued);
+    if (st != VBC_OK && issued) s->failed = true;
+    return st;
+}
+
+// Root staging buffers (max(m, n) compute-eltype elements each), allocated together on first use;
+// `s0` waits for the previous product that used them.
+int stage(vbc_sharded *s, hipStream_t s0)
+{
+    if (!s->hx) {
+        const size_t bytes = (size_t)std::max<int64_t>(std::max(s->m, s->n), 1) * s->esz;
+        void *a = nullptr, *b = nullptr;
+        if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) {
+            if (a) (void)hipFree(a);
+            return vbc::fail(VBC_HIP_ERROR, "hipMalloc of a staging buffer failed");
+        }
+        s->hx = a;
+        s->hy = b;
+    }
+    if (s->stage_used) VBC_HIPS(hipStreamWaitEvent(s0, s->stage_ev, 0));
+    return VBC_OK;
+}
+
+int unstage(vbc_sharded *s, hipStream_t s0)
+{
+    VBC_HIPS(hipEventRecord(s->stage_ev, s0));
+    s->stage_used = true;
+    return VBC_OK;
+}
+
+// Common validation of a product call; also refuses a FAILED handle.
+int check_product(const vbc_sharded *s, int trans, const void *x, int64_t nx, const void *y, int64_t ny, int mem)
+{
+    if (!s) return vbc::fail(VBC_INVALID_ARG, "NULL handle");
+    if (s->failed)
+        return vbc::fail(VBC_RCCL_ERROR, "sharded handle is FAILED (an earlier product failed mid-exchange); "
+                                         "destroy and re-create it");
+    const int64_t want_x = trans ? s->m : s->n, want_y = trans ? s->n : s->m;
+    if (nx != want_x || ny != want_y) return vbc::fail(VBC_DIM_MISMATCH, "DimensionMismatch");
+    if ((nx > 0 && !x) || (ny > 0 && !y)) return vbc::fail(VBC_INVALID_ARG, "NULL x or y");
+    if (ny > 0 && x == y) return vbc::fail(VBC_INVALID_ARG, "x and y must not alias");
+    if (mem != VBC_MEM_DEVICE && mem != VBC_MEM_HOST)
+        return vbc::fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
+    return VBC_OK;
+}
+
+void quirks(unsigned flags, int trans, double &alpha, double &beta)
+{
+    if (flags & VBC_MUL_REFERENCE_QUIRKS) {  // applied here: the shards then run plain BLAS semantics
+        alpha = 1.0;
+        if (trans) beta = 0.0;
+    }
+}
+
+// Host operands of the compute eltype: staged on the root, the device path on the root's internal
+// stream, returns when y is final.  The caller holds s->mu.
+int mul_host(vbc_sharded *s, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha, double beta)
+{
+    DevGuard dg(s->dev[0]);
+    if (!dg.ok) return vbc::fail(VBC_HIP_ERROR, "hipSetDevice failed");
+    const int64_t esz = s->esz;
+    hipStream_t s0 = s->st[0];
+    if (int st = stage(s, s0)) return st;
+    if (nx > 0) VBC_HIPS(hipMemcpyAsync(s->hx, x, nx * esz, hipMemcpyHostToDevice, s0));
+    if (ny > 0 && beta != 0.0) VBC_HIPS(hipMemcpyAsync(s->hy, y, ny * esz, hipMemcpyHostToDevice, s0));
+    if (int st = mul_checked(s, trans, static_cast<const char *>(s->hx), nx, static_cast<char *>(s->hy), ny, alpha,
+                             beta, s0))
+        return st;
+    DevGuard dg2(s->dev[0]);
+    if (ny > 0) VBC_HIPS(hipMemcpyAsync(y, s->hy, ny * esz, hipMemcpyDeviceToHost, s0));
+    if (int st = unstage(s, s0)) return st;
+    VBC_HIPS(hipStreamSynchronize(s0));
+    return VBC_OK;
+}
+
+// The matrix of either format as the 2D format: 1DVBC = unit block rows (K = m, Π.spl = 1:m+1).
+struct Fields {
+    bool is2d = false;
+    int64_t m = 0, n = 0, U = 1, W = 0, K = 0, L = 0;
+    std::vector<int64_t> PS, S, P, I, O;  // 1-based, as the reference stores them
+    const char *V = nullptr;
+    int vsz = 0;
+    int64_t u(int64_t k) const { return is2d ? PS[k + 1] - PS[k] : 1; }  // height of block row k (0-based)
+};
+
+int validate(const Fields &f)
+{
+    const int64_t L = f.L;
+    if (f.S[0] != 1 || f.S[L] != f.n + 1 || f.P[0] != 1 || f.O[0] != 1) return vbc::fail(VBC_INVALID_ARG, "bad Φ.spl / pos / ofs");
+    if (f.is2d) {
+        if (f.PS[0] != 1 || f.PS[f.K] != f.m + 1) return vbc::fail(VBC_INVALID_ARG, "bad Π.spl");
+        for (int64_t k = 0; k < f.K; k++)
+            if (f.PS[k + 1] <= f.PS[k]) return vbc::fail(VBC_INVALID_ARG, "Π.spl must increase");
+    }
+    for (int64_t l = 0; l < L; l++)
+        if (f.S[l + 1] <= f.S[l] || f.P[l + 1] < f.P[l]) return vbc::fail(VBC_INVALID_ARG, "inconsistent Φ.spl / pos");
+    const int64_t lim = f.is2d ? f.K : f.m;
+    for (int64_t r = 0; r < f.P[L] - 1; r++)
+        if (f.I[r] < 1 || f.I[r] > lim) return vbc::fail(VBC_INVALID_ARG, f.is2d ? "idx out of range 1:K" : "idx out of range 1:m");
+    for (int64_t l = 0; l < L; l++) {  // ofs steps: Σ u·w over the stripe's blocks
+        int64_t want = 0;
+        const int64_t w = f.S[l + 1] - f.S[l];
+        for (int64_t r = f.P[l] - 1; r < f.P[l + 1] - 1; r++) want += f.u(f.I[r] - 1) * w;
+        if (f.O[l + 1] - f.O[l] != want) return vbc::fail(VBC_INVALID_ARG, "inconsistent ofs");
+    }
+    return VBC_OK;
+}
+
+// One shard's handle from its fields (1-based Int64 arrays, raw values of val_dtype).
+int create_shard(const Fields &f, vbc_handle **out, int64_t m, int64_t n, int64_t K, const int64_t *ps, int64_t L,
+                 const int64_t *spl, const int64_t *pos, const int64_t *idx, const int64_t *ofs, const char *val,
+                 const vbc_types *t64, int device, unsigned flags)
+{
+    const int64_t nv = ofs[L] - 1;
+    if (f.is2d)
+        return vbc2d_create_ex(out, m, n, f.U, f.W, K, ps, L, spl, pos, idx, ofs, nv > 0 ? val : nullptr, nv, t64, device,
+                               flags);
+    return vbc1d_create_ex(out, m, n, f.W, L, spl, pos, idx, ofs, nv > 0 ? val : nullptr, nv, t64, device, flags);
+}
+
+int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *types, int ngpus, const int *devices,
+                   int split, unsigned flags)
+{
+    if (!out) return vbc::fail(VBC_INVALID_ARG, "NULL out");
     *out = nullptr;
-    if (!types) return fail(VBC_INVALID_ARG, "NULL vbc_types");
-    if (ngpus < 1 || !devices) return fail(VBC_INVALID_ARG, "ngpus must be >= 1 with a device list");
+    if (!types) return vbc::fail(VBC_INVALID_ARG, "NULL vbc_types");
+    if (ngpus < 1 || !devices) return vbc::fail(VBC_INVALID_ARG, "ngpus must be >= 1 with a device list");
     if (split != VBC_SPLIT_STRIPES && split != VBC_SPLIT_ROWS)
-        return fail(VBC_INVALID_ARG, "split must be VBC_SPLIT_STRIPES or VBC_SPLIT_ROWS");
-    if (types->index_bits != 32 && types->index_bits != 64) return fail(VBC_INVALID_ARG, "index_bits must be 32 or 64");
-    if (L < 0 || m < 0 || n < 0 || !spl || !pos || !ofs) return fail(VBC_INVALID_ARG, "bad stripe arrays");
+        return vbc::fail(VBC_INVALID_ARG, "split must be VBC_SPLIT_STRIPES or VBC_SPLIT_ROWS");
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess) return fail(VBC_HIP_ERROR, "hipGetDeviceCount failed");
+    if (hipGetDeviceCount(&count) != hipSuccess) return vbc::fail(VBC_HIP_ERROR, "hipGetDeviceCount failed");
     bool all_same = true, distinct = true;
     for (int g = 0; g < ngpus; g++) {
-        if (devices[g] < 0 || devices[g] >= count) return fail(VBC_INVALID_ARG, "device ordinal out of range");
+        if (devices[g] < 0 || devices[g] >= count) return vbc::fail(VBC_INVALID_ARG, "device ordinal out of range");
         all_same = all_same && devices[g] == devices[0];
         for (int k = 0; k < g; k++) distinct = distinct && devices[k] != devices[g];
     }
     if (!all_same && !distinct)
-        return fail(VBC_INVALID_ARG, "devices must be all distinct (RCCL) or all the same device");
-    const int bits = types->index_bits;
-    const std::vector<int64_t> S = as64(spl, bits, L + 1), P = as64(pos, bits, L + 1), O = as64(ofs, bits, L + 1);
-    if (S[0] != 1 || S[L] != n + 1 || P[0] != 1 || O[0] != 1) return fail(VBC_INVALID_ARG, "bad Φ.spl / pos / ofs");
-    const int64_t q = P[L] - 1;
-    if (q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
-    if (O[L] - 1 > nval || (O[L] - 1 > 0 && !val)) return fail(VBC_INVALID_ARG, "val shorter than ofs[L+1]-1");
-    for (int64_t l = 0; l < L; l++)
-        if (S[l + 1] <= S[l] || P[l + 1] < P[l] || O[l + 1] - O[l] != (P[l + 1] - P[l]) * (S[l + 1] - S[l]))
-            return fail(VBC_INVALID_ARG, "inconsistent Φ.spl / pos / ofs");
-    const std::vector<int64_t> I = as64(idx, bits, q);
-    for (int64_t r = 0; r < q; r++)
-        if (I[r] < 1 || I[r] > m) return fail(VBC_INVALID_ARG, "idx out of range 1:m");
-    const int vsz = vbc::elem_size(types->val_dtype);
-    if (vsz == 0) return fail(VBC_UNSUPPORTED_DTYPE, "unknown val_dtype");
+        return vbc::fail(VBC_INVALID_ARG, "devices must be all distinct (RCCL) or all the same device");
+    if (int st = validate(f)) return st;
+    const int64_t L = f.L, m = f.m, n = f.n;
+    if (f.O[L] - 1 > nval || (f.O[L] - 1 > 0 && !f.V)) return vbc::fail(VBC_INVALID_ARG, "val shorter than ofs[L+1]-1");
+    f.vsz = vbc::elem_size(types->val_dtype);
+    if (f.vsz == 0) return vbc::fail(VBC_UNSUPPORTED_DTYPE, "unknown val_dtype");
     const int csz = vbc::elem_size(types->compute_dtype);
-    const char *V = static_cast<const char *>(val);
+    if (csz == 0) return vbc::fail(VBC_UNSUPPORTED_DTYPE, "unknown compute_dtype");
+    const char *V = f.V;
+    const int vsz = f.vsz;
 
     vbc_sharded *s = new vbc_sharded;
     s->m = m; s->n = n; s->ngpus = ngpus; s->split = split; s->cdt = types->compute_dtype;
@@ -285,6 +449,7 @@ int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int
     s->h.assign(ngpus, nullptr);
     vbc_types t64 = *types;
     t64.index_bits = 64;
+    const std::vector<int64_t> &S = f.S, &P = f.P, &I = f.I, &O = f.O;
 
     // byte-balanced cuts (distributed.py stripe_split / row_split): value bytes + 4-B keys + stripe headers
     if (split == VBC_SPLIT_STRIPES) {
@@ -302,38 +467,50 @@ int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int
                 pg[l] = P[a + l] - (P[a] - 1);
                 og[l] = O[a + l] - (O[a] - 1);
             }
-            const int64_t nvg = og[Lg] - 1;
-            int st = vbc1d_create_ex(&s->h[g], m, S[b] - S[a], W, Lg, sg.data(), pg.data(), I.data() + (P[a] - 1),
-                                     og.data(), nvg > 0 ? V + (O[a] - 1) * vsz : nullptr, nvg, &t64, devices[g], flags);
+            int st = create_shard(f, &s->h[g], m, S[b] - S[a], f.K, f.PS.data(), Lg, sg.data(), pg.data(),
+                                  I.data() + (P[a] - 1), og.data(), V + (O[a] - 1) * vsz, &t64, devices[g], flags);
             if (st) { destroy_all(s); return st; }
         }
     } else {
-        std::vector<double> per_row(m + 1, 0.0);
+        // cost per block row (1D: per row) = its blocks' value bytes + a 4-B key each
+        const int64_t K = f.is2d ? f.K : m;
+        std::vector<double> per(K + 1, 0.0);
         for (int64_t l = 0; l < L; l++)
             for (int64_t r = P[l] - 1; r < P[l + 1] - 1; r++)
-                per_row[I[r]] += (double)((S[l + 1] - S[l]) * csz + 4);  // I is 1-based: prefix index
-        for (int64_t i = 0; i < m; i++) per_row[i + 1] += per_row[i];
-        s->cut = balanced_cuts(per_row, ngpus);  // row ranges
+                per[I[r]] += (double)(f.u(I[r] - 1) * (S[l + 1] - S[l]) * csz + 4);  // I is 1-based: prefix index
+        for (int64_t k = 0; k < K; k++) per[k + 1] += per[k];
+        const std::vector<int64_t> kc = balanced_cuts(per, ngpus);  // block-row ranges
+        s->cut.resize(ngpus + 1);
+        for (int g = 0; g <= ngpus; g++) s->cut[g] = f.is2d ? f.PS[kc[g]] - 1 : kc[g];  // row ranges
         for (int g = 0; g < ngpus; g++) {
-            const int64_t r0 = s->cut[g], r1 = s->cut[g + 1];
-            std::vector<int64_t> pg(L + 1), og(L + 1), ig;
+            const int64_t k0 = kc[g], k1 = kc[g + 1];
+            std::vector<int64_t> pg(L + 1), og(L + 1), ig, psg;
             std::vector<char> vg;
             pg[0] = og[0] = 1;
             for (int64_t l = 0; l < L; l++) {
                 const int64_t w = S[l + 1] - S[l];
-                int64_t kept = 0;
+                int64_t kept = 0, kept_vals = 0, off = O[l] - 1;  // running value offset inside the stripe
                 for (int64_t r = P[l] - 1; r < P[l + 1] - 1; r++) {
-                    if (I[r] <= r0 || I[r] > r1) continue;
-                    ig.push_back(I[r] - r0);
-                    const char *src = V + (O[l] - 1 + (r - (P[l] - 1)) * w) * vsz;
-                    vg.insert(vg.end(), src, src + w * vsz);
-                    kept++;
+                    const int64_t bsz = f.u(I[r] - 1) * w;
+                    if (I[r] > k0 && I[r] <= k1) {
+                        ig.push_back(I[r] - k0);
+                        const char *src = V + off * vsz;
+                        vg.insert(vg.end(), src, src + bsz * vsz);
+                        kept++;
+                        kept_vals += bsz;
+                    }
+                    off += bsz;
                 }
                 pg[l + 1] = pg[l] + kept;
-                og[l + 1] = og[l] + kept * w;
+                og[l + 1] = og[l] + kept_vals;
             }
-            int st = vbc1d_create_ex(&s->h[g], r1 - r0, n, W, L, S.data(), pg.data(), ig.empty() ? nullptr : ig.data(),
-                                     og.data(), vg.empty() ? nullptr : vg.data(), og[L] - 1, &t64, devices[g], flags);
+            if (f.is2d) {
+                psg.resize(k1 - k0 + 1);
+                for (int64_t k = k0; k <= k1; k++) psg[k - k0] = f.PS[k] - (f.PS[k0] - 1);
+            }
+            int st = create_shard(f, &s->h[g], s->cut[g + 1] - s->cut[g], n, k1 - k0, psg.data(), L, S.data(),
+                                  pg.data(), ig.empty() ? nullptr : ig.data(), og.data(),
+                                  vg.empty() ? nullptr : vg.data(), &t64, devices[g], flags);
             if (st) { destroy_all(s); return st; }
         }
     }
@@ -349,16 +526,17 @@ int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int
         if (!dg.ok || hipStreamCreateWithFlags(&s->st[g], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s->done[g], hipEventDisableTiming) != hipSuccess) {
             destroy_all(s);
-            return fail(VBC_HIP_ERROR, "stream / event creation failed");
+            return vbc::fail(VBC_HIP_ERROR, "stream / event creation failed");
         }
-        if (g == 0 && hipEventCreateWithFlags(&s->start, hipEventDisableTiming) != hipSuccess) {
+        if (g == 0 && (hipEventCreateWithFlags(&s->start, hipEventDisableTiming) != hipSuccess ||
+                       hipEventCreateWithFlags(&s->stage_ev, hipEventDisableTiming) != hipSuccess)) {
             destroy_all(s);
-            return fail(VBC_HIP_ERROR, "event creation failed");
+            return vbc::fail(VBC_HIP_ERROR, "event creation failed");
         }
         if (g > 0 && !s->local &&
             (hipMalloc(&s->xb[g], big * csz) != hipSuccess || hipMalloc(&s->yb[g], big * csz) != hipSuccess)) {
             destroy_all(s);
-            return fail(VBC_HIP_ERROR, "hipMalloc of an exchange buffer failed");
+            return vbc::fail(VBC_HIP_ERROR, "hipMalloc of an exchange buffer failed");
         }
     }
     if (!s->local) {  // one rank too: the same collectives, trivially (in place on the root)
@@ -372,6 +550,58 @@ int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int
     }
     *out = s;
     return VBC_OK;
+}
+
+bool is_float(int dt) { return dt == VBC_F64 || dt == VBC_F32; }
+bool known_dtype(int dt) { return dt >= VBC_F64 && dt <= VBC_BOOL; }
+
+}  // namespace
+
+extern "C" {
+
+int vbc1d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t W, int64_t L, const void *spl,
+                         const void *pos, const void *idx, const void *ofs, const void *val, int64_t nval,
+                         const vbc_types *types, int ngpus, const int *devices, int split, unsigned flags)
+{
+    if (out) *out = nullptr;
+    if (!types) return fail(VBC_INVALID_ARG, "NULL vbc_types");
+    if (types->index_bits != 32 && types->index_bits != 64) return fail(VBC_INVALID_ARG, "index_bits must be 32 or 64");
+    if (L < 0 || m < 0 || n < 0 || !spl || !pos || !ofs) return fail(VBC_INVALID_ARG, "bad stripe arrays");
+    const int bits = types->index_bits;
+    Fields f;
+    f.m = m; f.n = n; f.W = W; f.K = m; f.L = L;
+    f.S = as64(spl, bits, L + 1);
+    f.P = as64(pos, bits, L + 1);
+    f.O = as64(ofs, bits, L + 1);
+    const int64_t q = f.P[L] - 1;
+    if (f.P[0] != 1 || q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
+    f.I = as64(idx, bits, q);
+    f.V = static_cast<const char *>(val);
+    return create_sharded(out, f, nval, types, ngpus, devices, split, flags);
+}
+
+int vbc2d_create_sharded(vbc_sharded **out, int64_t m, int64_t n, int64_t U, int64_t W, int64_t K, const void *pspl,
+                         int64_t L, const void *spl, const void *pos, const void *idx, const void *ofs, const void *val,
+                         int64_t nval, const vbc_types *types, int ngpus, const int *devices, int split, unsigned flags)
+{
+    if (out) *out = nullptr;
+    if (!types) return fail(VBC_INVALID_ARG, "NULL vbc_types");
+    if (types->index_bits != 32 && types->index_bits != 64) return fail(VBC_INVALID_ARG, "index_bits must be 32 or 64");
+    if (K < 0 || L < 0 || m < 0 || n < 0 || !pspl || !spl || !pos || !ofs)
+        return fail(VBC_INVALID_ARG, "bad partition arrays");
+    const int bits = types->index_bits;
+    Fields f;
+    f.is2d = true;
+    f.m = m; f.n = n; f.U = U; f.W = W; f.K = K; f.L = L;
+    f.PS = as64(pspl, bits, K + 1);
+    f.S = as64(spl, bits, L + 1);
+    f.P = as64(pos, bits, L + 1);
+    f.O = as64(ofs, bits, L + 1);
+    const int64_t q = f.P[L] - 1;
+    if (f.P[0] != 1 || q < 0 || (q > 0 && !idx)) return fail(VBC_INVALID_ARG, "bad pos");
+    f.I = as64(idx, bits, q);
+    f.V = static_cast<const char *>(val);
+    return create_sharded(out, f, nval, types, ngpus, devices, split, flags);
 }
 
 int vbc_sharded_destroy(vbc_sharded *s)
@@ -400,36 +630,71 @@ int vbc_sharded_shard(const vbc_sharded *s, int g, vbc_handle **h, int64_t *lo, 
 int vbc_sharded_mul(vbc_sharded *s, int trans, const void *x, int64_t nx, void *y, int64_t ny, double alpha,
                     double beta, int mem, void *stream, unsigned flags)
 {
-    if (!s) return fail(VBC_INVALID_ARG, "NULL handle");
-    const int64_t want_x = trans ? s->m : s->n, want_y = trans ? s->n : s->m;
-    if (nx != want_x || ny != want_y) return fail(VBC_DIM_MISMATCH, "DimensionMismatch");
-    if ((nx > 0 && !x) || (ny > 0 && !y)) return fail(VBC_INVALID_ARG, "NULL x or y");
-    if (ny > 0 && x == y) return fail(VBC_INVALID_ARG, "x and y must not alias");
-    if (mem != VBC_MEM_DEVICE && mem != VBC_MEM_HOST)
-        return fail(VBC_INVALID_ARG, "mem must be VBC_MEM_DEVICE or VBC_MEM_HOST");
-    if (flags & VBC_MUL_REFERENCE_QUIRKS) {  // applied here: the shards then run plain BLAS semantics
-        alpha = 1.0;
-        if (trans) beta = 0.0;
-    }
+    if (int st = check_product(s, trans, x, nx, y, ny, mem)) return st;
+    quirks(flags, trans, alpha, beta);
     std::lock_guard<std::mutex> lk(s->mu);
-    if (mem == VBC_MEM_DEVICE) return mul_device(s, trans, static_cast<const char *>(x), nx, static_cast<char *>(y),
-                                                 ny, alpha, beta, (hipStream_t)stream);
-    // host operands: staged on the root, then the device path on the root's internal stream
+    if (mem == VBC_MEM_DEVICE)
+        return mul_checked(s, trans, static_cast<const char *>(x), nx, static_cast<char *>(y), ny, alpha, beta,
+                           (hipStream_t)stream);
+    return mul_host(s, trans, x, nx, y, ny, alpha, beta);
+}
+
+int vbc_sharded_mul_ex(vbc_sharded *s, int trans, const void *x, int x_dtype, int64_t incx, int64_t nx, void *y,
+                       int y_dtype, int64_t incy, int64_t ny, double alpha, double beta, int mem, void *stream,
+                       unsigned flags)
+{
+    if (int st = check_product(s, trans, x, nx, y, ny, mem)) return st;
+    const int cdt = s->cdt;
+    if (!known_dtype(x_dtype) || !known_dtype(y_dtype)) return fail(VBC_UNSUPPORTED_DTYPE, "unknown eltype");
+    if (cdt == VBC_I64 && is_float(x_dtype))
+        return fail(VBC_UNSUPPORTED_DTYPE, "floating-point x on an integer handle (InexactError)");
+    if (is_float(cdt) ? y_dtype != cdt : (y_dtype != VBC_I64 && y_dtype != VBC_I32))
+        return fail(VBC_UNSUPPORTED_DTYPE, "eltype(y) must be the handle's compute eltype (or Int32 on an Int64 handle)");
+    if ((nx > 0 && incx == 0) || (ny > 0 && incy == 0)) return fail(VBC_INVALID_ARG, "zero stride");
+    if (cdt == VBC_I64 && (alpha != std::trunc(alpha) || beta != std::trunc(beta)))
+        return fail(VBC_INVALID_ARG, "alpha and beta must be integers on an integer handle (InexactError)");
+    const bool direct_x = x_dtype == cdt && (incx == 1 || nx <= 1);
+    const bool direct_y = y_dtype == cdt && (incy == 1 || ny <= 1);
+    if (direct_x && direct_y) return vbc_sharded_mul(s, trans, x, nx, y, ny, alpha, beta, mem, stream, flags);
+    quirks(flags, trans, alpha, beta);
+    const int64_t esz = s->esz;
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (mem == VBC_MEM_HOST) {  // convert on the host, then the contiguous host path
+        std::vector<char> xs, ys((size_t)std::max<int64_t>(ny, 1) * esz);
+        const void *xp = x;
+        if (!direct_x) {
+            xs.resize((size_t)std::max<int64_t>(nx, 1) * esz);
+            vbc::host_convert_to(x, x_dtype, nx, incx, xs.data(), cdt);
+            xp = xs.data();
+        }
+        if (beta != 0.0) vbc::host_convert_to(y, y_dtype, ny, incy, ys.data(), cdt);
+        if (int st = mul_host(s, trans, xp, nx, ys.data(), ny, alpha, beta)) return st;
+        vbc::host_store(ys.data(), cdt, ny, y, y_dtype, incy);
+        return VBC_OK;
+    }
+    // device operands on devices[0]: conversion kernels into / out of the root staging buffers
     DevGuard dg(s->dev[0]);
     if (!dg.ok) return fail(VBC_HIP_ERROR, "hipSetDevice failed");
-    const int64_t esz = s->esz, big = std::max<int64_t>(std::max(s->m, s->n), 1);
-    if (!s->hx && (hipMalloc(&s->hx, big * esz) != hipSuccess || hipMalloc(&s->hy, big * esz) != hipSuccess))
-        return fail(VBC_HIP_ERROR, "hipMalloc of a staging buffer failed");
-    hipStream_t s0 = s->st[0];
-    if (nx > 0) VBC_HIPS(hipMemcpyAsync(s->hx, x, nx * esz, hipMemcpyHostToDevice, s0));
-    if (ny > 0 && beta != 0.0) VBC_HIPS(hipMemcpyAsync(s->hy, y, ny * esz, hipMemcpyHostToDevice, s0));
-    if (int st = mul_device(s, trans, static_cast<const char *>(s->hx), nx, static_cast<char *>(s->hy), ny, alpha,
-                            beta, s0))
-        return st;
+    hipStream_t s0 = (hipStream_t)stream;
+    if (int st = stage(s, s0)) return st;
+    const char *dx = static_cast<const char *>(x);
+    char *dy = static_cast<char *>(y);
+    if (!direct_x) {
+        if (int st = vbc::convert_gather(x, x_dtype, incx, s->hx, cdt, nx, s0)) return st;
+        dx = static_cast<const char *>(s->hx);
+    }
+    if (!direct_y) {
+        if (beta != 0.0) {
+            if (int st = vbc::convert_gather(y, y_dtype, incy, s->hy, cdt, ny, s0)) return st;
+        }
+        dy = static_cast<char *>(s->hy);
+    }
+    if (int st = mul_checked(s, trans, dx, nx, dy, ny, alpha, beta, s0)) return st;
     DevGuard dg2(s->dev[0]);
-    if (ny > 0) VBC_HIPS(hipMemcpyAsync(y, s->hy, ny * esz, hipMemcpyDeviceToHost, s0));
-    VBC_HIPS(hipStreamSynchronize(s0));
-    return VBC_OK;
+    if (!direct_y) {
+        if (int st = vbc::convert_scatter(s->hy, cdt, y, y_dtype, incy, ny, s0)) return st;
+    }
+    return unstage(s, s0);
 }
 
 }  // extern "C"

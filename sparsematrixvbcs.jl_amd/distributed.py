@@ -187,34 +187,48 @@ class ShardedSparseMatrix1DVBC:
 
 
 class MultiGPUSparseMatrix1DVBC:
-    """ONE process driving several GPUs: libvbc's sharded handle (include/vbc.h vbc1d_create_sharded,
-    RCCL over xGMI between distinct devices).  Same splits as ShardedSparseMatrix1DVBC, but the
-    exchange runs inside the library on device pointers of devices[0] (the Julia drop-in's
-    configuration: one session, x and y on one device, the other GPUs as workers).
+    """ONE process driving several GPUs: libvbc's sharded handle (include/vbc.h vbc1d_create_sharded /
+    vbc2d_create_sharded, RCCL over xGMI between distinct devices).  Same splits as
+    ShardedSparseMatrix1DVBC, but the exchange runs inside the library on device pointers of
+    devices[0] (the Julia drop-in's configuration: one session, x and y on one device, the other GPUs
+    as workers).  B may be a SparseMatrix1DVBC or a SparseMatrixVBC (the 2D transposed product is
+    threaded the same way, multiply_VBC.jl:182-189; its row split keeps Π's block rows whole).
 
         S = MultiGPUSparseMatrix1DVBC(B, devices=[0, 1, 2, 3], split="stripes")
         mul_(y, S.T, x)      # mul!(y, B', x): x broadcast, y slices gathered on devices[0]
         mul_(y, S, x)        # mul!(y, B, x): x slices, ncclReduce(sum) of y
 
-    `devices` all equal (e.g. [0, 0, 0]) runs every shard on that device with no communicator."""
+    `devices` all equal (e.g. [0, 0, 0]) runs every shard on that device with no communicator.
+    Like the single-GPU mul_, x / y may be any strided vectors of any supported eltype (converted to
+    the handle's compute eltype, multiply_1DVBC.jl:9,85,102): vbc_sharded_mul_ex carries them."""
 
-    def __init__(self, B, devices=(0,), split="stripes", transposed=True, forward=True):
+    def __init__(self, B, devices=(0,), split="stripes", transposed=True, forward=True, serial=False):
         import ctypes as C
         from . import _lib as _L
         if split not in ("stripes", "rows"):
             raise ValueError("split must be 'stripes' or 'rows'")
         self.m, self.n, self.W = B.m, B.n, B.W
         self.val = B.val  # eltype queries (mul_ computes in eltype(y))
+        self.dtype = B.val.dtype
         self.split = split
+        self.is2d = hasattr(B, "Pi")
         self.devices = [int(d) for d in devices]
-        flags = (_L.VBC_CREATE_TRANSPOSED if transposed else 0) | (_L.VBC_CREATE_FORWARD if forward else 0)
+        flags = ((_L.VBC_CREATE_TRANSPOSED if transposed else 0) | (_L.VBC_CREATE_FORWARD if forward else 0)
+                 | (_L.VBC_CREATE_SERIAL if serial else 0))
         t = _L.vbc_types(_L.dtype_code(B.val.dtype), 64, _L.compute_code(B.val.dtype), 0)
         devs = (C.c_int * len(self.devices))(*self.devices)
         h = C.c_void_p()
-        _L.check(_L.lib().vbc1d_create_sharded(
-            C.byref(h), B.m, B.n, B.W, len(B.Phi), B.Phi.spl.ctypes.data, B.pos.ctypes.data, B.idx.ctypes.data,
-            B.ofs.ctypes.data, B.val.ctypes.data, len(B.val), C.byref(t), len(self.devices), devs,
-            _L.VBC_SPLIT_STRIPES if split == "stripes" else _L.VBC_SPLIT_ROWS, flags), "create_sharded")
+        kind = _L.VBC_SPLIT_STRIPES if split == "stripes" else _L.VBC_SPLIT_ROWS
+        if self.is2d:
+            _L.check(_L.lib().vbc2d_create_sharded(
+                C.byref(h), B.m, B.n, B.U, B.W, len(B.Pi), B.Pi.spl.ctypes.data, len(B.Phi), B.Phi.spl.ctypes.data,
+                B.pos.ctypes.data, B.idx.ctypes.data, B.ofs.ctypes.data, B.val.ctypes.data, len(B.val), C.byref(t),
+                len(self.devices), devs, kind, flags), "create_sharded (2D)")
+        else:
+            _L.check(_L.lib().vbc1d_create_sharded(
+                C.byref(h), B.m, B.n, B.W, len(B.Phi), B.Phi.spl.ctypes.data, B.pos.ctypes.data, B.idx.ctypes.data,
+                B.ofs.ctypes.data, B.val.ctypes.data, len(B.val), C.byref(t), len(self.devices), devs, kind, flags),
+                "create_sharded")
         self._h = h
         self.compute = t.compute_dtype
 
@@ -247,15 +261,14 @@ class MultiGPUSparseMatrix1DVBC:
         nx, ny = x.shape[0], y.shape[0]
         if (nx, ny) != ((self.m, self.n) if trans else (self.n, self.m)):
             raise _L.DimensionMismatch(f"size(A)={self.shape}, length(x)={nx}, length(y)={ny}")
-        for a in (x, y):
-            if _L.dtype_code(a.dtype) != self.compute or _stride(a) != 1:
-                raise _L.UnsupportedDtype("the multi-GPU product takes contiguous vectors of the matrix eltype")
+        xdt, ydt = _L.dtype_code(x.dtype), _L.dtype_code(y.dtype)
         mem, dev, stream = _mem_device_stream(x, y, stream)
         if mem == _L.VBC_MEM_DEVICE and dev != self.devices[0]:
             raise _L.ArgumentError(f"x and y must live on devices[0] = cuda:{self.devices[0]}")
         flags = _L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0
-        _L.check(_L.lib().vbc_sharded_mul(self._h, int(trans), _L.ptr(x), nx, _L.ptr(y), ny, float(alpha),
-                                          float(beta), mem, stream, flags), "mul! (sharded)")
+        _L.check(_L.lib().vbc_sharded_mul_ex(self._h, int(trans), _L.ptr(x), xdt, _stride(x), nx, _L.ptr(y), ydt,
+                                             _stride(y), ny, float(alpha), float(beta), mem, stream, flags),
+                 "mul! (sharded)")
         return y
 
     def release(self):
@@ -269,3 +282,6 @@ class MultiGPUSparseMatrix1DVBC:
             self.release()
         except Exception:
             pass
+
+
+MultiGPUSparseMatrix = MultiGPUSparseMatrix1DVBC  # either format (1DVBC or VBC)

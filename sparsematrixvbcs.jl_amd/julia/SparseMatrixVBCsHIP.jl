@@ -11,7 +11,7 @@
 #     Bd = HIPSparseMatrix1DVBC(B)                 # uploads once per compute eltype (vbc1d_create_ex)
 #     mul!(y, Bd', x)                              # host StridedVectors: staged through HBM
 #     mul!(y_dev, Bd', x_dev)                      # ROCVectors: enqueued on the task-local stream
-#     Bs = HIPShardedSparseMatrix1DVBC(B; devices=0:7)   # one session, 8 GPUs, RCCL over xGMI
+#     Bs = HIPShardedSparseMatrix(B; devices=0:7)        # one session, 8 GPUs, RCCL over xGMI (1D or 2D B)
 #     mul!(y, Bs', x)
 module SparseMatrixVBCsHIP
 
@@ -53,6 +53,13 @@ struct VbcTypes
 end
 vbc_types(::Type{Tv}, ::Type{Ti}, cdt::Cint) where {Tv, Ti <: Union{Int64, Int32}} =
     VbcTypes(vbc_dtype(Tv), 8 * sizeof(Ti), cdt, 0)
+
+# include/vbc.h VBC_VERSION: the structs below (VbcTypes; vbc_info, VBC_INFO_SIZE = 152 bytes) are those
+# of ABI major version 3
+function __init__()
+    v = ccall((:vbc_version, libvbc), Cint, ())
+    v ÷ 10000 == 3 || error("libvbc ABI version $v does not match SparseMatrixVBCsHIP (3.x); rebuild libvbc")
+end
 
 function last_error()
     buf = Vector{UInt8}(undef, 1024)
@@ -204,56 +211,118 @@ Base.:*(adjA::AdjOrTransHIP, x::StridedVector{T}) where {T} =
 TrSpMV!(y::StridedVector, A::HIPSparseMatrixCSC, x::StridedVector) = _mul!(y, A, true, x, true, false)
 
 """
-    HIPShardedSparseMatrix1DVBC(B; devices=0:7, split=:stripes)
+    HIPShardedSparseMatrix(B; devices=0:7, split=:stripes, serial=false)
 
-`B` split over several GPUs of the node by byte-balanced stripe (`split=:stripes`, the block rows of
-A when B stores Aᵀ) or row (`split=:rows`) ranges, one handle per GPU, RCCL over xGMI for the exchange
-(vbc1d_create_sharded).  This replaces the reference's threaded stripe loop (multiply_1DVBC.jl:
-169-177).  Computes in Tv; host vectors or (with AMDGPU) ROCVectors on `devices[1]`.
+`B` (a SparseMatrix1DVBC or a SparseMatrixVBC) split over several GPUs of the node by byte-balanced
+stripe (`split=:stripes`, the block rows of A when B stores Aᵀ) or row (`split=:rows`; Π's block rows
+for a SparseMatrixVBC) ranges, one handle per GPU, RCCL over xGMI for the exchange
+(vbc1d_create_sharded / vbc2d_create_sharded).  This replaces the reference's threaded stripe loops
+(multiply_1DVBC.jl:169-177, multiply_VBC.jl:182-189).  Computes in Tv (integers and Bool in exact
+Int64); host StridedVectors of any supported eltype (x converted like multiply_1DVBC.jl:102) or, with
+AMDGPU, ROCVectors on `devices[1]`.  `serial=true` keeps the reference's serial per-stripe summation
+order in every shard (VBC_CREATE_SERIAL).
 """
-mutable struct HIPShardedSparseMatrix1DVBC{W, Tv, Ti}
-    host::SparseMatrix1DVBC{W, Tv, Ti}
+mutable struct HIPShardedSparseMatrix{M}
+    host::M
     handle::Ptr{Cvoid}
+    compute::Cint
 end
+const HIPShardedSparseMatrix1DVBC = HIPShardedSparseMatrix  # round-2 name
 
-function HIPShardedSparseMatrix1DVBC(B::SparseMatrix1DVBC{W, Tv, Ti}; devices=0:7, split::Symbol=:stripes,
-                                     forward::Bool=true, transposed::Bool=true) where {W, Tv, Ti}
+const VBC_CREATE_SERIAL = Cuint(8)
+
+function _sharded_flags(split, forward, transposed, serial)
     split in (:stripes, :rows) || throw(ArgumentError("split must be :stripes or :rows"))
+    return (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0)) |
+           (serial ? VBC_CREATE_SERIAL : Cuint(0))
+end
+_default_compute(::Type{Tv}) where {Tv} = Tv <: AbstractFloat ? compute_dtype(Tv) : VBC_I64
+
+function HIPShardedSparseMatrix(B::SparseMatrix1DVBC{W, Tv, Ti}; devices=0:7, split::Symbol=:stripes,
+                                forward::Bool=true, transposed::Bool=true, serial::Bool=false) where {W, Tv, Ti}
+    flags = _sharded_flags(split, forward, transposed, serial)
     devs = Cint.(collect(devices))
-    flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0))
     h = Ref{Ptr{Cvoid}}(C_NULL)
-    t = Ref(vbc_types(Tv, Ti, compute_dtype(Tv <: Union{Bool, Int32} ? Int64 : Tv)))
+    cdt = _default_compute(Tv)
+    t = Ref(vbc_types(Tv, Ti, cdt))
     GC.@preserve B t devs check(ccall((:vbc1d_create_sharded, libvbc), Cint,
         (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Cvoid}, Int64,
          Ptr{VbcTypes}, Cint, Ptr{Cint}, Cint, Cuint),
         h, B.m, B.n, W, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val), t, length(devs), devs,
         split === :stripes ? VBC_SPLIT_STRIPES : VBC_SPLIT_ROWS, flags))
-    M = HIPShardedSparseMatrix1DVBC{W, Tv, Ti}(B, h[])
+    M = HIPShardedSparseMatrix(B, h[], cdt)
     finalizer(M -> ccall((:vbc_sharded_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle), M)
     return M
 end
 
-Base.size(A::HIPShardedSparseMatrix1DVBC) = size(A.host)
-Base.size(A::HIPShardedSparseMatrix1DVBC, d::Integer) = size(A.host, d)
+function HIPShardedSparseMatrix(B::SparseMatrixVBC{U, W, Tv, Ti}; devices=0:7, split::Symbol=:stripes,
+                                forward::Bool=true, transposed::Bool=true, serial::Bool=false) where {U, W, Tv, Ti}
+    flags = _sharded_flags(split, forward, transposed, serial)
+    devs = Cint.(collect(devices))
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    cdt = _default_compute(Tv)
+    t = Ref(vbc_types(Tv, Ti, cdt))
+    GC.@preserve B t devs check(ccall((:vbc2d_create_sharded, libvbc), Cint,
+        (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Int64, Ptr{Ti}, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Ti},
+         Ptr{Cvoid}, Int64, Ptr{VbcTypes}, Cint, Ptr{Cint}, Cint, Cuint),
+        h, B.m, B.n, U, W, length(B.Π), B.Π.spl, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val), t,
+        length(devs), devs, split === :stripes ? VBC_SPLIT_STRIPES : VBC_SPLIT_ROWS, flags))
+    M = HIPShardedSparseMatrix(B, h[], cdt)
+    finalizer(M -> ccall((:vbc_sharded_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle), M)
+    return M
+end
 
-function _mul!(y::Vector{T}, A::HIPShardedSparseMatrix1DVBC, trans::Bool, x::Vector{T}, α::Number, β::Number;
-               quirks::Bool=false) where {T}
-    GC.@preserve x y check(ccall((:vbc_sharded_mul, libvbc), Cint,
-        (Ptr{Cvoid}, Cint, Ptr{T}, Int64, Ptr{T}, Int64, Cdouble, Cdouble, Cint, Ptr{Cvoid}, Cuint),
-        A.handle, trans, x, length(x), y, length(y), Float64(α), Float64(β), VBC_MEM_HOST, C_NULL,
-        quirks ? VBC_MUL_REFERENCE_QUIRKS : Cuint(0)))
+Base.size(A::HIPShardedSparseMatrix) = size(A.host)
+Base.size(A::HIPShardedSparseMatrix, d::Integer) = size(A.host, d)
+Base.eltype(A::HIPShardedSparseMatrix) = eltype(A.host)
+
+# Host StridedVectors of any supported eltype: vbc_sharded_mul_ex carries each pointer's eltype and
+# stride (x converted to the compute eltype like multiply_1DVBC.jl:102; a y of another eltype is
+# refused with VBC_UNSUPPORTED_DTYPE), so a mismatch can never over-read or overwrite host memory.
+function _mul!(y::StridedVector{Ty}, A::HIPShardedSparseMatrix, trans::Bool, x::StridedVector{Tx}, α::Number,
+               β::Number; quirks::Bool=false) where {Ty, Tx}
+    GC.@preserve x y check(ccall((:vbc_sharded_mul_ex, libvbc), Cint,
+        (Ptr{Cvoid}, Cint, Ptr{Tx}, Cint, Int64, Int64, Ptr{Ty}, Cint, Int64, Int64, Cdouble, Cdouble, Cint,
+         Ptr{Cvoid}, Cuint),
+        A.handle, trans, pointer(x), vbc_dtype(Tx), stride(x, 1), length(x), pointer(y), vbc_dtype(Ty), stride(y, 1),
+        length(y), Float64(α), Float64(β), VBC_MEM_HOST, C_NULL, quirks ? VBC_MUL_REFERENCE_QUIRKS : Cuint(0)))
     return y
 end
 
-const AdjOrTransSharded = Union{Adjoint{<:Any, <:HIPShardedSparseMatrix1DVBC},
-                                Transpose{<:Any, <:HIPShardedSparseMatrix1DVBC}}
-LinearAlgebra.mul!(y::Vector, A::HIPShardedSparseMatrix1DVBC, x::Vector, α::Number, β::Number) =
+const AdjOrTransSharded = Union{Adjoint{<:Any, <:HIPShardedSparseMatrix}, Transpose{<:Any, <:HIPShardedSparseMatrix}}
+LinearAlgebra.mul!(y::StridedVector, A::HIPShardedSparseMatrix, x::StridedVector, α::Number, β::Number) =
     _mul!(y, A, false, x, α, β)
-LinearAlgebra.mul!(y::Vector, adjA::AdjOrTransSharded, x::Vector, α::Number, β::Number) =
+LinearAlgebra.mul!(y::StridedVector, adjA::AdjOrTransSharded, x::StridedVector, α::Number, β::Number) =
     _mul!(y, parent(adjA), true, x, α, β)
-LinearAlgebra.mul!(y::Vector, A::HIPShardedSparseMatrix1DVBC, x::Vector) = mul!(y, A, x, true, false)
-LinearAlgebra.mul!(y::Vector, adjA::AdjOrTransSharded, x::Vector) = mul!(y, adjA, x, true, false)
+LinearAlgebra.mul!(y::StridedVector, A::HIPShardedSparseMatrix, x::StridedVector) = mul!(y, A, x, true, false)
+LinearAlgebra.mul!(y::StridedVector, adjA::AdjOrTransSharded, x::StridedVector) = mul!(y, adjA, x, true, false)
 
+# Multi-RHS (the reference has no matrix mul!, multiply_1DVBC.jl:184-185): Y = α·op(A)·X + β·Y on
+# column-major matrices of the compute eltype through vbc_mul_mat_ex (eltypes carried; B'X on
+# matrix cores for a handle built with VBC_CREATE_MULTI), other eltypes column by column.
+function LinearAlgebra.mul!(Y::StridedMatrix{T}, adjA::AdjOrTransHIP, X::StridedMatrix{T}, α::Number,
+                            β::Number) where {T <: Union{Float64, Float32}}
+    A = parent(adjA)
+    (stride(X, 1) == 1 && stride(Y, 1) == 1) || return _mul_cols!(Y, adjA, X, α, β)
+    h = handle_for(A, T)
+    GC.@preserve X Y check(ccall((:vbc_mul_mat_ex, libvbc), Cint,
+        (Ptr{Cvoid}, Cint, Int64, Ptr{T}, Cint, Int64, Int64, Ptr{T}, Cint, Int64, Int64, Cdouble, Cdouble, Cint,
+         Ptr{Cvoid}, Cuint),
+        h, 1, size(X, 2), X, vbc_dtype(T), stride(X, 2), size(X, 1), Y, vbc_dtype(T), stride(Y, 2), size(Y, 1),
+        Float64(α), Float64(β), VBC_MEM_HOST, C_NULL, Cuint(0)))
+    return Y
+end
+function _mul_cols!(Y::StridedMatrix, adjA, X::StridedMatrix, α::Number, β::Number)
+    size(X, 2) == size(Y, 2) || throw(DimensionMismatch("X and Y have different numbers of columns"))
+    for c in axes(X, 2)
+        mul!(view(Y, :, c), adjA, view(X, :, c), α, β)
+    end
+    return Y
+end
+LinearAlgebra.mul!(Y::StridedMatrix, adjA::AdjOrTransHIP, X::StridedMatrix, α::Number, β::Number) =
+    _mul_cols!(Y, adjA, X, α, β)
+
+export HIPShardedSparseMatrix
 export HIPSparseMatrix1DVBC, HIPSparseMatrixVBC, HIPSparseMatrixCSC, HIPShardedSparseMatrix1DVBC, TrSpMV!
 
 end # module

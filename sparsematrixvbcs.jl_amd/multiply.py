@@ -156,9 +156,9 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="
     mfma = trans and cdt != _L.VBC_I64 and (engine == "mfma" or (engine == "auto" and nrhs >= MFMA_MIN_RHS))
     h = B.handle(dev, trans, multi=mfma, compute=cdt)
     flags = (_L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0) | (_L.VBC_MAT_ROWMAJOR if lx == "R" else 0)
-    _L.check(_L.lib().vbc_mul_mat(h, int(trans), nrhs, _L.ptr(X), max(ldx, 1), X.shape[0], _L.ptr(Y),
-                                  max(ldy, 1), Y.shape[0], float(alpha), float(beta), mem, stream, flags),
-             "mul!")
+    _L.check(_L.lib().vbc_mul_mat_ex(h, int(trans), nrhs, _L.ptr(X), _L.dtype_code(X.dtype), max(ldx, 1), X.shape[0],
+                                     _L.ptr(Y), _L.dtype_code(Y.dtype), max(ldy, 1), Y.shape[0], float(alpha),
+                                     float(beta), mem, stream, flags), "mul!")
     return Y
 
 

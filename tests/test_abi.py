@@ -161,3 +161,30 @@ def test_sharded_create_validation_without_gpu():
     assert lib.vbc_sharded_count(None, C.byref(n)) == L.VBC_INVALID_ARG
     assert lib.vbc_sharded_shard(None, 0, None, None, None, None) == L.VBC_INVALID_ARG
     assert lib.vbc_sharded_destroy(None) == L.VBC_OK
+
+
+def test_sharded_ex_and_2d_validation_without_gpu():
+    """vbc_sharded_mul_ex / vbc2d_create_sharded reject bad arguments before touching a device; the
+    library reports the ABI version this binding was written for (vbc.h VBC_VERSION, vbc_info size)."""
+    lib = L.lib()
+    assert lib.vbc_version() // 10000 == L.VBC_VERSION_MAJOR
+    assert C.sizeof(L.vbc_info) == L.VBC_INFO_SIZE
+    assert lib.vbc_sharded_mul_ex(None, 1, None, L.VBC_F32, 1, 0, None, L.VBC_F32, 1, 0, 1.0, 0.0,
+                                  L.VBC_MEM_HOST, None, 0) == L.VBC_INVALID_ARG
+    h = C.c_void_p()
+    pspl = np.array([1, 3], np.int64)
+    spl = np.array([1, 3], np.int64)
+    pos = np.array([1, 2], np.int64)
+    idx = np.array([1], np.int64)
+    ofs = np.array([1, 5], np.int64)
+    val = np.ones(4)
+    t = L.vbc_types(L.VBC_F64, 64, L.VBC_F64, 0)
+    devs = (C.c_int * 2)(0, 0)
+    args = (C.byref(h), 2, 2, 2, 2, 1, pspl.ctypes.data, 1, spl.ctypes.data, pos.ctypes.data, idx.ctypes.data,
+            ofs.ctypes.data, val.ctypes.data, 4, C.byref(t))
+    assert lib.vbc2d_create_sharded(*args, 0, devs, L.VBC_SPLIT_STRIPES, 0) == L.VBC_INVALID_ARG
+    assert lib.vbc2d_create_sharded(*args, 2, devs, 9, 0) == L.VBC_INVALID_ARG
+    assert lib.vbc2d_create_sharded(*args[:-1], None, 2, devs, L.VBC_SPLIT_ROWS, 0) == L.VBC_INVALID_ARG
+    assert lib.vbc2d_create_sharded(C.byref(h), 2, 2, 2, 2, 1, None, *args[7:], 2, devs, 0, 0) == L.VBC_INVALID_ARG
+    assert lib.vbc_mul_mat_ex(None, 1, 1, None, L.VBC_F64, 1, 0, None, L.VBC_F64, 1, 0, 1.0, 0.0,
+                              L.VBC_MEM_HOST, None, 0) == L.VBC_INVALID_ARG

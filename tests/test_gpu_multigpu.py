@@ -110,3 +110,182 @@ def test_sharded_more_shards_than_stripes():
         V.mul_(yf, S, dev(xf))
         assert np.allclose(yf.cpu().numpy(), A @ xf)
         S.release()
+
+
+# ---- round 3: eltypes and strides on the sharded boundary, the 2D sharded handle, RCCL over real GPUs --
+
+def _x_as_compute(x):
+    return np.asarray(x, dtype=np.float64)
+
+
+@pytest.mark.parametrize("split", ["stripes", "rows"])
+def test_sharded_mixed_eltypes_and_strides(mat, split):
+    """vbc_sharded_mul_ex: x of another eltype is converted (multiply_1DVBC.jl:102), strided x / y
+    views are read and written in place, and a y of another float eltype is refused -- host and
+    device operands, both directions."""
+    B = mat
+    R = ref_of(B)
+    rng = np.random.default_rng(21)
+    for devices in ([0], [0, 0, 0]):
+        S = D.MultiGPUSparseMatrix1DVBC(B, devices=devices, split=split)
+        for trans in (True, False):
+            nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+            x32 = rng.uniform(-1, 1, nx).astype(np.float32)
+            xi = rng.integers(-5, 6, nx).astype(np.int32)
+            y0 = rng.uniform(-1, 1, ny)
+            for x in (x32, xi):
+                ref = O.mul(R, _x_as_compute(x), y0.copy(), 0.5, 2.0, trans=trans, ref_semantics=False)
+                yh = y0.copy()
+                V.mul_(yh, S.T if trans else S, x, 0.5, 2.0)  # host, converted x
+                assert rel(yh, ref) <= TOL64, (split, devices, trans, x.dtype)
+                yd = dev(y0.copy())
+                V.mul_(yd, S.T if trans else S, torch.from_numpy(x).to(DEV), 0.5, 2.0)  # device, converted x
+                assert rel(yd.cpu().numpy(), ref) <= TOL64
+            # strided views: every other element of a wider buffer; the gaps stay untouched
+            xs = rng.uniform(-1, 1, 2 * nx)
+            ys = np.full(3 * ny, 7.0)
+            ys[::3] = y0
+            ref = O.mul(R, xs[::2].copy(), y0.copy(), 1.0, -1.0, trans=trans, ref_semantics=False)
+            V.mul_(ys[::3], S.T if trans else S, xs[::2], 1.0, -1.0)
+            assert rel(ys[::3], ref) <= TOL64
+            assert np.all(ys[1::3] == 7.0) and np.all(ys[2::3] == 7.0)
+            xt = dev(xs)
+            yt = dev(np.full(3 * ny, 7.0))
+            yt[::3] = dev(y0)
+            V.mul_(yt[::3], S.T if trans else S, xt[::2], 1.0, -1.0)
+            got = yt.cpu().numpy()
+            assert rel(got[::3], ref) <= TOL64
+            assert np.all(got[1::3] == 7.0) and np.all(got[2::3] == 7.0)
+            with pytest.raises(V.UnsupportedDtype):  # eltype(y) != the handle's compute eltype
+                V.mul_(np.zeros(ny, np.float32), S.T if trans else S, x32)
+            with pytest.raises(V.UnsupportedDtype):
+                V.mul_(torch.zeros(ny, dtype=torch.float32, device=DEV), S.T if trans else S,
+                       torch.from_numpy(x32).to(DEV))
+        S.release()
+
+
+def test_sharded_ex_never_reads_past_a_host_buffer(mat):
+    """A Float32 x whose last element ends a page followed by an inaccessible page: the converting
+    product reads exactly length(x) Float32s (the round-2 ABI read it as Float64 and overran); a
+    Float32 y on the Float64 handle is refused before any access."""
+    import ctypes as C
+    import mmap
+    B = mat
+    libc = C.CDLL(None)
+    libc.mprotect.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+    page = mmap.PAGESIZE
+    nbytes = max(B.m, B.n) * 4
+    npages = (nbytes + page - 1) // page
+    buf = mmap.mmap(-1, (npages + 1) * page)
+    base = C.addressof(C.c_char.from_buffer(buf))
+    assert libc.mprotect(base + npages * page, page, 0) == 0  # PROT_NONE guard page
+    x = np.frombuffer(buf, dtype=np.float32, count=B.m, offset=npages * page - B.m * 4)
+    x[:] = np.random.default_rng(4).uniform(-1, 1, B.m).astype(np.float32)
+    S = D.MultiGPUSparseMatrix1DVBC(B, devices=[0, 0], split="stripes")
+    y = np.zeros(B.n)
+    V.mul_(y, S.T, x)
+    ref = O.mul(ref_of(B), x.astype(np.float64), np.zeros(B.n), trans=True)
+    assert rel(y, ref) <= TOL64
+    y32 = np.frombuffer(buf, dtype=np.float32, count=B.n, offset=npages * page - B.n * 4)
+    L = V._lib
+    st = L.lib().vbc_sharded_mul_ex(S._h, 1, x.ctypes.data, L.VBC_F32, 1, B.m, y32.ctypes.data, L.VBC_F32, 1, B.n,
+                                    1.0, 0.0, L.VBC_MEM_HOST, None, 0)
+    assert st == L.VBC_UNSUPPORTED_DTYPE
+    S.release()
+    del x, y32
+    assert libc.mprotect(base + npages * page, page, 3) == 0  # PROT_READ | PROT_WRITE again
+
+
+def _vbc2d(seed, dtype=np.float64):
+    import scipy.sparse as sp
+    A = sp.random(700, 520, density=0.02, random_state=seed, format="csc", dtype=np.float64)
+    A.data = np.random.default_rng(seed).uniform(-1, 1, A.nnz)
+    B = V.SparseMatrixVBC[4, 4](A.astype(dtype), V.AlternatingPacker(V.OverlapChunker(0.9, 4), V.OverlapChunker(0.9, 4)))
+    return B
+
+
+@pytest.mark.parametrize("split", ["stripes", "rows"])
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_sharded_vbc2d(split, devices):
+    """vbc2d_create_sharded (multiply_VBC.jl:182-189 threaded the same way): both splits, both
+    directions, α/β, device and host operands, against the oracle's VBC products; the row split
+    keeps Π's block rows whole."""
+    B = _vbc2d(3)
+    R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    S = D.MultiGPUSparseMatrix(B, devices=devices, split=split)
+    assert S.is2d
+    if split == "rows":
+        bounds = set(int(b) - 1 for b in B.Pi.spl)
+        assert all(lo in bounds and hi in bounds for lo, hi, _ in S.shards())
+    rng = np.random.default_rng(9)
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        for alpha, beta in ((1.0, 0.0), (-0.5, 3.0)):
+            x = rng.uniform(-1, 1, nx)
+            y0 = rng.uniform(-1, 1, ny)
+            ref = O.mul(R, x, y0.copy(), alpha, beta, trans=trans, ref_semantics=False)
+            y = dev(y0.copy())
+            V.mul_(y, S.T if trans else S, dev(x), alpha, beta)
+            assert rel(y.cpu().numpy(), ref) <= TOL64, (split, devices, trans, alpha)
+            yh = y0.copy()
+            V.mul_(yh, S.T if trans else S, x, alpha, beta)
+            assert rel(yh, ref) <= TOL64
+        # one-hot probes (runtests.jl:63-87): exact on every shard layout
+        for j in (0, nx // 3, nx - 1):
+            e = np.zeros(nx)
+            e[j] = 1.0
+            ref = O.mul(R, e, np.zeros(ny), trans=trans)
+            y = dev(np.zeros(ny))
+            V.mul_(y, S.T if trans else S, dev(e))
+            assert np.array_equal(y.cpu().numpy(), ref)
+    S.release()
+
+
+def test_sharded_serial_flag_bit_identical_on_split_product_sizes():
+    """a small stripe shard may choose the split planar product (P slices per chunk) while
+    the whole matrix does not.  With serial=True (VBC_CREATE_SERIAL) every shard keeps the
+    reference's serial per-stripe order: the stripe-sharded B'x equals the single-GPU product and
+    the oracle bit for bit on the ct20stif stand-in, whose own default layout splits."""
+    A = V.synthetic.standin("Boeing/ct20stif", dtype=np.float64, seed=5)
+    B = V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
+    assert B.info(0, True)["planar_split"] > 1  # the default layout folds chunks in slices
+    B.release()
+    B.serial = True
+    assert B.info(0, True)["planar_split"] == 1
+    x = np.random.default_rng(2).uniform(-1, 1, B.m)
+    y1 = dev(np.zeros(B.n))
+    V.mul_(y1, B.T, dev(x))
+    ref = O.mul(ref_of(B), x, np.zeros(B.n), trans=True)
+    assert np.array_equal(y1.cpu().numpy(), ref)
+    S = D.MultiGPUSparseMatrix1DVBC(B, devices=[0] * 8, split="stripes", forward=False, serial=True)
+    y8 = dev(np.full(B.n, np.nan))
+    V.mul_(y8, S.T, dev(x))
+    assert torch.equal(y1, y8)
+    S.release()
+    B.release()
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs two GPUs (RCCL exchange between distinct devices)")
+@pytest.mark.parametrize("split", ["stripes", "rows"])
+def test_sharded_distinct_devices_rccl(mat, split):
+    """the RCCL exchange between distinct devices (broadcast / send-recv of x, the β slices,
+    the y gather or ncclReduce) against the oracle and the single-GPU handle, both directions, β != 0."""
+    B = mat
+    R = ref_of(B)
+    S = D.MultiGPUSparseMatrix1DVBC(B, devices=[0, 1], split=split)
+    rng = np.random.default_rng(33)
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        x = rng.uniform(-1, 1, nx)
+        y0 = rng.uniform(-1, 1, ny)
+        ref = O.mul(R, x, y0.copy(), 0.75, -1.5, trans=trans, ref_semantics=False)
+        y = dev(y0.copy())
+        V.mul_(y, S.T if trans else S, dev(x), 0.75, -1.5)
+        torch.cuda.synchronize()
+        assert rel(y.cpu().numpy(), ref) <= TOL64
+        y1 = dev(y0.copy())
+        V.mul_(y1, B.T if trans else B, dev(x), 0.75, -1.5)
+        if (split == "stripes") == trans:  # disjoint slices: the single-GPU result bit for bit
+            assert torch.equal(y, y1)
+    S.release()
