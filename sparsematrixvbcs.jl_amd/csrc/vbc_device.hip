@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstring>
 #include <cmath>
@@ -156,6 +157,8 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
 struct PendingSlot {
     SlotBin b;
     size_t o_key, o_val, o_out, o_rrow, o_rchunk, o_base = 0, o_doff = 0, o_nlive = 0;
+    size_t o_trow = 0, o_tseg = 0, o_lseg = 0;  // lanes layout (build_lanes)
+    bool lanes_done = false;                    // keys already stored (build_lanes: 32-bit keys per run)
     int64_t key_bytes = 0;       // index bytes as stored (keys, deltas, bases, delta offsets)
     std::vector<uint32_t> keys;  // full keys until commit_slot_keys picks the stored form
     int64_t rows = 0;
@@ -608,12 +611,210 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     return VBC_OK;
 }
 
+// Per-lane compacted streams (SlotBin::lanes, vbc_planar.h run_planar_lanes) for a planar B'x bucket in
+// natural order with contiguous outputs (out[q] = out[0] + q * w, wsrc == w).  Tiles of S consecutive
+// stripes (S a multiple of 4, at most one LDS tile buffer: 512 fp64 / 1024 fp32 3-wide stripes), k
+// tiles per range, the ranges ~ the kernel's resident waves; inside a tile the stripes are cut into 64
+// contiguous sub-blocks minimising the longest stream (binary search on the step count), and the
+// sub-blocks go to the lanes by decreasing length, so the live lanes of every step are a prefix.
+// An empty stripe is one zero run with PAD | LAST.  ents[sbeg[q] ..] are stripe q's rows (gather index
+// keys), rows in runs of `run`.
+// Whether a planar B'x bucket runs the lane-stream layout: VBC_PLANAR_LANES=1 forces it (where
+// representable), 0 never; auto: a bucket the masked order would take (natural order pads beyond
+// slots_pad) with natural contiguous outputs, few empty stripes, and >= 256 stripes per resident wave
+// (sub-blocks of ~4 stripes per lane balance the streams).
+static bool want_lanes(const vbc_handle *h, int wps, int w, const std::vector<int64_t> &sbeg,
+                       const std::vector<int32_t> &out, int64_t total_entries, bool mask)
+{
+    if (h->planar_lanes == 0 || !slot_planar(h, 0, w) || wps != w) return false;
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    if (nseg < 64 || nseg >= (int64_t(1) << 31)) return false;
+    for (size_t q = 1; q < out.size(); q++)
+        if ((int64_t)out[q] != (int64_t)out[0] + (int64_t)q * w) return false;
+    int64_t empty = 0;
+    for (int64_t q = 0; q < nseg; q++) empty += sbeg[q + 1] == sbeg[q];
+    if (h->planar_lanes == 1) return true;
+    if (!mask || empty * 100 > nseg) return false;
+    const int64_t real = sbeg[nseg] - sbeg[0];
+    const double share = (double)h->target_ranges_l * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    return (double)nseg >= 256.0 * std::max(1.0, share);
+}
+
+static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, const std::vector<int64_t> &sbeg,
+                       const std::vector<int32_t> &out, int run, int64_t total_entries, const char *val, Arena &ar,
+                       PendingSlot &ps)
+{
+    const int esz = h->esz;
+    const int64_t nseg = (int64_t)sbeg.size() - 1;
+    const int64_t real = sbeg[nseg] - sbeg[0];
+    std::vector<int32_t> len(nseg);  // runs per stripe (an empty stripe: one zero run)
+    for (int64_t q = 0; q < nseg; q++) len[q] = (int32_t)std::max<int64_t>(1, (sbeg[q + 1] - sbeg[q]) / run);
+    const int smax = (kLaneTileBytes / (w * esz)) & ~3;
+    const double share = (double)h->target_ranges_l * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    int64_t nr = std::max<int64_t>(1, std::llround(share));
+    const int64_t k = std::min<int64_t>(kLaneMaxTiles, std::max<int64_t>(1, (nseg + nr * smax - 1) / (nr * smax)));
+    int64_t S = (nseg + k * nr - 1) / (k * nr);
+    S = std::min<int64_t>(smax, std::max<int64_t>(4, (S + 3) / 4 * 4));
+    const int64_t ntiles = (nseg + S - 1) / S;
+    nr = (ntiles + k - 1) / k;
+    // per tile: 64 contiguous parts (first stripe of each), their stream lengths, steps
+    std::vector<int32_t> trow{0}, tseg;
+    std::vector<int16_t> lseg((size_t)ntiles * 64);
+    std::vector<std::vector<int32_t>> parts((size_t)ntiles);  // per tile: lane -> [first stripe, last+1) pairs
+    int64_t rows = 0;
+    for (int64_t t = 0; t < ntiles; t++) {
+        const int64_t a = t * S, e = std::min(nseg, a + S);
+        tseg.push_back((int32_t)a);
+        int64_t lo = 0, hi = 0;
+        for (int64_t q = a; q < e; q++) {
+            lo = std::max<int64_t>(lo, len[q]);
+            hi += len[q];
+        }
+        auto nparts = [&](int64_t cap) {
+            int64_t p = 1, cur = 0;
+            for (int64_t q = a; q < e; q++) {
+                if (cur + len[q] > cap) { p++; cur = len[q]; }
+                else cur += len[q];
+            }
+            return p;
+        };
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (nparts(mid) <= 64) hi = mid;
+            else lo = mid + 1;
+        }
+        const int64_t T = lo;
+        std::vector<std::array<int64_t, 3>> pv;  // {length, first stripe, end}
+        int64_t cur = 0, first = a;
+        for (int64_t q = a; q < e; q++) {
+            if (cur + len[q] > T) { pv.push_back({cur, first, q}); first = q; cur = 0; }
+            cur += len[q];
+        }
+        pv.push_back({cur, first, e});
+        std::stable_sort(pv.begin(), pv.end(), [](const std::array<int64_t, 3> &p, const std::array<int64_t, 3> &q) {
+            return p[0] > q[0];
+        });
+        std::vector<int32_t> &pt = parts[t];
+        for (int l = 0; l < 64; l++) {
+            const bool has = l < (int)pv.size();
+            lseg[(size_t)t * 64 + l] = (int16_t)(has ? pv[l][1] - a : e - a);
+            pt.push_back(has ? (int32_t)pv[l][1] : (int32_t)e);
+            pt.push_back(has ? (int32_t)pv[l][2] : (int32_t)e);
+        }
+        rows += T * run;
+        trow.push_back((int32_t)rows);
+    }
+    tseg.push_back((int32_t)nseg);
+    if (rows * 64 >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "lane-stream layout too large");
+    std::vector<int32_t> rrow, rchunk;
+    for (int64_t r = 0; r < nr; r++) {
+        rchunk.push_back((int32_t)(r * k));
+        rrow.push_back(trow[(size_t)(r * k)]);
+    }
+    rchunk.push_back((int32_t)ntiles);
+    rrow.push_back((int32_t)rows);
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] lanes bin w %d run %d stripes %lld tiles %lld x %lld stripes, %lld per range, ranges %lld, "
+                "rows %lld (real %lld: %.3f)\n", w, run, (long long)nseg, (long long)ntiles, (long long)S, (long long)k,
+                (long long)nr, (long long)rows, (long long)real, (double)real / (double)std::max<int64_t>(1, rows * 64));
+    ps = PendingSlot{};
+    SlotBin &b = ps.b;
+    b.kind = 0;
+    b.wkey = w;
+    b.w = w;
+    b.wst = w;
+    b.rpi = 64;
+    b.nranges = (int32_t)nr;
+    b.nseg = (int32_t)nseg;
+    b.u = h->slot_u;
+    b.diag = h->diag;
+    b.xcd = h->xcd_p;
+    b.spl = 1;
+    b.planar = 1;
+    b.run = run;
+    b.split = 1;
+    b.mask = 1;
+    b.lanes = 1;
+    b.ntiles = (int32_t)ntiles;
+    b.out_affine = 1;
+    b.out_base = out.empty() ? 0 : out[0];
+    b.out_stride = w;
+    b.contig = 1;
+    ps.rows = rows;
+    ps.real = real;
+    ps.o_val = ar.reserve((size_t)rows * 64 * w * esz);
+    ps.o_out = ar.reserve(4);
+    ps.o_rrow = ar.reserve(rrow.size() * 4);
+    ps.o_rchunk = ar.reserve(rchunk.size() * 4);
+    ps.o_nlive = ar.reserve((size_t)rows * 4);
+    ps.o_trow = ar.reserve(trow.size() * 4);
+    ps.o_tseg = ar.reserve(tseg.size() * 4);
+    ps.o_lseg = ar.reserve(lseg.size() * 2);
+    ps.o_key = ar.reserve((size_t)rows * 64 * 4);
+    ps.key_bytes = (int64_t)(real / run) * 4;  // one key per run is read
+    ps.lanes_done = true;
+    std::memcpy(ar.at<int32_t>(ps.o_rrow), rrow.data(), rrow.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_rchunk), rchunk.data(), rchunk.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_trow), trow.data(), trow.size() * 4);
+    std::memcpy(ar.at<int32_t>(ps.o_tseg), tseg.data(), tseg.size() * 4);
+    std::memcpy(ar.at<int16_t>(ps.o_lseg), lseg.data(), lseg.size() * 2);
+    *ar.at<int32_t>(ps.o_out) = b.out_base;
+    uint32_t *key = ar.at<uint32_t>(ps.o_key);
+    uint32_t *nlv = ar.at<uint32_t>(ps.o_nlive);
+    char *vv = ar.at<char>(ps.o_val);
+    std::memset(vv, 0, (size_t)rows * 64 * w * esz);
+    std::memset(key, 0, (size_t)rows * 64 * 4);
+    for (int64_t t = 0; t < ntiles; t++) {
+        const int64_t R0 = trow[t], T = (trow[t + 1] - R0) / run;
+        for (int64_t st = 0; st < T; st++) {
+            uint32_t nl = 0;
+            for (int l = 0; l < 64; l++) {
+                const int32_t qa = parts[t][2 * l], qb = parts[t][2 * l + 1];
+                int64_t tot = 0;
+                for (int32_t q = qa; q < qb; q++) tot += len[q];
+                if (tot > st) nl = (uint32_t)(l + 1);
+            }
+            for (int d = 0; d < run; d++) nlv[R0 + st * run + d] = nl;
+        }
+        for (int l = 0; l < 64; l++) {
+            int64_t st = 0;
+            for (int32_t q = parts[t][2 * l]; q < parts[t][2 * l + 1]; q++) {
+                const int64_t nrun = (sbeg[q + 1] - sbeg[q]) / run;
+                if (nrun == 0) {  // empty stripe: one zero run, PAD | LAST (writes its zeros)
+                    key[(R0 + st * run) * 64 + l] = kPad | kLast;
+                    st++;
+                    continue;
+                }
+                for (int64_t u = 0; u < nrun; u++, st++) {
+                    const int64_t row0 = R0 + st * run;
+                    key[row0 * 64 + l] = ents[sbeg[q] + u * run].key | (u + 1 == nrun ? kLast : 0u);
+                    for (int d = 0; d < run; d++) {
+                        const Entry &en = ents[sbeg[q] + u * run + d];
+                        char *rowp = vv + (row0 + d) * 64 * w * esz;
+                        for (int cc = 0; cc < w; cc++)
+                            std::memcpy(rowp + planar_off(esz, w, l, cc) * esz, val + (en.voff + cc) * esz, (size_t)esz);
+                    }
+                }
+            }
+        }
+    }
+    h->slot_rows_padded += rows * 64;
+    h->slot_rows_real += real;
+    h->slot_rows_padded_last = rows * 64;
+    return VBC_OK;
+}
+
 // One launch's slotted bins share one key form (the kernel is specialised on it).
 static void commit_launch_keys(const vbc_handle *h, std::vector<PendingSlot> &pss, Arena &ar)
 {
-    bool kc = !pss.empty();
-    for (const PendingSlot &ps : pss) kc = kc && ps.kc_ok;
-    for (PendingSlot &ps : pss) commit_slot_keys(ps, kc, ar, h->slot_dedup);
+    bool kc = false;
+    for (const PendingSlot &ps : pss) {
+        if (ps.lanes_done) continue;  // the lanes layout stores its own keys (its own launch)
+        kc = true;
+    }
+    for (const PendingSlot &ps : pss) kc = kc && (ps.lanes_done || ps.kc_ok);
+    for (PendingSlot &ps : pss)
+        if (!ps.lanes_done) commit_slot_keys(ps, kc, ar, h->slot_dedup);
 }
 
 // ---- row-swept layout (vbc_sweep.hip) ------------------------------------------------------------
@@ -824,7 +1025,11 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                     ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
             }
             PendingSlot ps;
-            if (int st = build_slots(h, 0, wps, w, ents, sbeg, out, total, val, ar, srange0, ps, order, mask)) return st;
+            if (want_lanes(h, wps, w, sbeg, out, total, mask)) {
+                if (int st = build_lanes(h, w, ents, sbeg, out, slot_runs(h, ents, sbeg), total, val, ar, ps)) return st;
+            } else if (int st = build_slots(h, 0, wps, w, ents, sbeg, out, total, val, ar, srange0, ps, order, mask)) {
+                return st;
+            }
             pss.push_back(std::move(ps));
             continue;
         }
@@ -848,7 +1053,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     }
     commit_launch_keys(h, pss, ar);
     for (const PendingSlot &ps : pss) {  // slotted bins: padded rows x (index bytes + values)
-        if (ps.b.mask) {  // masked: padding lanes fetch nothing; + the per-row live counts
+        if (ps.b.lanes) {  // lanes: real rows' values, one key per run, nlive per row, the tile tables
+            h->bytes_t += ps.real * (int64_t)ps.b.w * h->esz + ps.key_bytes + ps.rows * 4 + (int64_t)ps.b.ntiles * (8 + 128);
+        } else if (ps.b.mask) {  // masked: padding lanes fetch nothing; + the per-row live counts
             const double f = (double)ps.real / (double)std::max<int64_t>(1, ps.rows * ps.b.rpi);
             h->bytes_t += ps.real * (int64_t)ps.b.w * h->esz + (int64_t)(f * (double)ps.key_bytes) + ps.rows * 4;
         } else {
@@ -1308,6 +1515,9 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.base = reinterpret_cast<const uint32_t *>(base + ps.o_base);
         b.kdoff = reinterpret_cast<const uint32_t *>(base + ps.o_doff);
         b.nlive = reinterpret_cast<const uint32_t *>(base + ps.o_nlive);
+        b.trow = reinterpret_cast<const int32_t *>(base + ps.o_trow);
+        b.tseg = reinterpret_cast<const int32_t *>(base + ps.o_tseg);
+        b.lseg = reinterpret_cast<const int16_t *>(base + ps.o_lseg);
         (b.planar ? L.pbins : L.sbins).push_back(b);
     }
     if (!L.pbins.empty()) {
@@ -1484,6 +1694,9 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     }
     if (flags & VBC_CREATE_SERIAL) h->planar_split = 0;  // every stripe summed serially in stored row order
     h->occ_p = std::max(1, std::min(occupancy_planar(h->esz), 8));
+    h->target_ranges_l = prop.multiProcessorCount * std::max(1, std::min(occupancy_lanes(h->esz), 8)) * kWavesPerBlock;
+    if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = getenv("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));
@@ -1795,7 +2008,8 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
             info->planar_run = std::max<int32_t>(info->planar_run, b.run);
             info->planar_split = std::max<int32_t>(info->planar_split, b.split);
             info->planar_pair = std::max<int32_t>(info->planar_pair, b.pair);
-            info->planar_mask = std::max<int32_t>(info->planar_mask, b.mask);
+            info->planar_mask = std::max<int32_t>(info->planar_mask & 1, b.mask) | (info->planar_mask & ~1);
+            if (b.lanes) info->planar_mask |= 4;
         }
     info->fwd_run = 1;
     if (h->has_f)

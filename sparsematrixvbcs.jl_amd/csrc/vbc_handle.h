@@ -128,6 +128,9 @@ struct vbc_handle {
                                       // ldoor fp32 37.2 / 37.1 / 36.5 / 36.3)
     int planar_split = -1;            // VBC_PLANAR_SPLIT: -1 auto (few chunks), 0 never, 2 / 4 / 8 waves per chunk
     int target_ranges_p = 4096;       // resident waves of the planar kernel
+    int target_ranges_l = 4096;       // resident waves of the lane-stream planar kernel
+    int planar_lanes = -1;            // VBC_PLANAR_LANES: -1 auto, 0 never, 1 always (planar B'x buckets with
+                                      // natural contiguous outputs): per-lane compacted streams (run_planar_lanes)
     int occ_p = 4;                    // workgroups per CU of the planar kernel
     int sweep_mode = -1;              // VBC_SWEEP: -1 auto (no x locality), 0 never, 1 always (w <= 8)
     int sweep_tile = vbc::kSweepTileBytes;  // VBC_SWEEP_TILE=16: 16 KB of LDS accumulators per wave

@@ -106,6 +106,14 @@ struct SlotBin {
     const int32_t *rrow;   // per range: first row, nranges + 1 entries
     const int32_t *rchunk; // per range: first chunk
     const uint32_t *nlive; // mask: per row, live lanes (a prefix: lanes are in decreasing length order)
+    // lanes (planar B'x, vbc_planar.h run_planar_lanes): per-lane compacted streams.  A tile is a run of
+    // consecutive stripes dealt to the 64 lanes as contiguous sub-blocks balanced by rows; rchunk[r] is
+    // the range's first tile, rrow[r] its first row.
+    int32_t lanes;         // 1: per-lane streams (then mask = 1: nlive per row, dead lanes a suffix)
+    int32_t ntiles;
+    const int32_t *trow;   // ntiles + 1: first row of each tile
+    const int32_t *tseg;   // ntiles + 1: first segment of each tile
+    const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)
 };
 
 // XCD-aware workgroup order: the hardware deals workgroups round-robin over the 8 XCDs, so logical
@@ -163,6 +171,7 @@ int occupancy_slots(int esz, int kind);
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                   double alpha, double beta, bool rd, hipStream_t s);
 int occupancy_planar(int esz);
+int occupancy_lanes(int esz);
 
 __host__ __device__ constexpr int vec_elems(int esz, int w)
 {

@@ -138,10 +138,56 @@ static int launch_fwd(const SlotBin &hb, const SlotBin *d_b, bool faste, bool st
     return (int)hipErrorInvalidValue;
 }
 
+// per-lane compacted streams (vbc_planar.h run_planar_lanes): w in 3..8, runs of 1..3
+template <typename T, int RUN>
+static int launch_lanes_r(const SlotBin &hb, const SlotBin *d_b, const void *x, void *y, double alpha, double beta,
+                          bool rd, hipStream_t s)
+{
+    const int grid = (hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
+    const T *xs = static_cast<const T *>(x);
+    T *ys = static_cast<T *>(y);
+#define VBC_LANES(W)                                                                                      \
+    case W:                                                                                               \
+        hipLaunchKernelGGL((spmv_planar_lanes<T, W, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, \
+                           (T)alpha, (T)beta, (int)rd);                                                   \
+        break;
+    switch (hb.wkey) {
+        VBC_LANES(3) VBC_LANES(4) VBC_LANES(5) VBC_LANES(6) VBC_LANES(7) VBC_LANES(8)
+    default: return (int)hipErrorInvalidValue;
+    }
+#undef VBC_LANES
+    return (int)hipGetLastError();
+}
+
+template <typename T>
+static int launch_lanes(const SlotBin &hb, const SlotBin *d_b, const void *x, void *y, double alpha, double beta,
+                        bool rd, hipStream_t s)
+{
+    switch (hb.run) {
+    case 1: return launch_lanes_r<T, 1>(hb, d_b, x, y, alpha, beta, rd, s);
+    case 2: return launch_lanes_r<T, 2>(hb, d_b, x, y, alpha, beta, rd, s);
+    case 3: return launch_lanes_r<T, 3>(hb, d_b, x, y, alpha, beta, rd, s);
+    default: return (int)hipErrorInvalidValue;
+    }
+}
+
+int occupancy_lanes(int esz)
+{
+    int occ = 0;
+    if (esz == 8) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar_lanes<double, 3, 3>, kBlockThreads, 0);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar_lanes<float, 3, 3>, kBlockThreads, 0);
+    return occ;
+}
+
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                   double alpha, double beta, bool rd, hipStream_t s)
 {
     if (hb.nranges <= 0) return (int)hipSuccess;
+    if (hb.lanes) {  // per-lane compacted streams (B'x)
+        if (hb.kind != 0) return (int)hipErrorInvalidValue;
+        return esz == 8 ? launch_lanes<double>(hb, d_b, x, y, alpha, beta, rd, s)
+                        : launch_lanes<float>(hb, d_b, x, y, alpha, beta, rd, s);
+    }
     if (hb.kind == 1) {  // forward with row runs (vbc_planar.h run_planar_fwd)
         if (esz == 8)
             return hb.kc ? launch_fwd<double, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
