@@ -105,6 +105,9 @@ def kernel_name(B, local, k):
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     inf = B.info(local, True)
     if inf["planar_bins"] > 0:
+        if inf["planar_mask"] & 4:
+            return (f"vbc::spmv_planar_lanes<T, W, RUN={inf['planar_run']}, DEEP, RD> (per-lane compacted streams: "
+                    "tiles of stripes dealt to the lanes, csrc/vbc_planar.h)")
         if inf["planar_pair"]:
             return ("vbc::spmv_planar_pair<FASTE, NB, KC, MASK> (lane pairs, fp64 3-wide runs of 3"
                     + (", masked chunk-local order" if inf["planar_mask"] else "") + ", csrc/vbc_planar.h)")

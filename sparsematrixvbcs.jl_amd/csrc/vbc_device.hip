@@ -649,14 +649,15 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     const int64_t real = sbeg[nseg] - sbeg[0];
     std::vector<int32_t> len(nseg);  // runs per stripe (an empty stripe: one zero run)
     for (int64_t q = 0; q < nseg; q++) len[q] = (int32_t)std::max<int64_t>(1, (sbeg[q + 1] - sbeg[q]) / run);
-    const int smax = (kLaneTileBytes / (w * esz)) & ~3;
     const double share = (double)h->target_ranges_l * (double)real / (double)std::max<int64_t>(total_entries, 1);
-    int64_t nr = std::max<int64_t>(1, std::llround(share));
-    const int64_t k = std::min<int64_t>(kLaneMaxTiles, std::max<int64_t>(1, (nseg + nr * smax - 1) / (nr * smax)));
-    int64_t S = (nseg + k * nr - 1) / (k * nr);
+    const int64_t nr_target = std::max<int64_t>(1, std::llround(share));
+    // one tile per range (a wave) of at most one LDS tile buffer of outputs; S a multiple of 4 stripes,
+    // the ranges a whole number of rounds of the resident waves
+    const int64_t smax = (kLaneTileBytes / (w * esz)) & ~3;
+    const int64_t rounds = std::max<int64_t>(1, (nseg + nr_target * smax - 1) / (nr_target * smax));
+    int64_t S = (nseg + rounds * nr_target - 1) / (rounds * nr_target);
     S = std::min<int64_t>(smax, std::max<int64_t>(4, (S + 3) / 4 * 4));
-    const int64_t ntiles = (nseg + S - 1) / S;
-    nr = (ntiles + k - 1) / k;
+    const int64_t ntiles = (nseg + S - 1) / S, nr = ntiles;
     // per tile: 64 contiguous parts (first stripe of each), their stream lengths, steps
     std::vector<int32_t> trow{0}, tseg;
     std::vector<int16_t> lseg((size_t)ntiles * 64);
@@ -700,23 +701,20 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
             lseg[(size_t)t * 64 + l] = (int16_t)(has ? pv[l][1] - a : e - a);
             pt.push_back(has ? (int32_t)pv[l][1] : (int32_t)e);
             pt.push_back(has ? (int32_t)pv[l][2] : (int32_t)e);
+            pt.push_back(has ? (int32_t)pv[l][0] : 0);  // the lane's stream length (runs)
         }
         rows += T * run;
         trow.push_back((int32_t)rows);
     }
     tseg.push_back((int32_t)nseg);
     if (rows * 64 >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "lane-stream layout too large");
-    std::vector<int32_t> rrow, rchunk;
-    for (int64_t r = 0; r < nr; r++) {
-        rchunk.push_back((int32_t)(r * k));
-        rrow.push_back(trow[(size_t)(r * k)]);
-    }
-    rchunk.push_back((int32_t)ntiles);
-    rrow.push_back((int32_t)rows);
+    const std::vector<int32_t> &rrow = trow;  // one tile per range
+    std::vector<int32_t> rchunk(nr + 1);
+    for (int64_t r = 0; r <= nr; r++) rchunk[r] = (int32_t)r;
     if (getenv("VBC_VERBOSE"))
-        fprintf(stderr, "[vbc] lanes bin w %d run %d stripes %lld tiles %lld x %lld stripes, %lld per range, ranges %lld, "
-                "rows %lld (real %lld: %.3f)\n", w, run, (long long)nseg, (long long)ntiles, (long long)S, (long long)k,
-                (long long)nr, (long long)rows, (long long)real, (double)real / (double)std::max<int64_t>(1, rows * 64));
+        fprintf(stderr, "[vbc] lanes bin w %d run %d stripes %lld ranges %lld x %lld stripes (target %d), rows %lld "
+                "(real %lld: %.3f)\n", w, run, (long long)nseg, (long long)nr, (long long)S, h->target_ranges_l,
+                (long long)rows, (long long)real, (double)real / (double)std::max<int64_t>(1, rows * 64));
     ps = PendingSlot{};
     SlotBin &b = ps.b;
     b.kind = 0;
@@ -735,6 +733,7 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     b.split = 1;
     b.mask = 1;
     b.lanes = 1;
+    b.deep = h->lanes_deep;
     b.ntiles = (int32_t)ntiles;
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
@@ -767,18 +766,13 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     for (int64_t t = 0; t < ntiles; t++) {
         const int64_t R0 = trow[t], T = (trow[t + 1] - R0) / run;
         for (int64_t st = 0; st < T; st++) {
-            uint32_t nl = 0;
-            for (int l = 0; l < 64; l++) {
-                const int32_t qa = parts[t][2 * l], qb = parts[t][2 * l + 1];
-                int64_t tot = 0;
-                for (int32_t q = qa; q < qb; q++) tot += len[q];
-                if (tot > st) nl = (uint32_t)(l + 1);
-            }
+            uint32_t nl = 0;  // lanes are in decreasing stream length: the live ones are a prefix
+            while (nl < 64 && parts[t][3 * nl + 2] > st) nl++;
             for (int d = 0; d < run; d++) nlv[R0 + st * run + d] = nl;
         }
         for (int l = 0; l < 64; l++) {
             int64_t st = 0;
-            for (int32_t q = parts[t][2 * l]; q < parts[t][2 * l + 1]; q++) {
+            for (int32_t q = parts[t][3 * l]; q < parts[t][3 * l + 1]; q++) {
                 const int64_t nrun = (sbeg[q + 1] - sbeg[q]) / run;
                 if (nrun == 0) {  // empty stripe: one zero run, PAD | LAST (writes its zeros)
                     key[(R0 + st * run) * 64 + l] = kPad | kLast;
@@ -1697,6 +1691,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     h->target_ranges_l = prop.multiProcessorCount * std::max(1, std::min(occupancy_lanes(h->esz), 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));

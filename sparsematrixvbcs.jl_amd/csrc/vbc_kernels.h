@@ -111,6 +111,7 @@ struct SlotBin {
     // the range's first tile, rrow[r] its first row.
     int32_t lanes;         // 1: per-lane streams (then mask = 1: nlive per row, dead lanes a suffix)
     int32_t ntiles;
+    int32_t deep;          // lanes: 1 = keys two steps ahead, gathers one step ahead of their fold
     const int32_t *trow;   // ntiles + 1: first row of each tile
     const int32_t *tseg;   // ntiles + 1: first segment of each tile
     const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)

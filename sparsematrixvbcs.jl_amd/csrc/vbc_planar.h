@@ -275,118 +275,47 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__re
 
 // Per-lane compacted streams (SlotBin::lanes).  The masked chunk layout above steps every chunk
 // through its longest stripe's rows: on an irregular operator (FE-3D: 1..12 runs per stripe) a third
-// of its lane-rows are dead.  Here a range is a run of *tiles*; a tile's consecutive stripes
-// [s0, s0 + ns) are dealt to the 64 lanes as contiguous sub-blocks balanced by rows, and lane l walks
-// its sub-block's stored rows back to back -- stripe after stripe, each in stored (reference) row
-// order (multiply_1DVBC.jl:101-104) -- so a tile holds ~7 % dead lane-rows instead of ~38 %.  Lanes
-// are ordered by decreasing stream length: the live lanes of every step are a prefix (nlive, dead
-// lanes read lane 0's lines, as MASK).  A run whose key has LAST closes the lane's current stripe:
-// the lane stores its W_ sums into the tile's LDS buffer at that stripe's slot and moves to the next
-// (an empty stripe is one zero run with PAD | LAST).  Every slot of the tile is written exactly once,
-// so at the tile end the wave writes the tile's ns * W_ outputs as one contiguous run of 16-B stores
-// (y[j : j+w-1], :114-116, α and β applied there).  Tile switches are wave-uniform and happen inside
-// the pipeline (rows of consecutive tiles are contiguous), so the loads never drain at a tile edge.
+// of its lane-rows are dead.  Here a range (one wave) is a *tile* of consecutive stripes
+// [s0, s0 + ns), dealt to the 64 lanes as contiguous sub-blocks balanced by rows; lane l walks its
+// sub-block's stored rows back to back -- stripe after stripe, each in stored (reference) row order
+// (multiply_1DVBC.jl:101-104) -- so a tile holds ~5 % dead lane-rows instead of ~38 %.  Lanes are
+// ordered by decreasing stream length: the live lanes of every step are a prefix (nlive; dead lanes
+// read lane 0's lines, as MASK).  A run whose key has LAST closes the lane's current stripe: the lane
+// stores its W_ sums into the wave's LDS tile buffer at that stripe's slot and moves to its next
+// stripe (an empty stripe is one zero run with PAD | LAST).  Every slot of the tile is written exactly
+// once; after the loop the wave writes the tile's ns * W_ outputs y[j : j+w-1] (:114-116) as one
+// contiguous run of 16-B stores, α and β applied there.  (Writing the 24-B outputs straight from the
+// lanes measured 213 -> 275 us on FE-3D: partial-line writes; no global store sits inside the loop,
+// so the compiler's vmcnt accounting stays exact.)  DEEP: keys two steps ahead, the gathers one step
+// ahead of their fold.
 #ifndef VBC_LANE_TILE_BYTES
 #define VBC_LANE_TILE_BYTES 8192
 #endif
-constexpr int kLaneTileBytes = VBC_LANE_TILE_BYTES;  // LDS tile buffer per wave (8 KB + 1 KB of lane starts:
-                                                     // 4 workgroups of 4 waves per CU, the VGPR limit too)
-constexpr int kLaneMaxTiles = 8;                     // tiles per range (their lane starts are staged in LDS)
-template <typename T, int W_>
-__host__ __device__ constexpr int lanes_tile_stripes() { return (kLaneTileBytes / (W_ * (int)sizeof(T))) & ~3; }
+constexpr int kLaneTileBytes = VBC_LANE_TILE_BYTES;  // LDS tile buffer per wave (4 workgroups of 4 waves per
+                                                     // CU, as the VGPR limit)
 
-template <typename T, int W_, int U, int RUN>
+template <typename T, int W_, int U, int RUN, bool DEEP, bool RD>
 __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int lane, const T *__restrict__ x,
-                                                 T *__restrict__ y, T alpha, T beta, bool rd, T *buf, int16_t *lsegs)
+                                                 T *__restrict__ y, T alpha, T beta, T *buf)
 {
     typedef __attribute__((address_space(4))) const uint32_t *cptr;
-    typedef __attribute__((address_space(4))) const int32_t *ciptr;
-    const ciptr trow = (ciptr)b.trow, tseg = (ciptr)b.tseg, rch = (ciptr)b.rchunk;
-    int t = rch[r];
-    const int t1 = rch[r + 1];
-    if (t >= t1) return;
-    const int R0 = trow[t], R1 = trow[t1];
-    // the lane starts of the range's tiles, staged in LDS (read at each tile switch without waiting
-    // on the vector loads in flight)
-    for (int i = lane; i < (t1 - t) * 64; i += 64) lsegs[i] = G(b.lseg)[(size_t)t * 64 + i];
-    const int tfirst = t;
-    int tend = trow[t + 1], s0 = tseg[t], ns = tseg[t + 1] - s0;
+    const int R0 = G(b.rrow)[r], R1 = G(b.rrow)[r + 1];
+    if (R0 >= R1) return;
+    const int s0 = G(b.tseg)[r];
+    const int ns = G(b.tseg)[r + 1] - s0;
+    int cur = (int)G(b.lseg)[(size_t)r * 64 + lane];  // the lane's current stripe, relative to s0
     const gptr<const T> val = G(static_cast<const T *>(b.val));
     const gptr<const uint32_t> key = G(b.key);
     const gptr<const T> xg = G(x);
     const cptr nlive = (cptr)b.nlive;
     constexpr int NR = U / RUN;
     static_assert(NR * RUN == U, "a step holds whole runs");
-    __builtin_amdgcn_wave_barrier();
-    int cur = lsegs[lane];
-    auto load = [&](int R, uint32_t (&kk)[NR], int (&nl)[NR], T (&v)[U][W_]) {
-#pragma unroll
-        for (int j = 0; j < NR; j++) {
-            const int Rk = min(R + j * RUN, R1 - RUN);  // the run's first row (clamped: rows past the range)
-            nl[j] = (int)nlive[Rk];
-            const int ln = lane < nl[j] ? lane : 0;
-            kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + ln);
-#pragma unroll
-            for (int d = 0; d < RUN; d++) {
-                const int Rc = min(R + j * RUN + d, R1 - 1);
-                ld_row<T, W_, 0>(val + (size_t)Rc * 64 * W_, ln, v[j * RUN + d]);
-            }
-        }
-    };
-    auto gather = [&](const uint32_t (&kk)[NR], T (&xv)[NR][RUN]) {
-#pragma unroll
-        for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & kSlotIdx), xv[j]);
-    };
-    // the tile's outputs -> y (one contiguous run), then the next tile of the range
-    auto tile_done = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        T *dst = y + b.out_base + (int64_t)s0 * W_;
-        const int n = ns * W_;
-        constexpr int VE = 16 / (int)sizeof(T);
-        typedef T vt __attribute__((ext_vector_type(VE)));
-        if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-            for (int i = lane * VE; i < n; i += 64 * VE) {
-                if (i + VE <= n) {
-                    vt q = *reinterpret_cast<const vt *>(buf + i) * alpha;
-                    if (rd) {
-                        const vt yo = *(gptr<const vt>)(dst + i);
-#pragma unroll
-                        for (int e = 0; e < VE; e++) q[e] = fmadd(beta, yo[e], q[e]);
-                    }
-                    *(gptr<vt>)(dst + i) = q;
-                } else {
-                    for (int e = i; e < n; e++) {
-                        T q = alpha * buf[e];
-                        if (rd) q = fmadd(beta, dst[e], q);
-                        *(gptr<T>)(dst + e) = q;
-                    }
-                }
-            }
-        } else {
-            for (int e = lane; e < n; e += 64) {
-                T q = alpha * buf[e];
-                if (rd) q = fmadd(beta, dst[e], q);
-                *(gptr<T>)(dst + e) = q;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        t++;
-        if (t < t1) {
-            s0 = tseg[t];
-            ns = tseg[t + 1] - s0;
-            tend = trow[t + 1];
-            cur = lsegs[(t - tfirst) * 64 + lane];
-        }
-    };
     T acc[W_];
 #pragma unroll
     for (int e = 0; e < W_; e++) acc[e] = T(0);
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
+    // fold a step; kk: the runs' keys (or just their PAD / LAST bits)
     auto compute = [&](int R, const uint32_t (&kk)[NR], const int (&nl)[NR], const T (&v)[U][W_],
                        const T (&xv)[NR][RUN]) {
 #pragma unroll
@@ -410,39 +339,127 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
 #pragma unroll
             for (int e = 0; e < W_; e++) acc[e] = fl ? T(0) : acc[e];
             cur += fl ? 1 : 0;
-            if (R + j * RUN + RUN == tend) tile_done();
         }
     };
-    uint32_t kA[NR], kB[NR];
-    int nA[NR], nB[NR];
-    T vA[U][W_], vB[U][W_], xv[NR][RUN];
-    load(R0, kA, nA, vA);
-    __builtin_amdgcn_s_waitcnt(0);
-    for (int R = R0; R < R1; R += 2 * U) {
-        gather(kA, xv);
-        load(R + U, kB, nB, vB);
-        compute(R, kA, nA, vA, xv);
-        gather(kB, xv);
-        load(R + 2 * U, kA, nA, vA);
-        compute(R + U, kB, nB, vB, xv);
+    auto load_keys = [&](int R, uint32_t (&kk)[NR], int (&nl)[NR]) {
+#pragma unroll
+        for (int j = 0; j < NR; j++) {
+            const int Rk = min(R + j * RUN, R1 - RUN);  // the run's first row (clamped: rows past the range)
+            nl[j] = (int)nlive[Rk];
+            kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + (lane < nl[j] ? lane : 0));
+        }
+    };
+    auto load_vals = [&](int R, const int (&nl)[NR], T (&v)[U][W_]) {
+#pragma unroll
+        for (int j = 0; j < NR; j++) {
+            const int ln = lane < nl[j] ? lane : 0;
+#pragma unroll
+            for (int d = 0; d < RUN; d++)
+                ld_row<T, W_, 0>(val + (size_t)min(R + j * RUN + d, R1 - 1) * 64 * W_, ln, v[j * RUN + d]);
+        }
+    };
+    auto gather = [&](const uint32_t (&kk)[NR], T (&xv)[NR][RUN]) {
+#pragma unroll
+        for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & kSlotIdx), xv[j]);
+    };
+    if constexpr (!DEEP) {
+        uint32_t kA[NR], kB[NR];
+        int nA[NR], nB[NR];
+        T vA[U][W_], vB[U][W_], xv[NR][RUN];
+        load_keys(R0, kA, nA);
+        load_vals(R0, nA, vA);
+        __builtin_amdgcn_s_waitcnt(0);
+        for (int R = R0; R < R1; R += 2 * U) {
+            gather(kA, xv);
+            load_keys(R + U, kB, nB);
+            load_vals(R + U, nB, vB);
+            compute(R, kA, nA, vA, xv);
+            gather(kB, xv);
+            load_keys(R + 2 * U, kA, nA);
+            load_vals(R + 2 * U, nA, vA);
+            compute(R + U, kB, nB, vB, xv);
+        }
+    } else {
+        // a step's key buffer is free once its gathers are issued (PAD / LAST move to a flags word), so
+        // two key buffers rotate with the two value and gather buffers
+        auto issue = [&](const uint32_t (&kk)[NR], T (&xv)[NR][RUN], uint32_t (&fl)[NR]) {
+            gather(kk, xv);
+#pragma unroll
+            for (int j = 0; j < NR; j++) {
+                fl[j] = kk[j] & (kPad | kLast);
+                asm volatile("" : "+v"(fl[j]));  // materialise now: kk's register is reloaded next step
+            }
+        };
+        uint32_t kA[NR], kB[NR], fA[NR], fB[NR];
+        int nA[NR], nB[NR];
+        T vA[U][W_], vB[U][W_], xA[NR][RUN], xB[NR][RUN];
+        load_keys(R0, kA, nA);
+        load_keys(R0 + U, kB, nB);
+        load_vals(R0, nA, vA);
+        issue(kA, xA, fA);
+        for (int R = R0; R < R1; R += 2 * U) {
+            int nC[NR], nD[NR];
+            load_keys(R + 2 * U, kA, nC);  // step R: keys(R + 2U); gathers and values of R + U; fold R
+            issue(kB, xB, fB);
+            load_vals(R + U, nB, vB);
+            compute(R, fA, nA, vA, xA);
+#pragma unroll
+            for (int j = 0; j < NR; j++) nA[j] = nC[j];
+            load_keys(R + 3 * U, kB, nD);  // step R + U
+            issue(kA, xA, fA);
+            load_vals(R + 2 * U, nA, vA);
+            compute(R + U, fB, nB, vB, xB);
+#pragma unroll
+            for (int j = 0; j < NR; j++) nB[j] = nD[j];
+        }
+    }
+    // the tile's outputs -> y: one contiguous run (every slot was written once by its lane)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    T *dst = y + b.out_base + (int64_t)s0 * W_;
+    const int n = ns * W_;
+    constexpr int VE = 16 / (int)sizeof(T);
+    typedef T vt __attribute__((ext_vector_type(VE)));
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (int i = lane * VE; i < n; i += 64 * VE) {
+            if (i + VE <= n) {
+                vt q = *reinterpret_cast<const vt *>(buf + i) * alpha;
+                if constexpr (RD) {
+                    const vt yo = *(gptr<const vt>)(dst + i);
+#pragma unroll
+                    for (int e = 0; e < VE; e++) q[e] = fmadd(beta, yo[e], q[e]);
+                }
+                *(gptr<vt>)(dst + i) = q;
+            } else {
+                for (int e = i; e < n; e++) {
+                    T q = alpha * buf[e];
+                    if constexpr (RD) q = fmadd(beta, G(dst)[e], q);
+                    G(dst)[e] = q;
+                }
+            }
+        }
+    } else {
+        for (int e = lane; e < n; e += 64) {
+            T q = alpha * buf[e];
+            if constexpr (RD) q = fmadd(beta, G(dst)[e], q);
+            G(dst)[e] = q;
+        }
     }
 }
 
-template <typename T, int W_, int RUN>
+template <typename T, int W_, int RUN, bool DEEP, bool RD>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar_lanes(const SlotBin *__restrict__ bp,
                                                                    const T *__restrict__ x, T *__restrict__ y,
-                                                                   T alpha, T beta, int rd_i)
+                                                                   T alpha, T beta)
 {
     const SlotBin b = *bp;
     const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
-    const int lane = threadIdx.x & 63;
-    constexpr int TBE = kLaneTileBytes / (int)sizeof(T);
-    __shared__ __attribute__((aligned(16))) T tilebuf[kWavesPerBlock][TBE];
-    __shared__ int16_t lsegs[kWavesPerBlock][kLaneMaxTiles * 64];
-    run_planar_lanes<T, W_, planar_step<T, W_, RUN>(), RUN>(b, rg, lane, x, y, alpha, beta, rd_i != 0,
-                                                            tilebuf[threadIdx.x >> 6], lsegs[threadIdx.x >> 6]);
+    __shared__ __attribute__((aligned(16))) T tilebuf[kWavesPerBlock][kLaneTileBytes / sizeof(T)];
+    run_planar_lanes<T, W_, planar_step<T, W_, RUN>(), RUN, DEEP, RD>(b, rg, threadIdx.x & 63, x, y, alpha, beta,
+                                                                      tilebuf[threadIdx.x >> 6]);
 }
 
 // Planar forward product with row runs (SlotBin kind 1, run = R): mul!(y, B, x) for node-blocked rows.

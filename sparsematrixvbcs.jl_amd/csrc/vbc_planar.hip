@@ -139,23 +139,31 @@ static int launch_fwd(const SlotBin &hb, const SlotBin *d_b, bool faste, bool st
 }
 
 // per-lane compacted streams (vbc_planar.h run_planar_lanes): w in 3..8, runs of 1..3
+template <typename T, int W_, int RUN>
+static void launch_lanes_w(const SlotBin &hb, const SlotBin *d_b, const T *xs, T *ys, double alpha, double beta,
+                           bool rd, hipStream_t s)
+{
+    const dim3 grid((hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock), blk(kBlockThreads);
+    if (rd) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, true>), grid, blk, 0, s, d_b, xs, ys, (T)alpha, (T)beta);
+    else if (hb.deep) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, true, false>), grid, blk, 0, s, d_b, xs, ys, (T)alpha, (T)beta);
+    else hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false>), grid, blk, 0, s, d_b, xs, ys, (T)alpha, (T)beta);
+}
+
 template <typename T, int RUN>
 static int launch_lanes_r(const SlotBin &hb, const SlotBin *d_b, const void *x, void *y, double alpha, double beta,
                           bool rd, hipStream_t s)
 {
-    const int grid = (hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
-#define VBC_LANES(W)                                                                                      \
-    case W:                                                                                               \
-        hipLaunchKernelGGL((spmv_planar_lanes<T, W, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, \
-                           (T)alpha, (T)beta, (int)rd);                                                   \
-        break;
     switch (hb.wkey) {
-        VBC_LANES(3) VBC_LANES(4) VBC_LANES(5) VBC_LANES(6) VBC_LANES(7) VBC_LANES(8)
+    case 3: launch_lanes_w<T, 3, RUN>(hb, d_b, xs, ys, alpha, beta, rd, s); break;
+    case 4: launch_lanes_w<T, 4, RUN>(hb, d_b, xs, ys, alpha, beta, rd, s); break;
+    case 5: launch_lanes_w<T, 5, RUN>(hb, d_b, xs, ys, alpha, beta, rd, s); break;
+    case 6: launch_lanes_w<T, 6, RUN>(hb, d_b, xs, ys, alpha, beta, rd, s); break;
+    case 7: launch_lanes_w<T, 7, RUN>(hb, d_b, xs, ys, alpha, beta, rd, s); break;
+    case 8: launch_lanes_w<T, 8, RUN>(hb, d_b, xs, ys, alpha, beta, rd, s); break;
     default: return (int)hipErrorInvalidValue;
     }
-#undef VBC_LANES
     return (int)hipGetLastError();
 }
 
@@ -174,8 +182,8 @@ static int launch_lanes(const SlotBin &hb, const SlotBin *d_b, const void *x, vo
 int occupancy_lanes(int esz)
 {
     int occ = 0;
-    if (esz == 8) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar_lanes<double, 3, 3>, kBlockThreads, 0);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar_lanes<float, 3, 3>, kBlockThreads, 0);
+    if (esz == 8) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar_lanes<double, 3, 3, false, false>, kBlockThreads, 0);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, spmv_planar_lanes<float, 3, 3, false, false>, kBlockThreads, 0);
     return occ;
 }
 
