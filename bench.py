@@ -45,6 +45,7 @@ WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
              "fe": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2 (SuiteSparse-like mesh operator)",
              "fe3d": "FE-3D-stiffness-dof3-1e7x1e7-1e8nnz-w3 (irregular: random 18-neighbour subsets)",
              "c5": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS (costs.jl:200-220 generator)",
+             "c5-fwd": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS forward Y = B*X (costs.jl:200-220 generator)",
              "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
              "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)",
              "ldoor-csc": "C4 TrSpMV!(y, A, x) on the GHS_psdef/ldoor stand-in (CSC, 952203^2, 42.5M nnz)"}
@@ -83,7 +84,7 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
     if workload == "fe3d":
         n = 3 * int(round(3333333 * scale))
         return V.synthetic.fe_stiffness_3d_1dvbc(n, int(round(1e8 * scale)), 3, dtype=dtype, seed=seed)
-    if workload == "c5":
+    if workload in ("c5", "c5-fwd"):
         return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
     if workload in ("ldoor", "ct20stif", "ldoor-csc"):
         name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ldoor-csc": "GHS_psdef/ldoor"}[workload]
@@ -164,9 +165,10 @@ def timed_products(step, steps, device, stream, world, graph=True):
     return elapsed, ev0.elapsed_time(ev1) / steps, g is not None
 
 
-def parity(B, x_host, y_dev, k=1, cols=(0,)):
+def parity(B, x_host, y_dev, k=1, cols=(0,), trans=True):
     """Normwise relative error of the GPU y against the CPU oracle on the same full-size input
-    (oracle/vbc_oracle.c: multiply_1DVBC.jl:90-180 / multiply_VBC.jl:93-192 restated)."""
+    (oracle/vbc_oracle.c: multiply_1DVBC.jl:90-180 / multiply_VBC.jl:93-192 restated; trans=False:
+    the forward products multiply_1DVBC.jl:13-83 / multiply_VBC.jl:7-87)."""
     from oracle import oracle as O
     from oracle import simd as S
     th = S.host_threads()
@@ -184,13 +186,14 @@ def parity(B, x_host, y_dev, k=1, cols=(0,)):
     else:
         R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
     yg = y_dev.cpu().numpy()
-    X = x_host.reshape(B.m, -1)
-    Yg = yg.reshape(B.n, -1)
+    nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+    X = x_host.reshape(nx, -1)
+    Yg = yg.reshape(ny, -1)
     num = den = 0.0
     bitwise = True
     t0 = time.perf_counter()
     for c in (cols if k > 1 else (0,)):
-        ref = O.mul(R, np.ascontiguousarray(X[:, c]), np.zeros(B.n, B.val.dtype), trans=True, nthreads=th)
+        ref = O.mul(R, np.ascontiguousarray(X[:, c]), np.zeros(ny, B.val.dtype), trans=trans, nthreads=th)
         g = Yg[:, c]
         num += float(np.sum((g.astype(np.float64) - ref) ** 2))
         den += float(np.sum(ref.astype(np.float64) ** 2))
@@ -198,7 +201,8 @@ def parity(B, x_host, y_dev, k=1, cols=(0,)):
     err = (num ** 0.5) / max(den ** 0.5, 1e-300)
     tol = PARITY_TOL[np.dtype(B.val.dtype)]
     return {"rel_err": float(f"{err:.3e}"), "tol": tol, "pass": bool(err <= tol), "bitwise_equal": bitwise,
-            "oracle": "oracle/vbc_oracle.c orc_*_mul_t (multiply_1DVBC.jl:90-180 / multiply_VBC.jl:93-192)",
+            "oracle": ("oracle/vbc_oracle.c orc_*_mul_t (multiply_1DVBC.jl:90-180 / multiply_VBC.jl:93-192)" if trans
+                       else "oracle/vbc_oracle.c orc_*_mul (multiply_1DVBC.jl:13-83 / multiply_VBC.jl:7-87)"),
             "columns": list(cols) if k > 1 else None, "oracle_s": round(time.perf_counter() - t0, 2)}
 
 
@@ -248,20 +252,22 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     B = build_matrix(workload, dtype, args.scale)
     csc = not hasattr(B, "ofs")
     rng = np.random.default_rng(0xC0FFEE)
-    k = args.nrhs if workload == "c5" else 1
-    x_host = rng.uniform(-1, 1, (B.m, k) if k > 1 else B.m).astype(dtype)
+    k = args.nrhs if workload in ("c5", "c5-fwd") else 1
+    trans = workload != "c5-fwd"
+    nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+    x_host = rng.uniform(-1, 1, (nx, k) if k > 1 else nx).astype(dtype)
     x = torch.from_numpy(x_host).to(device)  # k > 1: row-major X (right-hand sides interleaved)
-    y = torch.empty((B.n, k) if k > 1 else B.n, dtype=x.dtype, device=device)
-    Bt = B.T
+    y = torch.empty((ny, k) if k > 1 else ny, dtype=x.dtype, device=device)
+    Bop = B.T if trans else B
 
     def step():
         if csc:
             V.TrSpMV_(y, B, x)
         else:
-            V.mul_(y, Bt, x)
+            V.mul_(y, Bop, x)
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
-        B.handle(local, True, multi=k > 1)  # build the HBM layout outside the timed region
+        B.handle(local, trans, multi=k > 1)  # build the HBM layout outside the timed region
         t_build = time.perf_counter() - t_build
         for _ in range(args.warmup):
             step()
@@ -276,7 +282,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     ms_per_step = elapsed / steps * 1e3
     achieved = bytes_roof / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload, "f64" if dtype == np.float64 else "f32")
-    layout_bytes = int(B.info(local, True, multi=k > 1)["device_bytes"])
+    layout_bytes = int(B.info(local, trans, multi=k > 1)["device_bytes"])
     out = {
         # TrSpMV! on a CSC: priced on the bytes its blocked layout moves, so `value` is a bandwidth
         # (the CSC byte formula divided by the same time is reported apart as `csc_equivalent_GBs`)
@@ -294,7 +300,9 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
             "op": ("TrSpMV!(y, A, x) -- CSC transposed product (TrSpMV.jl:1-20)" if csc else
                    "mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if k == 1 else
                    f"Y = B'X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:89-192 per column), "
-                   "matrix-core panel kernel"),
+                   "matrix-core panel kernel" if trans else
+                   f"Y = B*X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:3-87 per column), "
+                   "matrix-core panel kernel on the panel layout of B' (the matrix read once)"),
             "m": B.m, "n": B.n, "stripes": B.n if csc else len(B.Phi),
             "row_blocks": nnz if csc else int(B.pos[-1] - 1), "nnz": nnz, "W": 1 if csc else B.W,
             "index_bytes": 4, "nrhs": k, "launch": "hipGraph of K products" if graphed else "eager",
@@ -309,7 +317,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
         out["roofline"]["bytes_csc_formula"] = bytes_launch
         out["csc_equivalent_GBs"] = round(bytes_launch * steps / elapsed / 1e9, 2)
     if with_parity:
-        out["parity"] = parity(B, x_host, y, k, cols=tuple(range(k)) if k > 1 else (0,))
+        out["parity"] = parity(B, x_host, y, k, cols=tuple(range(k)) if k > 1 else (0,), trans=trans)
     if with_cpu:
         out["cpu_baseline"] = cpu_baseline(B, x_host, esz)
     B.release()
@@ -510,8 +518,8 @@ def main():
             out["rel_err"] = p["parity"]["rel_err"]
         if not args.no_secondary:
             sec = {}
-            for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("ct20stif", np.float64),
-                           ("ldoor", np.float64), ("ldoor-csc", np.float32)):
+            for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("c5-fwd", np.float32),
+                           ("ct20stif", np.float64), ("ldoor", np.float64), ("ldoor-csc", np.float32)):
                 if wl == args.workload:
                     continue
                 s = measure(args, wl, dt, device, local, with_cpu=False, with_parity=not args.no_parity)

@@ -65,6 +65,12 @@ typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
                                       Y = α·B'X + β·Y on matrix cores (vbc_mul_mat, trans = 1,
                                       any operand layout; stripes wider than 16 are cut into
                                       16-column pieces).  Independent of the SpMV layouts. */
+#define VBC_CREATE_MULTI_FORWARD 0x10u /* build the panel layout of the multi-RHS FORWARD product
+                                      Y = α·B·X + β·Y on matrix cores (vbc_mul_mat, trans = 0): the
+                                      panel layout of Bᵀ -- output row groups (Π's block rows of a
+                                      SparseMatrixVBC; runs of rows with identical stripe lists of a
+                                      1DVBC, <= 16) as stripes, every tile column a stored row -- so the
+                                      matrix is read once for all right-hand sides. */
 #define VBC_CREATE_SERIAL 0x8u     /* keep the reference's serial per-stripe summation order in every
                                       B'x layout (multiply_1DVBC.jl:101-104): no split planar product
                                       (vbc_info.planar_split stays 1), so every output is bit-identical
@@ -263,7 +269,8 @@ typedef struct vbc_info {
     int64_t device_bytes;   /* HBM held by the handle */
     int64_t bytes_t;        /* HBM bytes one transposed product moves in this layout */
     int64_t bytes_f;        /* same for the forward product */
-    int32_t bins_m;         /* width buckets of the multi-RHS panel layout (0 = absent) */
+    int32_t bins_m;         /* width buckets of the multi-RHS panel layout (0 = absent; a handle built with
+                               VBC_CREATE_MULTI_FORWARD only: those of its Bᵀ layout, bytes_m likewise) */
     int32_t slot_bins;      /* buckets laid out slotted (vbc_slots.h / vbc_planar.h), both directions */
     int64_t bytes_m;        /* matrix bytes (keys + values, panel-padded) one panel pass streams */
     int32_t sweep_bins;     /* B'x buckets laid out row-swept (vbc_sweep.hip) */

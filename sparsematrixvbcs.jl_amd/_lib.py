@@ -17,6 +17,7 @@ VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR, VBC_UN
 VBC_F64, VBC_F32, VBC_I64, VBC_I32, VBC_BOOL = range(5)
 VBC_MEM_DEVICE, VBC_MEM_HOST = 0, 1
 VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD, VBC_CREATE_MULTI, VBC_CREATE_SERIAL = 0x1, 0x2, 0x4, 0x8
+VBC_CREATE_MULTI_FORWARD = 0x10
 VBC_VERSION_MAJOR = 3  # include/vbc.h VBC_VERSION / 10000: the vbc_info layout below is that version's
 VBC_INFO_SIZE = 152
 VBC_MUL_REFERENCE_QUIRKS = 0x1

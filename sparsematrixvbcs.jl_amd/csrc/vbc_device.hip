@@ -1447,6 +1447,108 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     return VBC_OK;
 }
 
+// Forward panel layout (VBC_CREATE_MULTI_FORWARD): Y = B·X is the transposed product of C = Bᵀ, so
+// the transposed panel layout of C serves it.  C's stripes are B's output row groups g (rows
+// [a_g, a_g + u_g), u_g <= 16): Π's block rows for a SparseMatrixVBC, else runs of consecutive rows
+// whose stripe lists are identical (a node's dof rows), else single rows.  Every stripe l of B that
+// stores rows of group g contributes w_l stored rows of C (its columns c, ascending), each holding the
+// u_g values B[a_g .. a_g+u_g-1, col0_l + c] (0 for a row of the group the stripe does not store) and
+// gathering X row col0_l + c.  Groups in row order, their stripes in stripe order (the reference's
+// forward loop, multiply_VBC.jl:68-77).
+static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
+                               std::vector<PendingPanel> &pps, PanelLaunch &L)
+{
+    const int esz = h->esz;
+    const int64_t m = s.m;
+    // row groups
+    std::vector<int64_t> a;
+    if (!s.grp.empty()) {
+        for (size_t k = 0; k + 1 < s.grp.size(); k++)
+            for (int64_t i = s.grp[k]; i < s.grp[k + 1]; i += 16) a.push_back(i);  // blocks taller than 16: pieces
+    } else {
+        // the stripes storing each row (rows ascend inside a stripe, so each list comes out sorted)
+        std::vector<int64_t> cnt(m + 1, 0);
+        for (int64_t q = 0; q < (int64_t)s.rows.size(); q++) cnt[s.rows[q] + 1]++;
+        for (int64_t i = 0; i < m; i++) cnt[i + 1] += cnt[i];
+        std::vector<int64_t> lst(s.rows.size()), fillp(cnt.begin(), cnt.end() - 1);
+        for (int64_t l = 0; l < s.L; l++)
+            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) lst[fillp[s.rows[q]]++] = l;
+        auto same = [&](int64_t i, int64_t j) {
+            return cnt[i + 1] - cnt[i] == cnt[j + 1] - cnt[j] &&
+                   std::equal(lst.begin() + cnt[i], lst.begin() + cnt[i + 1], lst.begin() + cnt[j]);
+        };
+        for (int64_t i = 0; i < m;) {
+            int64_t e = i + 1;
+            while (e < m && e - i < 16 && cnt[i + 1] > cnt[i] && same(i, e)) e++;
+            a.push_back(i);
+            i = e;
+        }
+    }
+    a.push_back(m);
+    const int64_t ng = (int64_t)a.size() - 1;
+    std::vector<int64_t> gof(m);
+    for (int64_t g = 0; g < ng; g++)
+        for (int64_t i = a[g]; i < a[g + 1]; i++) gof[i] = g;
+    // (group, stripe) blocks: stored rows of B grouped
+    struct Blk {
+        int64_t g, l, q0;  // q0: first stored row of the stripe inside the group
+    };
+    std::vector<Blk> blks;
+    for (int64_t l = 0; l < s.L; l++) {
+        int64_t prev = -1;
+        for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+            const int64_t g = gof[s.rows[q]];
+            if (g != prev) blks.push_back({g, l, q});
+            prev = g;
+        }
+    }
+    std::stable_sort(blks.begin(), blks.end(), [](const Blk &x, const Blk &y) { return x.g < y.g; });
+    Stripes c;
+    c.m = s.n;  // C = Bᵀ: its x is B's x (length n), its y is B's y (length m)
+    c.n = m;
+    c.L = ng;
+    c.col0.resize(ng);
+    c.w.resize(ng);
+    c.rbeg.assign(ng + 1, 0);
+    c.voff.resize(ng);
+    for (int64_t g = 0; g < ng; g++) {
+        c.col0[g] = a[g];
+        c.w[g] = (int32_t)(a[g + 1] - a[g]);
+    }
+    for (const Blk &b : blks) c.rbeg[b.g + 1] += s.w[b.l];
+    for (int64_t g = 0; g < ng; g++) c.rbeg[g + 1] += c.rbeg[g];
+    const int64_t rows = c.rbeg[ng];
+    if (rows >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "matrix too large for the forward panel layout");
+    c.rows.resize(rows);
+    int64_t nv = 0;
+    for (int64_t g = 0; g < ng; g++) {
+        c.voff[g] = nv;
+        nv += (c.rbeg[g + 1] - c.rbeg[g]) * c.w[g];
+    }
+    std::vector<char> cv((size_t)std::max<int64_t>(nv, 1) * esz, 0);
+    std::vector<int64_t> at(c.rbeg.begin(), c.rbeg.end() - 1);  // next stored row of each group
+    for (const Blk &b : blks) {
+        const int64_t l = b.l, wl = s.w[l], u = c.w[b.g];
+        for (int64_t cc = 0; cc < wl; cc++) {
+            const int64_t row = at[b.g]++;
+            c.rows[row] = (int32_t)(s.col0[l] + cc);
+            char *dst = cv.data() + (c.voff[b.g] + (row - c.rbeg[b.g]) * u) * esz;
+            for (int64_t q = b.q0; q < s.rbeg[l + 1] && gof[s.rows[q]] == b.g; q++)
+                std::memcpy(dst + (s.rows[q] - a[b.g]) * esz, val + (s.voff[l] + (q - s.rbeg[l]) * wl + cc) * esz,
+                            (size_t)esz);
+        }
+    }
+    int32_t widest = 0;
+    for (int64_t g = 0; g < ng; g++) widest = std::max(widest, c.w[g]);
+    h->mf_group = widest;
+    const int64_t bytes0 = h->bytes_m;
+    std::vector<int32_t> fill;
+    const int st = build_panel(h, c, cv.data(), ar, pps, L, fill);
+    h->bytes_mf = h->bytes_m - bytes0;
+    h->bytes_m = bytes0;
+    return st;
+}
+
 static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, PanelLaunch &L)
 {
     L.bins.clear();
@@ -1539,6 +1641,7 @@ static void release(vbc_handle *h)
     if (h->lt.d_wbins) (void)hipFree(h->lt.d_wbins);
     if (h->lt.d_pbins) (void)hipFree(h->lt.d_pbins);
     if (h->lm.d_bins) (void)hipFree(h->lm.d_bins);
+    if (h->lmf.d_bins) (void)hipFree(h->lmf.d_bins);
     for (auto &l : h->lf) {
         if (l.d_bins) (void)hipFree(l.d_bins);
         if (l.d_sbins) (void)hipFree(l.d_sbins);
@@ -1610,7 +1713,8 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     int ndev = 0;
     VBC_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(VBC_INVALID_ARG, "device ordinal out of range");
-    if ((flags & (VBC_CREATE_TRANSPOSED | VBC_CREATE_FORWARD | VBC_CREATE_MULTI)) == 0) flags |= VBC_CREATE_TRANSPOSED;
+    if ((flags & (VBC_CREATE_TRANSPOSED | VBC_CREATE_FORWARD | VBC_CREATE_MULTI | VBC_CREATE_MULTI_FORWARD)) == 0)
+        flags |= VBC_CREATE_TRANSPOSED;
 
     vbc_handle *h = new vbc_handle();
     h->m = s.m;
@@ -1698,7 +1802,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         h->occ_p = 1;
     }
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
-    if (flags & VBC_CREATE_MULTI) {
+    if (flags & (VBC_CREATE_MULTI | VBC_CREATE_MULTI_FORWARD)) {
         const int om = occupancy_panel(h->esz);
         h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
         if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
@@ -1725,6 +1829,12 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
             h->lm.o_fill = ar.reserve(fill_m.size() * 4);
             std::memcpy(ar.at<int32_t>(h->lm.o_fill), fill_m.data(), fill_m.size() * 4);
         }
+    }
+    std::vector<PendingPanel> pmf;
+    if (st == VBC_OK && (flags & VBC_CREATE_MULTI_FORWARD)) {
+        st = build_forward_panel(h, s, v, ar, pmf, h->lmf);
+        h->has_mf = st == VBC_OK;
+        if (st == VBC_OK) h->lmf.o_fill = ar.reserve(4);
     }
     if (st == VBC_OK && (flags & VBC_CREATE_TRANSPOSED)) {
         st = build_transposed(h, s, v, ar, pt, st_t, sw_t, h->lt, fill_t);
@@ -1758,6 +1868,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     }
     if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt, sw_t))) { release(h); return st; }
     if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
+    if (h->has_mf && (st = finalize_panel(h, pmf, h->lmf))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)
         if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b], wf[b]))) { release(h); return st; }
     if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
@@ -1883,6 +1994,8 @@ int vbc2d_create(vbc_handle **out, int64_t m, int64_t n, int64_t U, int64_t W, i
         const int64_t k = idx[Q];
         for (int64_t i = pspl[k - 1] - 1; i < pspl[k] - 1; i++) s.rows[r++] = (int32_t)i;
     }
+    s.grp.resize(K + 1);
+    for (int64_t k = 0; k <= K; k++) s.grp[k] = pspl[k] - 1;
     return create_common(out, s, val, dtype, device, flags, ofs[L] - 1, K, q);
 }
 
@@ -1987,7 +2100,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->device_bytes = (int64_t)h->arena_bytes;
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
-    info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : 0;
+    info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : h->has_mf ? (int32_t)h->lmf.bins.size() : 0;
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)(l.sbins.size() + l.pbins.size()) : 0;  // + planar forward
     info->slot_bins = sl;
@@ -2013,7 +2126,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
                 info->fwd_run = std::max<int32_t>(info->fwd_run, b.run);
                 if (b.mask) info->planar_mask |= 2;
             }
-    info->bytes_m = h->bytes_m;
+    info->bytes_m = h->has_m ? h->bytes_m : h->bytes_mf;  // a forward-only multi handle: its Bᵀ panel layout
     return VBC_OK;
 }
 
@@ -2026,7 +2139,9 @@ static int check_mul(const vbc_handle *h, int trans, int64_t nx, int64_t ny, boo
     if (trans && !h->has_t && !(mat && h->has_m))
         return fail(VBC_INVALID_ARG, mat ? "handle built without VBC_CREATE_TRANSPOSED or VBC_CREATE_MULTI"
                                          : "handle built without VBC_CREATE_TRANSPOSED");
-    if (!trans && !h->has_f) return fail(VBC_INVALID_ARG, "handle built without VBC_CREATE_FORWARD");
+    if (!trans && !h->has_f && !(mat && h->has_mf))
+        return fail(VBC_INVALID_ARG, mat ? "handle built without VBC_CREATE_FORWARD or VBC_CREATE_MULTI_FORWARD"
+                                         : "handle built without VBC_CREATE_FORWARD");
     return VBC_OK;
 }
 
@@ -2144,10 +2259,10 @@ static int mul_mat_device(vbc_handle *h, int trans, int64_t nrhs, const char *dX
     bool fused = rowmajor && trans && nrhs > 0 && h->n > 0 && h->has_t && h->dtype != VBC_I64;
     for (const Bin &b : h->lt.bins) fused = fused && b.wkey != 0;  // runtime-width buckets: per column
     fused = fused && h->lt.sbins.empty() && h->lt.wbins.empty() && h->lt.pbins.empty();  // the fused vector kernel reads the merge layout only
-    if (trans && h->has_m && nrhs > 0 && h->n > 0) {  // matrix-core panel product (any layout)
+    if (trans ? (h->has_m && nrhs > 0 && h->n > 0) : (h->has_mf && nrhs > 0 && h->m > 0)) {  // matrix-core panels
         const int64_t sxr = rowmajor ? ldx : 1, sxc = rowmajor ? 1 : ldx;
         const int64_t syr = rowmajor ? ldy : 1, syc = rowmajor ? 1 : ldy;
-        return mulmat_panel_any(h, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
+        return mulmat_panel_any(h, trans, nrhs, dX, sxr, sxc, dY, syr, syc, alpha, beta, s);
     }
     if (fused) return mulmat_rowmajor(h, nrhs, dX, ldx, dY, ldy, alpha, beta, s);
     if (!rowmajor) {

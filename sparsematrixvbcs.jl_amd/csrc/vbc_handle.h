@@ -71,6 +71,7 @@ struct Stripes {
     std::vector<int64_t> rbeg;  // L+1 prefix into rows
     std::vector<int32_t> rows;  // 0-based x row of each stored w-wide row
     std::vector<int64_t> voff;  // element offset of the stripe's first value in the input val
+    std::vector<int64_t> grp;   // 2D input: Π's block-row starts (K + 1, 0-based); empty for 1D / CSC
 };
 
 }  // namespace vbc
@@ -83,6 +84,11 @@ struct vbc_handle {
     bool has_t = false, has_f = false, has_m = false;
     vbc::PanelLaunch lm;          // multi-RHS transposed product on matrix cores (VBC_CREATE_MULTI)
     int64_t bytes_m = 0;          // matrix bytes one panel product streams
+    vbc::PanelLaunch lmf;         // multi-RHS forward product on matrix cores (VBC_CREATE_MULTI_FORWARD): the
+                                  // panel layout of Bᵀ (output row groups as stripes, tile columns as rows)
+    bool has_mf = false;
+    int64_t bytes_mf = 0;         // matrix bytes one forward panel product streams
+    int32_t mf_group = 0;         // forward panel: widest output row group
     int target_ranges_m = 4096;
     int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
@@ -165,7 +171,7 @@ int mul_int(const vbc_handle *h, int trans, const void *x, void *y, double alpha
 int convert_gather(const void *src, int src_dtype, int64_t inc, void *dst, int dst_dtype, int64_t n, hipStream_t s);
 int convert_scatter(const void *src, int src_dtype, void *dst, int dst_dtype, int64_t inc, int64_t n, hipStream_t s);
 // vbc_panel_launch.hip
-int mulmat_panel_any(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
+int mulmat_panel_any(const vbc_handle *h, int trans, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
                      int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s);
 int occupancy_panel(int esz);
 

@@ -9,11 +9,14 @@ namespace vbc {
 
 // Multi-RHS transposed product on the panel layout (MFMA), X / Y addressed by (row, column) strides,
 // in chunks of <= 64 right-hand sides (four 16-column accumulators).
+// trans = 1: Y = αB'X + βY on the panel layout of B (lm); trans = 0: Y = αBX + βY on the panel layout
+// of Bᵀ (lmf, VBC_CREATE_MULTI_FORWARD) -- the same kernel with x and y extents exchanged.
 template <typename T>
-static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
-                        int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s)
+static int mulmat_panel(const vbc_handle *h, int trans, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc,
+                        char *Y, int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s)
 {
-    const PanelLaunch &L = h->lm;
+    const PanelLaunch &L = trans ? h->lm : h->lmf;
+    const int64_t xrows = trans ? h->m : h->n, yrows = trans ? h->n : h->m;
     const bool rd = beta != 0.0;
     for (int64_t c0 = 0; c0 < nrhs; c0 += 64) {
         const int nr = (int)std::min<int64_t>(64, nrhs - c0);
@@ -22,8 +25,8 @@ static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_
         if (L.total_ranges > 0) {
             const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
             // byte extents of X and Y as addressed by this chunk (rows 0..m-1 / 0..n-1, columns 0..nr-1)
-            const int64_t span = ((h->m - 1) * sxr + (int64_t)(nr - 1) * sxc + 1) * (int64_t)sizeof(T);
-            const int64_t yspan = ((h->n - 1) * syr + (int64_t)(nr - 1) * syc + 1) * (int64_t)sizeof(T);
+            const int64_t span = ((xrows - 1) * sxr + (int64_t)(nr - 1) * sxc + 1) * (int64_t)sizeof(T);
+            const int64_t yspan = ((yrows - 1) * syr + (int64_t)(nr - 1) * syc + 1) * (int64_t)sizeof(T);
             const int64_t lim = int64_t(1) << 31;
             const bool buf = span + 64 * sxc * (int64_t)sizeof(T) < lim && h->panel_val_bytes < lim && !h->panel_nobuf;
             bool affine = true;
@@ -57,11 +60,11 @@ static int mulmat_panel(const vbc_handle *h, int64_t nrhs, const char *X, int64_
     return VBC_OK;
 }
 
-int mulmat_panel_any(const vbc_handle *h, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
+int mulmat_panel_any(const vbc_handle *h, int trans, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
                      int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s)
 {
-    return h->dtype == VBC_F64 ? mulmat_panel<double>(h, nrhs, X, sxr, sxc, Y, syr, syc, alpha, beta, s)
-                               : mulmat_panel<float>(h, nrhs, X, sxr, sxc, Y, syr, syc, alpha, beta, s);
+    return h->dtype == VBC_F64 ? mulmat_panel<double>(h, trans, nrhs, X, sxr, sxc, Y, syr, syc, alpha, beta, s)
+                               : mulmat_panel<float>(h, trans, nrhs, X, sxr, sxc, Y, syr, syc, alpha, beta, s);
 }
 
 int occupancy_panel(int esz)

@@ -69,17 +69,21 @@ class _DeviceMatrix:
 
     def handle(self, device=0, trans=True, multi=False, compute=None):
         """libvbc handle for mul!(y, B', x) (trans), mul!(y, B, x), or -- multi=True -- the
-        matrix-core multi-RHS product Y = B'X (a separate panel layout, built on first use).
+        matrix-core multi-RHS product Y = B'X (trans) / Y = B·X (a separate panel layout of B / Bᵀ,
+        built on first use).
         `compute` = the vbc_dtype the product runs in (eltype(y)); default: the value eltype's own
         (floats) or exact Int64 (integers, Bool).  One handle per (device, layout, compute).
         Setting `B.serial = True` before the first product builds layouts that keep the reference's
         serial per-stripe summation order whatever the size (vbc.h VBC_CREATE_SERIAL)."""
-        flags = _L.VBC_CREATE_MULTI if multi else (_L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD)
+        if multi:  # matrix-core panels: of B for B'X, of Bᵀ for B·X
+            flags = _L.VBC_CREATE_MULTI if trans else _L.VBC_CREATE_MULTI_FORWARD
+        else:
+            flags = _L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD
         compute = _L.compute_code(self.val.dtype) if compute is None else int(compute)
         if compute == _L.VBC_I64 and self.val.dtype.kind == "f":
             raise _L.UnsupportedDtype("a floating-point matrix cannot run in an integer eltype (InexactError)")
-        if multi and compute == _L.VBC_I64:
-            flags = _L.VBC_CREATE_TRANSPOSED  # integer eltypes: one SpMV per column
+        if multi and compute == _L.VBC_I64:  # integer eltypes: one SpMV per column
+            flags = _L.VBC_CREATE_TRANSPOSED if trans else _L.VBC_CREATE_FORWARD
         if getattr(self, "serial", False) and not multi:
             flags |= _L.VBC_CREATE_SERIAL  # the reference's serial per-stripe order in every layout
         return self._handles.get((int(device), flags, compute),

@@ -128,9 +128,9 @@ MFMA_MIN_RHS = 2
 
 def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="auto"):
     """Multi-RHS Y = α·op(A)·X + β·Y (column-by-column semantics; the reference has no matrix
-    mul!).  engine="mfma" (default for B'X with >= MFMA_MIN_RHS columns): the matrix-core panel
-    product, row- or column-major operands; engine="vector": the SpMV layout (fused vector kernel for
-    row-major B'X, one SpMV per column otherwise)."""
+    mul!).  engine="mfma" (default with >= MFMA_MIN_RHS columns): the matrix-core panel product --
+    of B for B'X, of Bᵀ for B·X -- row- or column-major operands, the matrix read once; engine="vector":
+    the SpMV layout (fused vector kernel for row-major B'X, one SpMV per column otherwise)."""
     B, trans = _unwrap(A)
     mem, dev, stream = _mem_device_stream(X, Y, stream)
     cdt = _compute_for(Y, B)
@@ -151,9 +151,8 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="
     nrhs = X.shape[1]
     if engine not in ("auto", "mfma", "vector"):
         raise _L.ArgumentError(f"engine must be 'auto', 'mfma' or 'vector', got {engine!r}")
-    if engine == "mfma" and not trans:
-        raise _L.ArgumentError("the matrix-core engine computes B'X (pass an adjoint)")
-    mfma = trans and cdt != _L.VBC_I64 and (engine == "mfma" or (engine == "auto" and nrhs >= MFMA_MIN_RHS))
+    # matrix cores for B'X (panel layout of B) and B·X (panel layout of Bᵀ): the matrix is read once
+    mfma = cdt != _L.VBC_I64 and (engine == "mfma" or (engine == "auto" and nrhs >= MFMA_MIN_RHS))
     h = B.handle(dev, trans, multi=mfma, compute=cdt)
     flags = (_L.VBC_MUL_REFERENCE_QUIRKS if quirks else 0) | (_L.VBC_MAT_ROWMAJOR if lx == "R" else 0)
     _L.check(_L.lib().vbc_mul_mat_ex(h, int(trans), nrhs, _L.ptr(X), _L.dtype_code(X.dtype), max(ldx, 1), X.shape[0],

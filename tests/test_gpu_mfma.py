@@ -158,9 +158,13 @@ def test_mfma_quirks_and_errors():
     assert rel(Yd.cpu().numpy(), ref_cols(R, X, Y0, 1.0, 0.0)) <= TOL64
     with pytest.raises(V.DimensionMismatch):
         V.mul_(torch.zeros((B.n + 1, 8), dtype=torch.float64, device=DEV), B.T, as_dev(X, "R"), engine="mfma")
-    with pytest.raises(V.ArgumentError):
-        V.mul_(torch.zeros((B.m, 8), dtype=torch.float64, device=DEV), B, as_dev(np.zeros((B.n, 8)), "R"),
-               engine="mfma")
+    # round 3: the forward product runs on matrix cores too (panel layout of B'); forward quirks drop α
+    Xf = np.random.default_rng(1).uniform(-1, 1, (B.n, 8))
+    Yf = as_dev(np.ones((B.m, 8)), "R")
+    V.mul_(Yf, B, as_dev(Xf, "R"), 3.0, 2.0, quirks=True, engine="mfma")
+    want = np.stack([O.mul(R, Xf[:, j].copy(), np.ones(B.m), 1.0, 2.0, trans=False, ref_semantics=False)
+                     for j in range(8)], axis=1)
+    assert rel(Yf.cpu().numpy(), want) <= TOL64
 
 
 def test_mfma_host_memory_and_info():
