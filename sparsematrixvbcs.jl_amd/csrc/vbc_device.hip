@@ -430,9 +430,11 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         split = 1;
         if (planar && h->planar_split != 0) {
             if (h->planar_split > 1) split = h->planar_split;
-            else  // P waves per chunk while the grid stays within half the wave slots (ct20stif stand-in:
-                  // P = 4 10.6 us vs 8 11.2; ldoor's 1/8 stripe shard: P = 2 16.3 us vs 4 17.3, 8 18.7, 1 20.0)
-                while (split < 8 && (double)nch * split * 2 * 2 <= share) split *= 2;
+            else  // P waves per chunk while the grid stays within a quarter of the wave slots: the phased
+                  // split kernel (three memory round trips per NS steps) wants longer slices (ct20stif
+                  // stand-in, graph-timed: P = 2 8.9 us, 4 9.7, 8 9.4, one wave 10.6; round 2's kernel
+                  // took P = 4 at half the slots)
+                while (split < 8 && (double)nch * split * 2 * 4 <= share) split *= 2;
             if (mask && split == 2 && h->planar_split < 0) split = 1;  // masked: P = 2 measured slower
         }
         // the split product runs the plain planar layout; so does a pair layout that would fill fewer than
@@ -490,6 +492,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.u = h->slot_u;
     b.diag = h->diag;
     b.xcd = (planar && split == 1) ? h->xcd_p : 0;  // split grids are small (one chunk per workgroup)
+    b.nowonly = h->slot_wonly ? 0 : 1;
     b.spl = slot_spl(h, kind, w);
     b.planar = planar ? 1 : 0;
     b.run = run;
@@ -604,7 +607,10 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     }
     // compressed keys: measured faster on FE except the fp32 forward product (145 -> 158 us)
     const bool kc_wanted = h->slot_keys16 == 1 ? !(kind == 1 && esz == 4) : h->slot_keys16 == 2;
-    ps.kc_ok = kc_wanted && slot_keys_compressible(ps.keys, rows, RPI);
+    // split bins (small matrices, latency-bound): 32-bit keys unless VBC_SPLIT_KC=1 -- a compressed key
+    // costs a dependent scalar load (its row's pattern offset) before the key itself
+    const bool split_kc = split == 1 || h->split_kc;
+    ps.kc_ok = kc_wanted && split_kc && slot_keys_compressible(ps.keys, rows, RPI);
     h->slot_rows_padded += E;
     h->slot_rows_real += real;
     h->slot_rows_padded_last = E;
@@ -1796,6 +1802,8 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));

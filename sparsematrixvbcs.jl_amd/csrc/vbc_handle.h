@@ -135,6 +135,8 @@ struct vbc_handle {
     int planar_split = -1;            // VBC_PLANAR_SPLIT: -1 auto (few chunks), 0 never, 2 / 4 / 8 waves per chunk
     int target_ranges_p = 4096;       // resident waves of the planar kernel
     int target_ranges_l = 4096;       // resident waves of the lane-stream planar kernel
+    int slot_wonly = 1;               // VBC_SLOT_WONLY=0: the all-width slotted kernel even for one-width launches
+    int split_kc = 0;                 // VBC_SPLIT_KC=1: compressed keys for split planar bins too
     int lanes_deep = 0;               // VBC_LANES_DEEP=1: the lanes kernel's deeper pipeline (gathers a step ahead)
     int planar_lanes = -1;            // VBC_PLANAR_LANES: -1 auto, 0 never, 1 always (planar B'x buckets with
                                       // natural contiguous outputs): per-lane compacted streams (run_planar_lanes)

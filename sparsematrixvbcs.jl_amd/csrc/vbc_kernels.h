@@ -112,6 +112,7 @@ struct SlotBin {
     int32_t lanes;         // 1: per-lane streams (then mask = 1: nlive per row, dead lanes a suffix)
     int32_t ntiles;
     int32_t deep;          // lanes: 1 = keys two steps ahead, gathers one step ahead of their fold
+    int32_t nowonly;       // slotted: 1 = keep the all-width kernel even when every bin has one width (A/B)
     const int32_t *trow;   // ntiles + 1: first row of each tile
     const int32_t *tseg;   // ntiles + 1: first segment of each tile
     const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)
@@ -164,9 +165,10 @@ constexpr int kSweepTileBytes = 8192;  // LDS accumulators per wave: VBC_SWEEP_T
 int launch_sweep(int esz, int kind, const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag, const void *x,
                  void *y, double alpha, double beta, bool rd, hipStream_t stream);
 
+constexpr int kWonlyNarrow2 = 102;  // spmv_slots WONLY: fp32 B'x w = 2 folded two segments per lane (run_slots_narrow)
 // Launches spmv_slots (vbc_slots.hip): returns the hipError_t of the launch.
 int launch_slots(int esz, int kind, const SlotBin *d_bins, int nbins, int total_ranges, bool faste, int xcd, int u, int diag, int stage, bool kc,
-                 const void *x, void *y, double alpha, double beta, bool rd, hipStream_t stream);
+                 int wonly, const void *x, void *y, double alpha, double beta, bool rd, hipStream_t stream);
 int occupancy_slots(int esz, int kind);
 // vbc_planar.hip
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,

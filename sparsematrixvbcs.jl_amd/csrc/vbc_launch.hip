@@ -37,8 +37,18 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
         int stage = slot_stage;
         if (stage < 0) stage = kind == 0 ? 8 : 0;
         if (!(faste && contig)) stage = 0;
+        int wonly = L.sbins[0].wkey;  // one width in every bin: the one-width kernel
+        bool narrow = kind == 0 && sizeof(T) == 4;
+        for (const SlotBin &sb : L.sbins) {
+            wonly = sb.wkey == wonly ? wonly : -1;
+            narrow = narrow && sb.spl == 2 && sb.wkey == 2;
+        }
+        if (wonly == 2 && narrow) wonly = kWonlyNarrow2;
+        else if (wonly == 2 && kind == 0 && sizeof(T) == 4) wonly = -1;  // mixed narrow / plain w = 2 bins
+        if (L.sbins[0].nowonly) wonly = -1;  // VBC_SLOT_WONLY=0 (A/B knob)
         const hipError_t e = (hipError_t)launch_slots((int)sizeof(T), kind, L.d_sbins, (int)L.sbins.size(), L.slot_ranges,
-                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, L.sbins[0].kc != 0, x, y, alpha, beta, rd, stream);
+                                                      faste, xcd, L.sbins[0].u, L.sbins[0].diag, stage, L.sbins[0].kc != 0,
+                                                      wonly, x, y, alpha, beta, rd, stream);
         if (e != hipSuccess) {
             set_error("spmv_slots launch failed: %s", hipGetErrorString(e));
             return VBC_HIP_ERROR;

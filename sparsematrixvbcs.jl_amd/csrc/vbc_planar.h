@@ -257,10 +257,9 @@ __host__ __device__ constexpr int planar_nb()
 }
 
 template <typename T, int W_, bool FASTE, int NB, bool KC, int RUN, bool MASK = false>
-__global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin *__restrict__ bp, const T *__restrict__ x,
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin b, const T *__restrict__ x,
                                                              T *__restrict__ y, T alpha, T beta, int rd_i)
 {
-    const SlotBin b = *bp;
     const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
@@ -449,11 +448,10 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
 }
 
 template <typename T, int W_, int RUN, bool DEEP, bool RD>
-__global__ __launch_bounds__(kBlockThreads) void spmv_planar_lanes(const SlotBin *__restrict__ bp,
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar_lanes(const SlotBin b,
                                                                    const T *__restrict__ x, T *__restrict__ y,
                                                                    T alpha, T beta)
 {
-    const SlotBin b = *bp;
     const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
@@ -595,10 +593,9 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
 }
 
 template <typename T, int W_, int R, bool FASTE, int NB, bool KC, bool MASK = false>
-__global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin *__restrict__ bp, const T *__restrict__ x,
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin b, const T *__restrict__ x,
                                                                  T *__restrict__ y, T alpha, T beta, int rd_i)
 {
-    const SlotBin b = *bp;
     const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
@@ -786,11 +783,10 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
 }
 
 template <bool FASTE, int NB, bool KC, bool MASK = false>
-__global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin *__restrict__ bp,
+__global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin b,
                                                                   const double *__restrict__ x, double *__restrict__ y,
                                                                   double alpha, double beta, int rd_i)
 {
-    const SlotBin b = *bp;
     const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
@@ -827,10 +823,9 @@ __host__ __device__ constexpr int planar_split_step()
 }
 
 template <typename T, int W_, bool KC, int RUN, int P>
-__global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin *__restrict__ bp, const T *__restrict__ x,
+__global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, const T *__restrict__ x,
                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
 {
-    const SlotBin b = *bp;
     const int c = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     if (c >= b.nranges) return;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -848,41 +843,55 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin *__res
     T acc[W_];
 #pragma unroll
     for (int k = 0; k < W_; k++) acc[k] = T(0);
-    for (int R = a; R < e; R += U) {
-        uint32_t kk[NR], bs[NR];
-        T v[U][W_], xv[NR][RUN];
+    // A slice is a few steps (ct20stif: 12 rows per wave): latency-bound, so NS steps at a time go
+    // through three phases -- all keys and values, then all gathers, then the folds in stored order --
+    // one memory round trip per phase instead of one per step.
+#ifndef VBC_SPLIT_NS
+#define VBC_SPLIT_NS 2
+#endif
+    constexpr int NS = VBC_SPLIT_NS;
+    for (int R = a; R < e; R += NS * U) {
+        uint32_t kk[NS][NR], bs[NS][NR];
+        T v[NS][U][W_], xv[NS][NR][RUN];
 #pragma unroll
-        for (int j = 0; j < NR; j++) {
-            const int Rk = min(R + j * RUN, e - RUN);
-            if constexpr (KC) {
-                kk[j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + lane];
-                bs[j] = bases[Rk];
-            } else {
-                kk[j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
-                bs[j] = 0;
+        for (int t = 0; t < NS; t++)
+#pragma unroll
+            for (int j = 0; j < NR; j++) {
+                const int Rk = min(R + t * U + j * RUN, e - RUN);
+                if constexpr (KC) {
+                    kk[t][j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + lane];
+                    bs[t][j] = bases[Rk];
+                } else {
+                    kk[t][j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
+                    bs[t][j] = 0;
+                }
+#pragma unroll
+                for (int d = 0; d < RUN; d++)
+                    ld_row<T, W_, 0>(val + (size_t)min(R + t * U + j * RUN + d, e - 1) * 64 * W_, lane, v[t][j * RUN + d]);
             }
 #pragma unroll
-            for (int d = 0; d < RUN; d++) ld_row<T, W_, 0>(val + (size_t)min(R + j * RUN + d, e - 1) * 64 * W_, lane, v[j * RUN + d]);
-        }
+        for (int t = 0; t < NS; t++)
 #pragma unroll
-        for (int j = 0; j < NR; j++) {
-            const uint32_t gi = KC ? (bs[j] & kSlotIdx) + (kk[j] == kPad16 ? 0u : kk[j]) : kk[j] & kSlotIdx;
-            ld_run<T, RUN>(xg + gi, xv[j]);
-        }
+            for (int j = 0; j < NR; j++) {
+                const uint32_t gi = KC ? (bs[t][j] & kSlotIdx) + (kk[t][j] == kPad16 ? 0u : kk[t][j]) : kk[t][j] & kSlotIdx;
+                ld_run<T, RUN>(xg + gi, xv[t][j]);
+            }
 #pragma unroll
-        for (int j = 0; j < NR; j++) {
-            const bool live = R + j * RUN < e;
-            const bool pad = KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0;
+        for (int t = 0; t < NS; t++)
 #pragma unroll
-            for (int d = 0; d < RUN; d++) {
-                const T xe = pad ? T(0) : xv[j][d];
+            for (int j = 0; j < NR; j++) {
+                const bool live = R + t * U + j * RUN < e;
+                const bool pad = KC ? kk[t][j] == kPad16 : (kk[t][j] & kPad) != 0;
 #pragma unroll
-                for (int k = 0; k < W_; k++) {
-                    const T nv = fmadd(v[j * RUN + d][k], xe, acc[k]);
-                    acc[k] = live ? nv : acc[k];
+                for (int d = 0; d < RUN; d++) {
+                    const T xe = pad ? T(0) : xv[t][j][d];
+#pragma unroll
+                    for (int k = 0; k < W_; k++) {
+                        const T nv = fmadd(v[t][j * RUN + d][k], xe, acc[k]);
+                        acc[k] = live ? nv : acc[k];
+                    }
                 }
             }
-        }
     }
     __shared__ T part[P > 1 ? P - 1 : 1][64 * W_];
     if (wv > 0) {

@@ -15,16 +15,16 @@ static void launch_w(const SlotBin &hb, const SlotBin *d_b, bool faste, bool sta
     T *ys = static_cast<T *>(y);
     constexpr int NB = planar_nb<T, W_>();
     if (hb.mask)  // chunk-local length order: a y-offset table, never the affine write path
-        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC, RUN, true>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs,
+        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC, RUN, true>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs,
                            ys, (T)alpha, (T)beta, (int)rd);
     else if (faste && staged)
-        hipLaunchKernelGGL((spmv_planar<T, W_, true, NB, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar<T, W_, true, NB, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else if (faste)
-        hipLaunchKernelGGL((spmv_planar<T, W_, true, 0, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar<T, W_, true, 0, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else
-        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar<T, W_, false, 0, KC, RUN>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
 }
 
@@ -36,9 +36,9 @@ static void launch_split(const SlotBin &hb, const SlotBin *d_b, const void *x, v
     T *ys = static_cast<T *>(y);
     const dim3 grid(hb.nranges);
     switch (hb.split) {
-    case 2: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 2>), grid, dim3(128), 0, s, d_b, xs, ys, (T)alpha, (T)beta, (int)rd); break;
-    case 4: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 4>), grid, dim3(256), 0, s, d_b, xs, ys, (T)alpha, (T)beta, (int)rd); break;
-    default: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 8>), grid, dim3(512), 0, s, d_b, xs, ys, (T)alpha, (T)beta, (int)rd); break;
+    case 2: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 2>), grid, dim3(128), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
+    case 4: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 4>), grid, dim3(256), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
+    default: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 8>), grid, dim3(512), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
     }
 }
 
@@ -91,16 +91,16 @@ static int launch_pair(const SlotBin &hb, const SlotBin *d_b, bool faste, bool s
     const double *xs = static_cast<const double *>(x);
     double *ys = static_cast<double *>(y);
     if (hb.mask)
-        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            alpha, beta, (int)rd);
     else if (faste && staged)
-        hipLaunchKernelGGL((spmv_planar_pair<true, 8, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
+        hipLaunchKernelGGL((spmv_planar_pair<true, 8, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys, alpha,
                            beta, (int)rd);
     else if (faste)
-        hipLaunchKernelGGL((spmv_planar_pair<true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
+        hipLaunchKernelGGL((spmv_planar_pair<true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys, alpha,
                            beta, (int)rd);
     else
-        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys, alpha,
+        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys, alpha,
                            beta, (int)rd);
     return (int)hipGetLastError();
 }
@@ -114,16 +114,16 @@ static void launch_fwd_wr(const SlotBin &hb, const SlotBin *d_b, bool faste, boo
     T *ys = static_cast<T *>(y);
     constexpr int NB = (8192 / (64 * R * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * R * (int)sizeof(T)));
     if (hb.mask)
-        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs,
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs,
                            ys, (T)alpha, (T)beta, (int)rd);
     else if (faste && staged)
-        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, NB, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, NB, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else if (faste)
-        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
     else
-        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, d_b, xs, ys,
+        hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            (T)alpha, (T)beta, (int)rd);
 }
 
@@ -144,9 +144,9 @@ static void launch_lanes_w(const SlotBin &hb, const SlotBin *d_b, const T *xs, T
                            bool rd, hipStream_t s)
 {
     const dim3 grid((hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock), blk(kBlockThreads);
-    if (rd) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, true>), grid, blk, 0, s, d_b, xs, ys, (T)alpha, (T)beta);
-    else if (hb.deep) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, true, false>), grid, blk, 0, s, d_b, xs, ys, (T)alpha, (T)beta);
-    else hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false>), grid, blk, 0, s, d_b, xs, ys, (T)alpha, (T)beta);
+    if (rd) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, true>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
+    else if (hb.deep) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, true, false>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
+    else hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
 }
 
 template <typename T, int RUN>

@@ -412,7 +412,10 @@ __host__ __device__ constexpr int slot_step(int w, int U)
     return (sizeof(T) == 4 && w > 0 && vec_elems(4, w) == 4) ? U / 2 : U;
 }
 
-template <typename T, int KIND, int U, bool FASTE, int DIAG = 0, int NB = 0, bool KC = false>
+// WONLY >= 0: every bin of the launch has width WONLY, so only that case is compiled -- the register
+// budget is that width's (the all-width switch spilled 83 / ~600 SGPRs in fp64 / fp32, the maximum over
+// cases it never runs on FE).
+template <typename T, int KIND, int U, bool FASTE, int DIAG = 0, int NB = 0, bool KC = false, int WONLY = -1>
 __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__restrict__ bins, int nbins,
                                                             int total_ranges, int xcd_chunk, const T *__restrict__ x,
                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
@@ -441,11 +444,16 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_slots(const SlotBin *__res
     int *lds_out = outs + (FASTE ? 0 : (threadIdx.x >> 6) * kSlotOutEntries);
     // narrow B'x rows: fp32 w = 2 only (FE fp32 124 -> 115 us); the w = 1 forms (CSC columns,
     // 2 / 4 segments per lane) measured slower than one segment per lane (C4: 90 -> 102 us)
-    if constexpr (KIND == 0 && DIAG == 0 && sizeof(T) == 4) {
-        if (b.spl == 2 && b.wkey == 2) {
+    if constexpr (KIND == 0 && DIAG == 0 && sizeof(T) == 4 && (WONLY < 0 || WONLY == kWonlyNarrow2)) {
+        if (WONLY == kWonlyNarrow2 || (b.spl == 2 && b.wkey == 2)) {
             run_slots_narrow<T, 2, 2, U / 2, FASTE, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out);
             return;
         }
+    }
+    if constexpr (WONLY >= 0 && WONLY != kWonlyNarrow2) {
+        run_slots<T, KIND, WONLY, slot_step<T>(WONLY, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds,
+                                                                              lds_out);
+        return;
     }
     switch (b.wkey) {
     case 0: run_slots<T, KIND, 0, slot_step<T>(0, U), FASTE, DIAG, NB, KC>(b, r, lane, x, y, alpha, beta, rd, lds, lds_out); break;

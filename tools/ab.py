@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--nrhs", type=int, default=0, help=">0: time the multi-RHS product (row-major X / Y)")
     ap.add_argument("--shard", default="", help="R/N: time stripe shard R of the N-way split (distributed.stripe_split)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time each variant as one HIP-graph replay of --reps products (span / reps), as bench.py "
+                         "does: per-launch event brackets inflate small kernels")
     ap.add_argument("--copies", type=int, default=1,
                     help="build every variant this many times (A B .. A B ..): placement effects show as spread")
     args = ap.parse_args()
@@ -99,8 +102,28 @@ def main():
             run(i)
     torch.cuda.synchronize()
     times = {i: [] for i in range(len(variants))}
+    graphs = []
+    if args.graph:
+        gs = torch.cuda.Stream()
+        for i in range(len(variants)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs):
+                stream = torch.cuda.current_stream()
+                for _ in range(args.reps):
+                    run(i)
+            graphs.append(g)
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
     for _ in range(args.rounds):
         for i in range(len(variants)):
+            if args.graph:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                graphs[i].replay()
+                b.record(stream)
+                torch.cuda.synchronize()
+                times[i].append(a.elapsed_time(b) / args.reps)
+                continue
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
             for a, b in ev:
                 a.record(stream)
