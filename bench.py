@@ -240,6 +240,25 @@ def cpu_baseline(B, x_host, esz, budget_s=4.0):
                 nproc=os.cpu_count(), cpu_model=S.cpu_model(), isa=S.isa())
 
 
+def box_info(device):
+    """The GPU and its current clocks (rocm-smi --showclocks), recorded with every line: boxes of the
+    pool differ by a few per cent on the same kernel (round 2: FE 176 us on the driver's box, 170 on
+    others), and the clocks at measurement time are the first thing to compare."""
+    import subprocess
+
+    import torch
+    p = torch.cuda.get_device_properties(device)
+    out = {"name": p.name, "cus": p.multi_processor_count, "hbm_gib": round(p.total_memory / 2 ** 30, 1),
+           "arch": getattr(p, "gcnArchName", None)}
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=30)
+        card = next(iter(json.loads(r.stdout).values()))
+        out["clocks"] = {k: v for k, v in card.items() if "clock" in k.lower() or "level" in k.lower()}
+    except Exception as e:  # no rocm-smi / no permission: the line still stands
+        out["clocks"] = f"unavailable ({type(e).__name__})"
+    return out
+
+
 def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=None):
     """One single-GPU workload: build, warm up, time K products, optional CPU baseline + parity."""
     import torch
@@ -516,6 +535,7 @@ def main():
                    roofline=p["roofline"], cpu_baseline=p.get("cpu_baseline"), parity=p.get("parity"))
         if "parity" in p:
             out["rel_err"] = p["parity"]["rel_err"]
+        out["device"] = box_info(device)
         if not args.no_secondary:
             sec = {}
             for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("c5-fwd", np.float32),
