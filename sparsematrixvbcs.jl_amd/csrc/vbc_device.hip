@@ -1746,7 +1746,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (dtype == VBC_I64) {  // exact integer products (vbc_generic.hip): one layout, both directions
         if (int st = create_int(h, s, static_cast<const int64_t *>(val), nval)) { release(h); return st; }
         h->has_t = (flags & (VBC_CREATE_TRANSPOSED | VBC_CREATE_MULTI)) != 0;
-        h->has_f = (flags & VBC_CREATE_FORWARD) != 0;
+        h->has_f = (flags & (VBC_CREATE_FORWARD | VBC_CREATE_MULTI_FORWARD)) != 0;
         *out = h;
         return VBC_OK;
     }

@@ -26,6 +26,7 @@ const VBC_OK, VBC_DIM_MISMATCH, VBC_INVALID_ARG, VBC_HIP_ERROR, VBC_RCCL_ERROR,
 const VBC_F64, VBC_F32, VBC_I64, VBC_I32, VBC_BOOL = Cint(0), Cint(1), Cint(2), Cint(3), Cint(4)
 const VBC_MEM_DEVICE, VBC_MEM_HOST = Cint(0), Cint(1)
 const VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD = Cuint(1), Cuint(2)
+const VBC_CREATE_MULTI, VBC_CREATE_MULTI_FORWARD = Cuint(4), Cuint(16)  # matrix-core panels of B and of Bᵀ
 const VBC_MUL_REFERENCE_QUIRKS = Cuint(1)
 const VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = Cint(0), Cint(1)
 
@@ -92,8 +93,9 @@ mutable struct HIPSparseMatrix1DVBC{W, Tv, Ti}
 end
 
 function HIPSparseMatrix1DVBC(B::SparseMatrix1DVBC{W, Tv, Ti}; device::Integer=0, forward::Bool=true,
-                              transposed::Bool=true) where {W, Tv, Ti}
-    flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0))
+                              transposed::Bool=true, multi::Bool=false) where {W, Tv, Ti}
+    flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0)) |
+            (multi ? (VBC_CREATE_MULTI | VBC_CREATE_MULTI_FORWARD) : Cuint(0))
     M = HIPSparseMatrix1DVBC{W, Tv, Ti}(B, device, flags, Dict{Cint, Ptr{Cvoid}}())
     finalizer(destroy_handles, M)
     return M
@@ -117,8 +119,9 @@ mutable struct HIPSparseMatrixVBC{U, W, Tv, Ti}
 end
 
 function HIPSparseMatrixVBC(B::SparseMatrixVBC{U, W, Tv, Ti}; device::Integer=0, forward::Bool=true,
-                            transposed::Bool=true) where {U, W, Tv, Ti}
-    flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0))
+                            transposed::Bool=true, multi::Bool=false) where {U, W, Tv, Ti}
+    flags = (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0)) |
+            (multi ? (VBC_CREATE_MULTI | VBC_CREATE_MULTI_FORWARD) : Cuint(0))
     M = HIPSparseMatrixVBC{U, W, Tv, Ti}(B, device, flags, Dict{Cint, Ptr{Cvoid}}())
     finalizer(destroy_handles, M)
     return M
@@ -300,17 +303,27 @@ LinearAlgebra.mul!(y::StridedVector, adjA::AdjOrTransSharded, x::StridedVector) 
 # Multi-RHS (the reference has no matrix mul!, multiply_1DVBC.jl:184-185): Y = α·op(A)·X + β·Y on
 # column-major matrices of the compute eltype through vbc_mul_mat_ex (eltypes carried; B'X on
 # matrix cores for a handle built with VBC_CREATE_MULTI), other eltypes column by column.
-function LinearAlgebra.mul!(Y::StridedMatrix{T}, adjA::AdjOrTransHIP, X::StridedMatrix{T}, α::Number,
-                            β::Number) where {T <: Union{Float64, Float32}}
-    A = parent(adjA)
-    (stride(X, 1) == 1 && stride(Y, 1) == 1) || return _mul_cols!(Y, adjA, X, α, β)
+# (A handle built with multi=true runs both directions on matrix cores, the matrix read once for all
+# right-hand sides; otherwise one SpMV per column.)
+function _mul_mat!(Y::StridedMatrix{T}, A::HIPMatrix, trans::Bool, X::StridedMatrix{T}, α::Number,
+                   β::Number) where {T <: Union{Float64, Float32}}
     h = handle_for(A, T)
     GC.@preserve X Y check(ccall((:vbc_mul_mat_ex, libvbc), Cint,
         (Ptr{Cvoid}, Cint, Int64, Ptr{T}, Cint, Int64, Int64, Ptr{T}, Cint, Int64, Int64, Cdouble, Cdouble, Cint,
          Ptr{Cvoid}, Cuint),
-        h, 1, size(X, 2), X, vbc_dtype(T), stride(X, 2), size(X, 1), Y, vbc_dtype(T), stride(Y, 2), size(Y, 1),
+        h, trans, size(X, 2), X, vbc_dtype(T), stride(X, 2), size(X, 1), Y, vbc_dtype(T), stride(Y, 2), size(Y, 1),
         Float64(α), Float64(β), VBC_MEM_HOST, C_NULL, Cuint(0)))
     return Y
+end
+function LinearAlgebra.mul!(Y::StridedMatrix{T}, adjA::AdjOrTransHIP, X::StridedMatrix{T}, α::Number,
+                            β::Number) where {T <: Union{Float64, Float32}}
+    (stride(X, 1) == 1 && stride(Y, 1) == 1) || return _mul_cols!(Y, adjA, X, α, β)
+    return _mul_mat!(Y, parent(adjA), true, X, α, β)
+end
+function LinearAlgebra.mul!(Y::StridedMatrix{T}, A::HIPMatrix, X::StridedMatrix{T}, α::Number,
+                            β::Number) where {T <: Union{Float64, Float32}}
+    (stride(X, 1) == 1 && stride(Y, 1) == 1) || return _mul_cols!(Y, A, X, α, β)
+    return _mul_mat!(Y, A, false, X, α, β)
 end
 function _mul_cols!(Y::StridedMatrix, adjA, X::StridedMatrix, α::Number, β::Number)
     size(X, 2) == size(Y, 2) || throw(DimensionMismatch("X and Y have different numbers of columns"))
@@ -321,6 +334,7 @@ function _mul_cols!(Y::StridedMatrix, adjA, X::StridedMatrix, α::Number, β::Nu
 end
 LinearAlgebra.mul!(Y::StridedMatrix, adjA::AdjOrTransHIP, X::StridedMatrix, α::Number, β::Number) =
     _mul_cols!(Y, adjA, X, α, β)
+LinearAlgebra.mul!(Y::StridedMatrix, A::HIPMatrix, X::StridedMatrix, α::Number, β::Number) = _mul_cols!(Y, A, X, α, β)
 
 export HIPShardedSparseMatrix
 export HIPSparseMatrix1DVBC, HIPSparseMatrixVBC, HIPSparseMatrixCSC, HIPShardedSparseMatrix1DVBC, TrSpMV!
