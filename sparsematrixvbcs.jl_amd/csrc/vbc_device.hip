@@ -651,6 +651,9 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
                        PendingSlot &ps)
 {
     const int esz = h->esz;
+    // lane pairs (spmv_pair_lanes): fp64 3-wide stripes in runs of 3 -- one 16-B x gather per lane per run
+    const bool pair = h->lanes_pair && esz == 8 && w == 3 && run == 3;
+    const int NS = pair ? 32 : 64;  // streams per tile
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     const int64_t real = sbeg[nseg] - sbeg[0];
     std::vector<int32_t> len(nseg);  // runs per stripe (an empty stripe: one zero run)
@@ -664,10 +667,11 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     int64_t S = (nseg + rounds * nr_target - 1) / (rounds * nr_target);
     S = std::min<int64_t>(smax, std::max<int64_t>(4, (S + 3) / 4 * 4));
     const int64_t ntiles = (nseg + S - 1) / S, nr = ntiles;
-    // per tile: 64 contiguous parts (first stripe of each), their stream lengths, steps
+    // per tile: NS contiguous streams (first stripe of each), their lengths in runs, the steps
     std::vector<int32_t> trow{0}, tseg;
     std::vector<int16_t> lseg((size_t)ntiles * 64);
-    std::vector<std::vector<int32_t>> parts((size_t)ntiles);  // per tile: lane -> [first stripe, last+1) pairs
+    std::vector<std::vector<int32_t>> parts((size_t)ntiles);  // per tile: stream -> {first, end, runs}
+    const int rows_per_step = pair ? 1 : run;  // a pair layout row is a run-row
     int64_t rows = 0;
     for (int64_t t = 0; t < ntiles; t++) {
         const int64_t a = t * S, e = std::min(nseg, a + S);
@@ -687,7 +691,7 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
         };
         while (lo < hi) {
             const int64_t mid = (lo + hi) / 2;
-            if (nparts(mid) <= 64) hi = mid;
+            if (nparts(mid) <= NS) hi = mid;
             else lo = mid + 1;
         }
         const int64_t T = lo;
@@ -703,13 +707,13 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
         });
         std::vector<int32_t> &pt = parts[t];
         for (int l = 0; l < 64; l++) {
-            const bool has = l < (int)pv.size();
+            const bool has = l < NS && l < (int)pv.size();
             lseg[(size_t)t * 64 + l] = (int16_t)(has ? pv[l][1] - a : e - a);
             pt.push_back(has ? (int32_t)pv[l][1] : (int32_t)e);
             pt.push_back(has ? (int32_t)pv[l][2] : (int32_t)e);
-            pt.push_back(has ? (int32_t)pv[l][0] : 0);  // the lane's stream length (runs)
+            pt.push_back(has ? (int32_t)pv[l][0] : 0);  // the stream's length (runs)
         }
-        rows += T * run;
+        rows += T * rows_per_step;
         trow.push_back((int32_t)rows);
     }
     tseg.push_back((int32_t)nseg);
@@ -718,16 +722,16 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     std::vector<int32_t> rchunk(nr + 1);
     for (int64_t r = 0; r <= nr; r++) rchunk[r] = (int32_t)r;
     if (getenv("VBC_VERBOSE"))
-        fprintf(stderr, "[vbc] lanes bin w %d run %d stripes %lld ranges %lld x %lld stripes (target %d), rows %lld "
-                "(real %lld: %.3f)\n", w, run, (long long)nseg, (long long)nr, (long long)S, h->target_ranges_l,
-                (long long)rows, (long long)real, (double)real / (double)std::max<int64_t>(1, rows * 64));
+        fprintf(stderr, "[vbc] lanes bin w %d run %d pair %d stripes %lld ranges %lld x %lld stripes (target %d), rows "
+                "%lld (live %.3f)\n", w, run, (int)pair, (long long)nseg, (long long)nr, (long long)S, h->target_ranges_l,
+                (long long)rows, (double)real / (double)std::max<int64_t>(1, rows * NS * (run / rows_per_step)));
     ps = PendingSlot{};
     SlotBin &b = ps.b;
     b.kind = 0;
     b.wkey = w;
     b.w = w;
     b.wst = w;
-    b.rpi = 64;
+    b.rpi = NS;
     b.nranges = (int32_t)nr;
     b.nseg = (int32_t)nseg;
     b.u = h->slot_u;
@@ -737,6 +741,7 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     b.planar = 1;
     b.run = run;
     b.split = 1;
+    b.pair = pair ? 1 : 0;
     b.mask = 1;
     b.lanes = 1;
     b.deep = h->lanes_deep;
@@ -747,7 +752,9 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     b.contig = 1;
     ps.rows = rows;
     ps.real = real;
-    ps.o_val = ar.reserve((size_t)rows * 64 * w * esz);
+    const int64_t vals_per_row = pair ? 288 : (int64_t)64 * w;
+    const int64_t keys_per_row = NS;
+    ps.o_val = ar.reserve((size_t)rows * vals_per_row * esz);
     ps.o_out = ar.reserve(4);
     ps.o_rrow = ar.reserve(rrow.size() * 4);
     ps.o_rchunk = ar.reserve(rchunk.size() * 4);
@@ -755,7 +762,7 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     ps.o_trow = ar.reserve(trow.size() * 4);
     ps.o_tseg = ar.reserve(tseg.size() * 4);
     ps.o_lseg = ar.reserve(lseg.size() * 2);
-    ps.o_key = ar.reserve((size_t)rows * 64 * 4);
+    ps.o_key = ar.reserve((size_t)rows * keys_per_row * 4);
     ps.key_bytes = (int64_t)(real / run) * 4;  // one key per run is read
     ps.lanes_done = true;
     std::memcpy(ar.at<int32_t>(ps.o_rrow), rrow.data(), rrow.size() * 4);
@@ -767,27 +774,43 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     uint32_t *key = ar.at<uint32_t>(ps.o_key);
     uint32_t *nlv = ar.at<uint32_t>(ps.o_nlive);
     char *vv = ar.at<char>(ps.o_val);
-    std::memset(vv, 0, (size_t)rows * 64 * w * esz);
-    std::memset(key, 0, (size_t)rows * 64 * 4);
+    std::memset(vv, 0, (size_t)rows * vals_per_row * esz);
+    std::memset(key, 0, (size_t)rows * keys_per_row * 4);
     for (int64_t t = 0; t < ntiles; t++) {
-        const int64_t R0 = trow[t], T = (trow[t + 1] - R0) / run;
+        const int64_t R0 = trow[t], T = (trow[t + 1] - R0) / rows_per_step;
         for (int64_t st = 0; st < T; st++) {
-            uint32_t nl = 0;  // lanes are in decreasing stream length: the live ones are a prefix
-            while (nl < 64 && parts[t][3 * nl + 2] > st) nl++;
-            for (int d = 0; d < run; d++) nlv[R0 + st * run + d] = nl;
+            uint32_t nl = 0;  // streams are in decreasing length: the live ones are a prefix
+            while ((int)nl < NS && parts[t][3 * nl + 2] > st) nl++;
+            for (int d = 0; d < rows_per_step; d++) nlv[R0 + st * rows_per_step + d] = nl;
         }
-        for (int l = 0; l < 64; l++) {
+        for (int l = 0; l < NS; l++) {
             int64_t st = 0;
             for (int32_t q = parts[t][3 * l]; q < parts[t][3 * l + 1]; q++) {
                 const int64_t nrun = (sbeg[q + 1] - sbeg[q]) / run;
                 if (nrun == 0) {  // empty stripe: one zero run, PAD | LAST (writes its zeros)
-                    key[(R0 + st * run) * 64 + l] = kPad | kLast;
+                    key[(R0 + st * rows_per_step) * keys_per_row + l] = kPad | kLast;
                     st++;
                     continue;
                 }
                 for (int64_t u = 0; u < nrun; u++, st++) {
-                    const int64_t row0 = R0 + st * run;
-                    key[row0 * 64 + l] = ents[sbeg[q] + u * run].key | (u + 1 == nrun ? kLast : 0u);
+                    const int64_t row0 = R0 + st * rows_per_step;
+                    key[row0 * keys_per_row + l] = ents[sbeg[q] + u * run].key | (u + 1 == nrun ? kLast : 0u);
+                    if (pair) {  // the run's 3 x 3 values in the pair run-row form (run_pair)
+                        double v[3][3];
+                        for (int d = 0; d < 3; d++)
+                            std::memcpy(v[d], val + ents[sbeg[q] + u * 3 + d].voff * esz, 3 * sizeof(double));
+                        double *blk = reinterpret_cast<double *>(vv) + row0 * 288;
+                        blk[4 * l + 0] = v[0][0];
+                        blk[4 * l + 1] = v[0][1];
+                        blk[4 * l + 2] = v[0][2];
+                        blk[4 * l + 3] = v[1][2];
+                        blk[128 + 2 * l + 0] = v[1][0];
+                        blk[128 + 2 * l + 1] = v[1][1];
+                        blk[192 + l] = v[2][2];
+                        blk[224 + 2 * l + 0] = v[2][0];
+                        blk[224 + 2 * l + 1] = v[2][1];
+                        continue;
+                    }
                     for (int d = 0; d < run; d++) {
                         const Entry &en = ents[sbeg[q] + u * run + d];
                         char *rowp = vv + (row0 + d) * 64 * w * esz;
@@ -798,9 +821,9 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
             }
         }
     }
-    h->slot_rows_padded += rows * 64;
+    h->slot_rows_padded += rows * NS * (run / rows_per_step);
     h->slot_rows_real += real;
-    h->slot_rows_padded_last = rows * 64;
+    h->slot_rows_padded_last = rows * NS * (run / rows_per_step);
     return VBC_OK;
 }
 
@@ -1802,6 +1825,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
+    if (const char *e = getenv("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;

@@ -293,7 +293,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar(const SlotBin b, co
 constexpr int kLaneTileBytes = VBC_LANE_TILE_BYTES;  // LDS tile buffer per wave (4 workgroups of 4 waves per
                                                      // CU, as the VGPR limit)
 
-template <typename T, int W_, int U, int RUN, bool DEEP, bool RD>
+template <typename T, int W_, int U, int RUN, bool DEEP, bool RD, int DIAG = 0>
 __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int lane, const T *__restrict__ x,
                                                  T *__restrict__ y, T alpha, T beta, T *buf)
 {
@@ -331,7 +331,7 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
                 }
             }
             const bool fl = live && (kk[j] & kLast) != 0;
-            if (fl) {
+            if (DIAG != 3 && fl) {
 #pragma unroll
                 for (int e = 0; e < W_; e++) buf[cur * W_ + e] = acc[e];
             }
@@ -357,9 +357,18 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
                 ld_row<T, W_, 0>(val + (size_t)min(R + j * RUN + d, R1 - 1) * 64 * W_, ln, v[j * RUN + d]);
         }
     };
+    // DIAG (tools/ab.py ablations, VBC_DIAG): 1 = no x gathers (x taken as 1), 2 = gathers confined to
+    // the first 16 K rows of x (L2-resident), 3 = no LDS stores of finished stripes
     auto gather = [&](const uint32_t (&kk)[NR], T (&xv)[NR][RUN]) {
 #pragma unroll
-        for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & kSlotIdx), xv[j]);
+        for (int j = 0; j < NR; j++) {
+            if constexpr (DIAG == 1) {
+#pragma unroll
+                for (int d = 0; d < RUN; d++) xv[j][d] = T(1);
+            } else {
+                ld_run<T, RUN>(xg + (kk[j] & (DIAG == 2 ? 0x3FFFu : kSlotIdx)), xv[j]);
+            }
+        }
     };
     if constexpr (!DEEP) {
         uint32_t kA[NR], kB[NR];
@@ -447,7 +456,7 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
     }
 }
 
-template <typename T, int W_, int RUN, bool DEEP, bool RD>
+template <typename T, int W_, int RUN, bool DEEP, bool RD, int DIAG = 0>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar_lanes(const SlotBin b,
                                                                    const T *__restrict__ x, T *__restrict__ y,
                                                                    T alpha, T beta)
@@ -456,7 +465,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_lanes(const SlotBin
     const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
     if (rg >= b.nranges) return;
     __shared__ __attribute__((aligned(16))) T tilebuf[kWavesPerBlock][kLaneTileBytes / sizeof(T)];
-    run_planar_lanes<T, W_, planar_step<T, W_, RUN>(), RUN, DEEP, RD>(b, rg, threadIdx.x & 63, x, y, alpha, beta,
+    run_planar_lanes<T, W_, planar_step<T, W_, RUN>(), RUN, DEEP, RD, DIAG>(b, rg, threadIdx.x & 63, x, y, alpha, beta,
                                                                       tilebuf[threadIdx.x >> 6]);
 }
 
@@ -799,6 +808,149 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin 
 #define VBC_PAIR_NRS 4  // run-rows per pipeline stage (ldoor stand-in: 2 -> 82, 3 -> 80, 4 -> 77 us)
 #endif
     run_pair<VBC_PAIR_NRS, FASTE, NB, KC, MASK>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
+}
+
+// Lane-pair streams (SlotBin::lanes with pair: fp64, 3-wide stripes, rows in runs of 3 -- FE-3D): the
+// lane-stream layout with a lane PAIR per stream, so a run's 24 B of x are ONE dwordx4 gather per lane
+// (the pair reads x[g .. g+1] and x[g+1 .. g+2], one line, merged by the addresser) instead of a
+// dwordx4 + dwordx2 per lane: the lane-stream kernel is bound by L1 -> L2 requests, of which the x
+// gathers are two thirds (FE-3D ablation: no gathers 157 us, L2-resident gathers 197, real 204).
+// A tile's stripes are cut into 32 streams; a layout row is a run-row of the 32 streams in the pair
+// kernel's 288-value form (segments A, B, C, D, run_pair), keys and nlive per run-row; the even lane
+// folds columns 0-1, the odd lane column 2, each in stored row order, and a LAST run stores them into
+// the wave's LDS tile buffer at the stream's current stripe slot.  After the loop the wave writes the
+// tile's outputs as one contiguous run (α, β applied there).
+template <int NRS, bool RD>
+__device__ __forceinline__ void run_pair_lanes(const SlotBin &b, int r, int lane, const double *__restrict__ x,
+                                               double *__restrict__ y, double alpha, double beta, double *buf)
+{
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;
+    const int R0 = G(b.rrow)[r], R1 = G(b.rrow)[r + 1];
+    if (R0 >= R1) return;
+    const int s0 = G(b.tseg)[r];
+    const int ns = G(b.tseg)[r + 1] - s0;
+    const bool odd = (lane & 1) != 0;
+    const int ps = lane >> 1;  // stream slot of the pair
+    int cur = (int)G(b.lseg)[(size_t)r * 64 + ps];
+    const gptr<const double> val = G(static_cast<const double *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const double> xg = G(x);
+    const cptr nlive = (cptr)b.nlive;
+    const int o0 = 2 * lane, o1 = odd ? 192 + ps : 128 + 2 * ps, o2 = 224 + 2 * ps;
+    auto load = [&](int R, uint32_t (&kk)[NRS], int (&nl)[NRS], d2 (&v)[NRS][3]) {
+#pragma unroll
+        for (int j = 0; j < NRS; j++) {
+            const int Rc = min(R + j, R1 - 1);
+            nl[j] = (int)nlive[Rc];
+            const bool dead = ps >= nl[j];  // dead pairs: pair 0's addresses (lane parity kept)
+            const int mps = dead ? 0 : ps;
+            const int m0 = dead ? (odd ? 2 : 0) : o0, m1 = dead ? (odd ? 192 : 128) : o1, m2 = dead ? 224 : o2;
+            kk[j] = key[(size_t)Rc * 32 + mps];
+            const gptr<const double> rowp = val + (size_t)Rc * 288;
+            v[j][0] = __builtin_nontemporal_load((gptr<const d2>)(rowp + m0));
+            v[j][1] = *(const __attribute__((address_space(1))) d2 *)(rowp + m1);  // 8-B aligned (odd lanes)
+            v[j][2] = __builtin_nontemporal_load((gptr<const d2>)(rowp + m2));
+        }
+    };
+    auto gather = [&](const uint32_t (&kk)[NRS], d2 (&xv)[NRS]) {
+#pragma unroll
+        for (int j = 0; j < NRS; j++)
+            xv[j] = *(const __attribute__((address_space(1))) d2 *)(xg + (kk[j] & kSlotIdx) + (odd ? 1 : 0));
+    };
+    double acc0 = 0.0, acc1 = 0.0;  // even: columns 0, 1; odd: column 2 in acc0
+    int R1v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
+    auto compute = [&](int R, const uint32_t (&kk)[NRS], const int (&nl)[NRS], const d2 (&v)[NRS][3],
+                       const d2 (&xv)[NRS]) {
+#pragma unroll
+        for (int j = 0; j < NRS; j++) {
+            const bool live = R + j < R1v && ps < nl[j];  // dead pairs hold pair 0's values
+            const bool kpad = (kk[j] & kPad) != 0;        // an empty stripe's zero run
+            // even sends x[g] (its .x), odd sends x[g+2] (its .y); each receives the element it lacks
+            const double t = odd ? xv[j].y : xv[j].x;
+            const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)tb, 0xB1, 0xF, 0xF, true);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(tb >> 32), 0xB1, 0xF, 0xF, true);
+            const double other = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+            double x0 = odd ? other : xv[j].x, x1 = odd ? xv[j].x : xv[j].y, x2 = odd ? xv[j].y : other;
+            if (kpad) x0 = x1 = x2 = 0.0;
+            // even: v[0] = {r0c0, r0c1}, v[1] = {r1c0, r1c1}, v[2] = {r2c0, r2c1}
+            // odd:  v[0] = {r0c2, r1c2}, v[1].x = r2c2
+            const double n0 = odd ? fmadd(v[j][1].x, x2, fmadd(v[j][0].y, x1, fmadd(v[j][0].x, x0, acc0)))
+                                  : fmadd(v[j][2].x, x2, fmadd(v[j][1].x, x1, fmadd(v[j][0].x, x0, acc0)));
+            const double n1 = fmadd(v[j][2].y, x2, fmadd(v[j][1].y, x1, fmadd(v[j][0].y, x0, acc1)));
+            acc0 = live ? n0 : acc0;
+            acc1 = live ? n1 : acc1;
+            const bool fl = live && (kk[j] & kLast) != 0;
+            if (fl) {
+                if (odd) buf[cur * 3 + 2] = acc0;
+                else {
+                    buf[cur * 3 + 0] = acc0;
+                    buf[cur * 3 + 1] = acc1;
+                }
+            }
+            acc0 = fl ? 0.0 : acc0;
+            acc1 = fl ? 0.0 : acc1;
+            cur += fl ? 1 : 0;
+        }
+    };
+    uint32_t kA[NRS], kB[NRS];
+    int nA[NRS], nB[NRS];
+    d2 vA[NRS][3], vB[NRS][3], xv[NRS];
+    load(R0, kA, nA, vA);
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int R = R0; R < R1; R += 2 * NRS) {
+        gather(kA, xv);
+        load(R + NRS, kB, nB, vB);
+        compute(R, kA, nA, vA, xv);
+        gather(kB, xv);
+        load(R + 2 * NRS, kA, nA, vA);
+        compute(R + NRS, kB, nB, vB, xv);
+    }
+    // the tile's outputs -> y: one contiguous run (every slot was written once by its pair)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double *dst = y + b.out_base + (int64_t)s0 * 3;
+    const int n = ns * 3;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (int i = lane * 2; i < n; i += 128) {
+            if (i + 2 <= n) {
+                d2 q = *reinterpret_cast<const d2 *>(buf + i) * alpha;
+                if constexpr (RD) {
+                    const d2 yo = *(gptr<const d2>)(dst + i);
+                    q.x = fmadd(beta, yo.x, q.x);
+                    q.y = fmadd(beta, yo.y, q.y);
+                }
+                *(gptr<d2>)(dst + i) = q;
+            } else {
+                double q = alpha * buf[i];
+                if constexpr (RD) q = fmadd(beta, G(dst)[i], q);
+                G(dst)[i] = q;
+            }
+        }
+    } else {
+        for (int e = lane; e < n; e += 64) {
+            double q = alpha * buf[e];
+            if constexpr (RD) q = fmadd(beta, G(dst)[e], q);
+            G(dst)[e] = q;
+        }
+    }
+}
+
+template <bool RD>
+__global__ __launch_bounds__(kBlockThreads) void spmv_pair_lanes(const SlotBin b, const double *__restrict__ x,
+                                                                 double *__restrict__ y, double alpha, double beta)
+{
+    const int blk = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (rg >= b.nranges) return;
+    __shared__ __attribute__((aligned(16))) double tilebuf[kWavesPerBlock][kLaneTileBytes / sizeof(double)];
+#ifndef VBC_PAIR_LANES_NRS
+#define VBC_PAIR_LANES_NRS 4  // run-rows per pipeline stage (as VBC_PAIR_NRS)
+#endif
+    run_pair_lanes<VBC_PAIR_LANES_NRS, RD>(b, rg, threadIdx.x & 63, x, y, alpha, beta, tilebuf[threadIdx.x >> 6]);
 }
 
 // Split planar product (SlotBin::split = P > 1; ranges are single chunks): workgroup c = chunk c, wave k

@@ -144,6 +144,11 @@ static void launch_lanes_w(const SlotBin &hb, const SlotBin *d_b, const T *xs, T
                            bool rd, hipStream_t s)
 {
     const dim3 grid((hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock), blk(kBlockThreads);
+    if constexpr (W_ == 3 && RUN == 3) {  // ablations (tools/ab.py, VBC_DIAG=1..3)
+        if (hb.diag == 1) { hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false, 1>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta); return; }
+        if (hb.diag == 2) { hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false, 2>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta); return; }
+        if (hb.diag == 3) { hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false, 3>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta); return; }
+    }
     if (rd) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, true>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
     else if (hb.deep) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, true, false>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
     else hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
@@ -191,6 +196,15 @@ int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bo
                   double alpha, double beta, bool rd, hipStream_t s)
 {
     if (hb.nranges <= 0) return (int)hipSuccess;
+    if (hb.lanes && hb.pair) {  // lane-pair streams (B'x, fp64, w = 3, runs of 3)
+        if (hb.kind != 0 || esz != 8 || hb.wkey != 3 || hb.run != 3) return (int)hipErrorInvalidValue;
+        const dim3 grid((hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock), blk(kBlockThreads);
+        const double *xs = static_cast<const double *>(x);
+        double *ys = static_cast<double *>(y);
+        if (rd) hipLaunchKernelGGL((spmv_pair_lanes<true>), grid, blk, 0, s, hb, xs, ys, alpha, beta);
+        else hipLaunchKernelGGL((spmv_pair_lanes<false>), grid, blk, 0, s, hb, xs, ys, alpha, beta);
+        return (int)hipGetLastError();
+    }
     if (hb.lanes) {  // per-lane compacted streams (B'x)
         if (hb.kind != 0) return (int)hipErrorInvalidValue;
         return esz == 8 ? launch_lanes<double>(hb, d_b, x, y, alpha, beta, rd, s)

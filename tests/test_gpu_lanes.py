@@ -86,14 +86,18 @@ def test_widths_integer_data_bitwise(forced, dtype, w, ranges):
         assert rel(y.cpu().numpy(), ref) <= (TOL64 if dtype == np.float64 else TOL32), (w, alpha)
 
 
+@pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("R", [2, 3])
-def test_row_runs_nonfinite(forced, dtype, R):
+def test_row_runs_nonfinite(forced, dtype, R, pair):
     """Row runs (one key and one R-wide gather per run) with Inf / NaN in x: non-finite values land
     where the oracle puts them; fp64 bit for bit."""
+    forced.setenv("VBC_LANES_PAIR", pair)
     rng = np.random.default_rng(R)
     B = expand_runs(V.synthetic.vbr_1dvbc(6000, 3000, 15000, 3, W=8, dtype=dtype, seed=R), R, seed=R + 1)
     assert lanes_on(B) and B.info(trans=True)["planar_run"] == R
+    # lane pairs: fp64 3-wide runs of 3 only
+    assert B.info(trans=True)["planar_pair"] == (1 if (pair == "1" and R == 3 and dtype == np.float64) else 0)
     x = rng.uniform(-1, 1, B.m).astype(dtype)
     x[[0, 7, 4321]] = [np.inf, np.nan, -np.inf]  # x[0]: the address dead lanes / empty stripes touch
     y = torch.zeros(B.n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
@@ -108,9 +112,12 @@ def test_row_runs_nonfinite(forced, dtype, R):
         assert rel(np.nan_to_num(got[fin], posinf=0, neginf=0), np.nan_to_num(ref[fin], posinf=0, neginf=0)) <= TOL32
 
 
+@pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("ranges", [None, "40"])
-def test_fe3d_bitwise_and_equal_to_masked(forced, ranges):
-    """The irregular 3-dof stiffness operator: lanes == oracle == the masked planar layout, bit for bit."""
+def test_fe3d_bitwise_and_equal_to_masked(forced, ranges, pair):
+    """The irregular 3-dof stiffness operator: lanes (one lane or a lane pair per stream) == oracle ==
+    the masked planar layout, bit for bit."""
+    forced.setenv("VBC_LANES_PAIR", pair)
     if ranges:
         forced.setenv("VBC_TARGET_RANGES_L", ranges)
     B = V.synthetic.fe_stiffness_3d_1dvbc(300000, 3_000_000)
