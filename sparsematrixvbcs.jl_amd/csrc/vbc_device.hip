@@ -430,12 +430,18 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         split = 1;
         if (planar && h->planar_split != 0) {
             if (h->planar_split > 1) split = h->planar_split;
-            else  // P waves per chunk while the grid stays within a quarter of the wave slots: the phased
-                  // split kernel (three memory round trips per NS steps) wants longer slices (ct20stif
-                  // stand-in, graph-timed: P = 2 8.9 us, 4 9.7, 8 9.4, one wave 10.6; round 2's kernel
-                  // took P = 4 at half the slots)
-                while (split < 8 && (double)nch * split * 2 * 4 <= share) split *= 2;
-            if (mask && split == 2 && h->planar_split < 0) split = 1;  // masked: P = 2 measured slower
+            else if ((double)nch / (pair ? 2 : 1) * 2 <= share) {  // in 64-stripe chunks
+                // few chunks (at most half the wave slots): P waves per chunk while the grid stays within
+                // twice the slots and every wave keeps >= 12 (fp64) / 6 (fp32) rows of its chunk.  Graph-
+                // timed (profiles/r03_splitu_*.log, r03_split3_*.log): ct20stif stand-in fp64 (56 rows per
+                // chunk) P = 2 6.5 us, 4 5.9, 8 6.2; fp32 5.1 / 4.3 / 4.2; ldoor's 1/8 shard fp64 11.5 /
+                // 11.0 / 11.8, fp32 8.5 / 7.5 / 7.3; 1/4 shard fp64: lane pairs 22.3, P = 4 20.6; the 1/2
+                // shard (2500 chunks) and the whole ldoor keep the lane pairs (37.6 vs P = 2 40.6; 67 vs 87)
+                const double avg = (double)rows * (pair ? 3 : 1) / (double)std::max<int64_t>(nch, 1);  // x rows
+                const double minrows = (double)h->split_rows * esz / 8.0;
+                while (split < 8 && (double)nch / (pair ? 2 : 1) * split * 2 <= 2 * share && avg / (split * 2) >= minrows)
+                    split *= 2;
+            }
         }
         // the split product runs the plain planar layout; so does a pair layout that would fill fewer than
         // half the wave slots, when the split product may be chosen instead (ldoor's 1/8 shard: 1250 pair
@@ -1827,6 +1833,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
     if (const char *e = getenv("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {

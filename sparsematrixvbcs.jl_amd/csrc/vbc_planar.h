@@ -37,10 +37,17 @@ __host__ __device__ inline int64_t planar_off(int esz, int w, int s, int c)
 
 // VG consecutive elements of a group (non-temporal: the value stream is read once); a 12-B group
 // (fp32, 3 columns) is one dwordx3 load.
-template <typename T, int VG>
+template <typename T, int VG, bool NT = true>
 __device__ __forceinline__ void ld_group(gptr<const T> p, T *r)
 {
-    if constexpr (VG == 3) {
+    if constexpr (!NT && VG == 1) {  // cached loads (small matrices that stay in L2 between products)
+        r[0] = *p;
+    } else if constexpr (!NT && VG != 3) {
+        typedef T vt __attribute__((ext_vector_type(VG)));
+        const vt t = *(gptr<const vt>)p;
+#pragma unroll
+        for (int e = 0; e < VG; e++) r[e] = t[e];
+    } else if constexpr (VG == 3) {
         struct __attribute__((packed, aligned(4))) p3 { T a, b, c; };
         const __attribute__((address_space(1))) p3 *q = (const __attribute__((address_space(1))) p3 *)p;
         r[0] = q->a;  // merged into one dwordx3 load
@@ -56,13 +63,13 @@ __device__ __forceinline__ void ld_group(gptr<const T> p, T *r)
     }
 }
 
-template <typename T, int W_, int GI>
+template <typename T, int W_, int GI, bool NT = true>
 __device__ __forceinline__ void ld_row(gptr<const T> row, int lane, T (&v)[W_])
 {
     if constexpr (GI < planar_ngroups<T, W_>()) {
         constexpr int G = planar_g<T>(), VG = planar_vg<T, W_, GI>();
-        ld_group<T, VG>(row + 64 * GI * G + lane * VG, v + GI * G);
-        ld_row<T, W_, GI + 1>(row, lane, v);
+        ld_group<T, VG, NT>(row + 64 * GI * G + lane * VG, v + GI * G);
+        ld_row<T, W_, GI + 1, NT>(row, lane, v);
     }
 }
 
@@ -959,22 +966,27 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_pair_lanes(const SlotBin b
 // For matrices with fewer chunks than the chip has wave slots (ct20stif: 273 chunks of ~48 rows),
 // where one wave per chunk leaves the product latency-bound.  Same keys, values and gathers as
 // run_planar; summation order is per slice, then across slices.
-// Rows per step of the split product: planar_step's, unless an A/B build sets -DVBC_SPLIT_VALS
-// (values per lane per step; 72 -- usually the whole slice in one step -- measured slower: ct20stif
-// stand-in fp64 10.8 -> 13.2 us, ldoor's 1/8 shard 16.3 -> 20.1 us).
+// Rows per step of the split product: about VBC_SPLIT_VALS values per lane, whole runs (fp64 w = 3,
+// runs of 3: one run).  Short steps measured fastest (cached loads, NS = 1, graph-timed,
+// profiles/r03_splitu_*.log): ct20stif stand-in P = 4: 9 / 18 / 36 values 5.9 / 6.3 / 7.1 us; ldoor's 1/8
+// stripe shard P = 4: 11.0 / 12.0 / 13.3 us.
+#ifndef VBC_SPLIT_VALS
+#define VBC_SPLIT_VALS 9
+#endif
 template <typename T, int W_, int RUN>
 __host__ __device__ constexpr int planar_split_step()
 {
-#ifdef VBC_SPLIT_VALS
     constexpr int cap = 8 * RUN;  // <= 8 runs: their scalar key bases stay in SGPRs
     constexpr int u = (VBC_SPLIT_VALS / W_) / RUN * RUN;
     return u < RUN ? RUN : (u > cap ? cap / RUN * RUN : u);
-#else
-    return planar_step<T, W_, RUN>();
-#endif
 }
 
-template <typename T, int W_, bool KC, int RUN, int P>
+// Keys and values are CACHED loads here (the streaming kernels use non-temporal ones): a split bucket
+// is small by construction, and its layout stays in L2 / MALL from one product to the next (ct20stif
+// stand-in, 25 MB, graph-timed: 8.8 -> 6.2 us; ldoor's 1/8 stripe shard, 52 MB: 11.5 -> 11.0 us).
+// DIAG (A/B ablations, tools/ab.py VBC_DIAG): 1 no x gathers, 2 gathers confined to 2 KB of x,
+// 3 no y store, 4 non-temporal key / value loads.
+template <typename T, int W_, bool KC, int RUN, int P, int DIAG = 0>
 __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, const T *__restrict__ x,
                                                             T *__restrict__ y, T alpha, T beta, int rd_i)
 {
@@ -995,11 +1007,12 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
     T acc[W_];
 #pragma unroll
     for (int k = 0; k < W_; k++) acc[k] = T(0);
-    // A slice is a few steps (ct20stif: 12 rows per wave): latency-bound, so NS steps at a time go
-    // through three phases -- all keys and values, then all gathers, then the folds in stored order --
-    // one memory round trip per phase instead of one per step.
+    // NS steps at a time go through three phases -- all keys and values, then all gathers, then the
+    // folds in stored order.  NS = 1 measured fastest (ct20stif stand-in P = 2: NS 1 / 2 / 3 / 4 =
+    // 8.7 / 8.8 / 9.5 / 11.1 us; ldoor 1/8 shard 11.4 / 13.1 / 13.7 / 16.3 us,
+    // profiles/r03_splitns_*.log): a longer phase only adds clamped duplicate rows at the slice end.
 #ifndef VBC_SPLIT_NS
-#define VBC_SPLIT_NS 2
+#define VBC_SPLIT_NS 1
 #endif
     constexpr int NS = VBC_SPLIT_NS;
     for (int R = a; R < e; R += NS * U) {
@@ -1014,19 +1027,24 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
                     kk[t][j] = (uint32_t)(int32_t)((gptr<const int16_t>)key)[(size_t)doffs[Rk] + lane];
                     bs[t][j] = bases[Rk];
                 } else {
-                    kk[t][j] = __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
+                    kk[t][j] = DIAG != 4 ? key[(size_t)Rk * 64 + lane] : __builtin_nontemporal_load(key + (size_t)Rk * 64 + lane);
                     bs[t][j] = 0;
                 }
 #pragma unroll
                 for (int d = 0; d < RUN; d++)
-                    ld_row<T, W_, 0>(val + (size_t)min(R + t * U + j * RUN + d, e - 1) * 64 * W_, lane, v[t][j * RUN + d]);
+                    ld_row<T, W_, 0, DIAG == 4>(val + (size_t)min(R + t * U + j * RUN + d, e - 1) * 64 * W_, lane, v[t][j * RUN + d]);
             }
 #pragma unroll
         for (int t = 0; t < NS; t++)
 #pragma unroll
             for (int j = 0; j < NR; j++) {
                 const uint32_t gi = KC ? (bs[t][j] & kSlotIdx) + (kk[t][j] == kPad16 ? 0u : kk[t][j]) : kk[t][j] & kSlotIdx;
-                ld_run<T, RUN>(xg + gi, xv[t][j]);
+                if constexpr (DIAG == 1) {
+#pragma unroll
+                    for (int d = 0; d < RUN; d++) xv[t][j][d] = T(1) + T(gi & 1);
+                } else {
+                    ld_run<T, RUN>(xg + (DIAG == 2 ? (gi & 0xFFu) : gi), xv[t][j]);
+                }
             }
 #pragma unroll
         for (int t = 0; t < NS; t++)
@@ -1058,6 +1076,7 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
         for (int k = 0; k < W_; k++) acc[k] += part[q][k * 64 + lane];
     const int seg = c * 64 + lane;
     if (seg >= b.nseg) return;
+    if (DIAG == 3 && acc[0] != T(-12345.678)) return;
     const int o = b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
     gptr<T> yo = G(y) + o;
 #pragma unroll

@@ -35,6 +35,19 @@ static void launch_split(const SlotBin &hb, const SlotBin *d_b, const void *x, v
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
     const dim3 grid(hb.nranges);
+    if constexpr (W_ == 3 && RUN == 3 && !KC) {  // ablations (tools/ab.py, VBC_DIAG=1..4)
+        if (hb.diag >= 1 && hb.diag <= 4) {
+#define VBC_SPLIT_DIAG(D)                                                                                                     \
+    if (hb.diag == D) {                                                                                                       \
+        if (hb.split == 2) hipLaunchKernelGGL((spmv_planar_split<T, 3, false, 3, 2, D>), grid, dim3(128), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); \
+        else if (hb.split == 4) hipLaunchKernelGGL((spmv_planar_split<T, 3, false, 3, 4, D>), grid, dim3(256), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); \
+        else hipLaunchKernelGGL((spmv_planar_split<T, 3, false, 3, 8, D>), grid, dim3(512), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); \
+        return;                                                                                                               \
+    }
+            VBC_SPLIT_DIAG(1) VBC_SPLIT_DIAG(2) VBC_SPLIT_DIAG(3) VBC_SPLIT_DIAG(4)
+#undef VBC_SPLIT_DIAG
+        }
+    }
     switch (hb.split) {
     case 2: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 2>), grid, dim3(128), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
     case 4: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 4>), grid, dim3(256), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
