@@ -281,7 +281,9 @@ typedef struct vbc_info {
     int32_t fwd_run;        /* forward product: output rows in runs of fwd_run share one x-slice gather */
     int32_t planar_mask;    /* bit 0: a B'x planar bucket, bit 1: the forward planar bucket, in masked chunk-local
                                length order (padding lanes fetch nothing); bit 2: a B'x planar bucket in
-                               per-lane compacted streams (tiles of stripes dealt to the lanes) */
+                               per-lane compacted streams (tiles of stripes dealt to the lanes); bit 3:
+                               the forward planar bucket runs the split product (P waves per chunk);
+                               bit 4: the forward bucket in lane streams (node blocks transposed) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

@@ -1145,7 +1145,10 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
     for (int32_t c : cr) rows += c;
     if (real == 0) return false;
     bool mask = false;
-    if ((double)(rows * RPI) > h->slots_pad * (double)real) {
+    // few chunks: natural order for the split product below, unless it pads by more than half
+    const bool few = h->planar_split != 0 && (double)nch * 2 <= (double)h->target_ranges_p &&
+                     (double)(rows * RPI) <= 1.5 * (double)real;
+    if (!few && (double)(rows * RPI) > h->slots_pad * (double)real) {
         if (h->slots_sort == 0) return false;
         if (h->planar_mask != 0) {  // masked chunk-local length order (SlotBin::mask, as the B'x planar bins)
             order = chunk_sorted_order(rb, RPI * h->mask_window);
@@ -1163,12 +1166,25 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
         }
     }
     auto seg_of = [&](int64_t p) { return order.empty() ? p : order[p]; };  // layout position -> run-segment
-    const int64_t nr = std::max<int64_t>(1, std::min<int64_t>(h->target_ranges_p, nch));
+    // few chunks (natural order): P waves per chunk (spmv_planar_fwd_split), the rule of the B'x split
+    // product with its rows counted in values (>= 36 fp64 / 18 fp32 values per lane per wave: 4 blocks
+    // of a 3 x 3 node block in fp64)
+    int split = 1;
+    if (h->planar_split != 0 && order.empty()) {
+        const double share = (double)h->target_ranges_p;
+        if (h->planar_split > 1) split = h->planar_split;
+        else if ((double)nch * 2 <= share) {
+            const double avg = (double)rows / (double)std::max<int64_t>(nch, 1);
+            const double minrows = std::max(1.0, (double)h->split_rows * 3.0 * esz / 8.0 / WV);
+            while (split < 8 && (double)nch * split * 2 <= 2 * share && avg / (split * 2) >= minrows) split *= 2;
+        }
+    }
+    const int64_t nr = split > 1 ? nch : std::max<int64_t>(1, std::min<int64_t>(h->target_ranges_p, nch));
     std::vector<int32_t> rrow{0}, rchunk{0};
     int64_t acc = 0;
     for (int64_t c = 0; c < nch; c++) {
         acc += cr[c];
-        if (c + 1 < nch && (int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows) {
+        if (c + 1 < nch && (split > 1 || ((int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows))) {
             rrow.push_back((int32_t)acc);
             rchunk.push_back((int32_t)(c + 1));
         }
@@ -1186,11 +1202,11 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
     b.nseg = (int32_t)nseg;
     b.u = h->slot_u;
     b.diag = h->diag;
-    b.xcd = h->xcd_p;
+    b.xcd = split > 1 ? 0 : h->xcd_p;
     b.spl = 1;
     b.planar = 1;
     b.run = R;
-    b.split = 1;
+    b.split = split;
     b.pair = 0;
     b.mask = mask ? 1 : 0;
     b.out_affine = order.empty() ? 1 : 0;
@@ -1240,11 +1256,62 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
             }
         }
     }
-    ps.kc_ok = h->slot_keys16 != 0 && slot_keys_compressible(ps.keys, rows, RPI);
+    ps.kc_ok = h->slot_keys16 != 0 && (split == 1 || h->split_kc) && slot_keys_compressible(ps.keys, rows, RPI);
     h->slot_rows_padded += E;
     h->slot_rows_real += real;
     (void)range0;
     return true;
+}
+
+// Forward lane streams (VBC_PLANAR_LANES as for B'x): the B'x lane-stream kernel (run_planar_lanes) with
+// a node block's rows and columns exchanged.  Segment q = output rows R*q .. R*q+R-1 (the kernel's W = R
+// outputs per stripe slot); the k-th block of the segment (stripe j, w columns) is one "run" of w
+// consecutive x rows (the kernel's RUN = w, one w-wide gather) whose d-th row holds A[R*q + 0..R-1][j + d],
+// so the kernel folds acc[r] += A[R*q + r][j + d] * x[j + d] for d = 0..w-1, blocks in stripe order.
+// Chosen where the forward run layout would need the masked order (natural chunks pad beyond
+// slots_pad), with few empty segments and >= 256 segments per resident wave -- FE-3D.
+static bool want_fwd_lanes(const vbc_handle *h, int w, int R, int64_t m, const std::vector<int64_t> &sbeg)
+{
+    if (h->planar_lanes == 0 || w < 1 || w > 3 || !slot_planar(h, 0, R) || m % R) return false;
+    const int64_t nseg = m / R;
+    if (nseg < 64 || nseg >= (int64_t(1) << 31)) return false;
+    if (h->planar_lanes == 1) return true;
+    std::vector<int64_t> rb(nseg + 1, 0);
+    int64_t empty = 0;
+    for (int64_t q = 0; q < nseg; q++) {
+        rb[q + 1] = rb[q] + sbeg[R * q + 1] - sbeg[R * q];
+        empty += sbeg[R * q + 1] == sbeg[R * q];
+    }
+    int64_t rows = 0;
+    for (int32_t c : chunk_rows(rb, 64)) rows += c;
+    if ((double)(rows * 64) <= h->slots_pad * (double)rb[nseg] || empty * 100 > nseg) return false;
+    return (double)nseg >= 256.0 * std::max(1, h->target_ranges_l);
+}
+
+static int build_fwd_lanes(vbc_handle *h, int w, int R, const std::vector<Entry> &ents, const std::vector<int64_t> &sbeg,
+                           int64_t m, const char *val, Arena &ar, PendingSlot &ps)
+{
+    const int esz = h->esz;
+    const int64_t nseg = m / R;
+    std::vector<int64_t> sb(nseg + 1, 0);
+    for (int64_t q = 0; q < nseg; q++) sb[q + 1] = sb[q] + (sbeg[R * q + 1] - sbeg[R * q]) * w;
+    std::vector<Entry> e2((size_t)sb[nseg]);
+    std::vector<char> tv((size_t)sb[nseg] * R * esz);  // the blocks transposed: [block][d][r]
+    for (int64_t q = 0; q < nseg; q++) {
+        const int64_t nb = sbeg[R * q + 1] - sbeg[R * q];
+        for (int64_t k = 0; k < nb; k++) {
+            const uint32_t col = ents[sbeg[R * q] + k].key & kSlotIdx;
+            for (int d = 0; d < w; d++) {
+                const int64_t i = sb[q] + k * w + d;
+                e2[i] = {col + (uint32_t)d, i * R};
+                for (int r = 0; r < R; r++)
+                    std::memcpy(tv.data() + (i * R + r) * esz, val + (ents[sbeg[R * q + r] + k].voff + d) * esz, (size_t)esz);
+            }
+        }
+    }
+    std::vector<int32_t> out(nseg);
+    for (int64_t q = 0; q < nseg; q++) out[q] = (int32_t)(R * q);
+    return build_lanes(h, R, e2, sb, out, w, sb[nseg], tv.data(), ar, ps);
 }
 
 // Forward layout: per width bucket, segments = output rows with entries of that width (ascending),
@@ -1310,16 +1377,24 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
                 ents[e] = {(uint32_t)s.col0[l] | (!slotted && e == cnt[i] ? kHead : 0u), s.voff[l] + (r - s.rbeg[l]) * w};
             }
         Ls.emplace_back();
-        if (single) {  // node-blocked rows: the planar forward layout with row runs
+        if (single) {  // node-blocked rows: the planar forward layout with row runs (or lane streams)
             const int R = fwd_runs(h, w, s.m, ents, sbeg);
             PendingSlot ps;
             int zero = 0;
-            if (R > 1 && build_fwd_runs(h, w, R, ents, sbeg, s.m, val, ar, zero, ps)) {
+            const bool lanes = R > 1 && want_fwd_lanes(h, w, R, s.m, sbeg);
+            if (lanes) {
+                if (int st = build_fwd_lanes(h, w, R, ents, sbeg, s.m, val, ar, ps)) return st;
+            }
+            if (lanes || (R > 1 && build_fwd_runs(h, w, R, ents, sbeg, s.m, val, ar, zero, ps))) {
                 std::vector<PendingSlot> one;
                 one.push_back(std::move(ps));
                 commit_launch_keys(h, one, ar);
                 const PendingSlot &p1 = one[0];
-                h->bytes_f += p1.rows * p1.b.rpi * (int64_t)w * R * h->esz + p1.key_bytes + s.m * h->esz;
+                if (lanes)  // real values, one key per block, nlive per row, the tile tables, y
+                    h->bytes_f += p1.real * (int64_t)R * h->esz + p1.key_bytes + p1.rows * 4 +
+                                  (int64_t)p1.b.ntiles * (8 + 128) + s.m * h->esz;
+                else
+                    h->bytes_f += p1.rows * p1.b.rpi * (int64_t)w * R * h->esz + p1.key_bytes + s.m * h->esz;
                 std::fill(any.begin(), any.end(), 1);
                 pbs.push_back({});
                 pss.push_back(std::move(one));
@@ -2162,8 +2237,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     if (h->has_f)
         for (const auto &l : h->lf)
             for (const auto &b : l.pbins) {
-                info->fwd_run = std::max<int32_t>(info->fwd_run, b.run);
-                if (b.mask) info->planar_mask |= 2;
+                info->fwd_run = std::max<int32_t>(info->fwd_run, b.lanes ? b.wkey : b.run);  // lanes: W = R rows
+                if (b.mask && !b.lanes) info->planar_mask |= 2;
+                if (b.split > 1) info->planar_mask |= 8;
+                if (b.lanes) info->planar_mask |= 16;
             }
     info->bytes_m = h->has_m ? h->bytes_m : h->bytes_mf;  // a forward-only multi handle: its Bᵀ panel layout
     return VBC_OK;

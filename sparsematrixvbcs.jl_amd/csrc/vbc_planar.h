@@ -246,6 +246,10 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
 // Values per lane per stage: fp64 24 (36 / 48 measured the same on ldoor and fe3d), fp32 with row
 // runs 36 (ldoor stand-in 49.5 -> 44.7 us against 24; 48 the same; without runs 36 spills SGPRs:
 // one scalar base per row).  A/B builds: -DVBC_PLANAR_VALS=...
+// values per lane per step of the split products (spmv_planar_split, spmv_planar_fwd_split)
+#ifndef VBC_SPLIT_VALS
+#define VBC_SPLIT_VALS 9
+#endif
 #ifndef VBC_PLANAR_VALS
 #define VBC_PLANAR_VALS (sizeof(T) == 8 || RUN == 1 ? 24 : 36)
 #endif
@@ -626,6 +630,75 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_fwd(const SlotBin b
     run_planar_fwd<T, W_, R, U, FASTE, NB, KC, MASK>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds);
 }
 
+// Split planar forward product (SlotBin kind 1, run = R, split = P > 1; ranges are single chunks of the
+// natural-order layout): the forward counterpart of spmv_planar_split for matrices with few chunks
+// (ct20stif: 273 chunks of ~19 blocks).  Wave k of workgroup c folds the blocks [R0 + k*S, R0 + (k+1)*S)
+// of chunk c in stripe order, one block per step (keys and values, then the w-wide x gather, then the R
+// dot products), keys and values through the cache as in spmv_planar_split; the P partial sums meet in
+// LDS and wave 0 writes y[R*q .. R*q+R-1] = alpha * (((p0 + p1) + p2) + ...) + beta * y.
+template <typename T, int W_, int R, int P>
+__global__ __launch_bounds__(64 * P) void spmv_planar_fwd_split(const SlotBin b, const T *__restrict__ x,
+                                                                T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    constexpr int WV = R * W_;
+    constexpr int U = (VBC_SPLIT_VALS / WV) < 1 ? 1 : (VBC_SPLIT_VALS / WV);
+    const int c = blockIdx.x;
+    if (c >= b.nranges) return;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int R0 = G(b.rrow)[c], R1 = G(b.rrow)[c + 1];
+    const int S = (R1 - R0 + P - 1) / P;
+    const int a = __builtin_amdgcn_readfirstlane(min(R1, R0 + wv * S)), e = __builtin_amdgcn_readfirstlane(min(R1, a + S));
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> xg = G(x);
+    T acc[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) acc[q] = T(0);
+    for (int Rr = a; Rr < e; Rr += U) {
+        uint32_t kk[U];
+        T v[U][WV], xv[U][W_];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int Rc = min(Rr + u, e - 1);
+            kk[u] = key[(size_t)Rc * 64 + lane];
+            ld_row<T, WV, 0, false>(val + (size_t)Rc * 64 * WV, lane, v[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) ld_run<T, W_>(xg + (kk[u] & kSlotIdx), xv[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool live = Rr + u < e && (kk[u] & kPad) == 0;
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                T d = v[u][q * W_] * xv[u][0];
+#pragma unroll
+                for (int k = 1; k < W_; k++) d = fmadd(v[u][q * W_ + k], xv[u][k], d);
+                acc[q] = live ? acc[q] + d : acc[q];
+            }
+        }
+    }
+    __shared__ T part[P - 1][64 * R];
+    if (wv > 0) {
+#pragma unroll
+        for (int q = 0; q < R; q++) part[wv - 1][q * 64 + lane] = acc[q];
+    }
+    __syncthreads();
+    if (wv != 0) return;
+#pragma unroll
+    for (int p = 0; p < P - 1; p++)
+#pragma unroll
+        for (int q = 0; q < R; q++) acc[q] += part[p][q * 64 + lane];
+    const int seg = c * 64 + lane;
+    if (seg >= b.nseg) return;
+    gptr<T> yo = G(y) + b.out_base + (int64_t)seg * R;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        T t = alpha * acc[q];
+        if (rd_i) t = fmadd(beta, yo[q], t);
+        yo[q] = t;
+    }
+}
+
 // Lane-pair planar product (SlotBin::pair: fp64, 3-wide stripes, rows in runs of 3 -- a 3-dof
 // stiffness operator).  A run's three x values are 24 B: one lane needs a dwordx4 + dwordx2 gather
 // (two requests).  Here lanes 2s and 2s+1 share stripe s: they gather x[g .. g+1] and x[g+1 .. g+2]
@@ -970,9 +1043,6 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_pair_lanes(const SlotBin b
 // runs of 3: one run).  Short steps measured fastest (cached loads, NS = 1, graph-timed,
 // profiles/r03_splitu_*.log): ct20stif stand-in P = 4: 9 / 18 / 36 values 5.9 / 6.3 / 7.1 us; ldoor's 1/8
 // stripe shard P = 4: 11.0 / 12.0 / 13.3 us.
-#ifndef VBC_SPLIT_VALS
-#define VBC_SPLIT_VALS 9
-#endif
 template <typename T, int W_, int RUN>
 __host__ __device__ constexpr int planar_split_step()
 {

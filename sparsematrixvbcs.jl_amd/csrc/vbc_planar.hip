@@ -125,6 +125,15 @@ static void launch_fwd_wr(const SlotBin &hb, const SlotBin *d_b, bool faste, boo
     const int grid = (hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
+    if constexpr (!KC) {
+        if (hb.split > 1) {  // few chunks: P waves per chunk (spmv_planar_fwd_split)
+            const dim3 g(hb.nranges);
+            if (hb.split == 2) hipLaunchKernelGGL((spmv_planar_fwd_split<T, W_, R, 2>), g, dim3(128), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd);
+            else if (hb.split == 4) hipLaunchKernelGGL((spmv_planar_fwd_split<T, W_, R, 4>), g, dim3(256), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd);
+            else hipLaunchKernelGGL((spmv_planar_fwd_split<T, W_, R, 8>), g, dim3(512), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd);
+            return;
+        }
+    }
     constexpr int NB = (8192 / (64 * R * (int)sizeof(T))) > 8 ? 8 : (8192 / (64 * R * (int)sizeof(T)));
     if (hb.mask)
         hipLaunchKernelGGL((spmv_planar_fwd<T, W_, R, false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs,

@@ -141,3 +141,57 @@ def test_auto_selection_full_size_fe3d():
     B = V.synthetic.fe_stiffness_3d_1dvbc(3 * 3333333, int(1e8))
     assert lanes_on(B)
     B.release()
+
+
+@pytest.mark.parametrize("ranges", [None, "5"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w", [2, 3])
+def test_forward_lanes(forced, dtype, w, ranges):
+    """Forward mul!(y, B, x) in lane streams (planar_mask bit 4): node blocks of R = 3 output rows
+    transposed into the B'x lane-stream kernel (W = 3 outputs, runs of w x rows).  Random x within
+    tolerance of the oracle's forward product (multiply_1DVBC.jl:9-83), alpha / beta, forward quirks,
+    rows without blocks (beta * y), several tiles per wave; integer values bit for bit."""
+    from tests.test_gpu_planar import sp_blocked
+    if ranges:
+        forced.setenv("VBC_TARGET_RANGES_L", ranges)
+    rng = np.random.default_rng(w + (7 if ranges else 0))
+    base = V.synthetic.vbr_1dvbc(5000, 1500, 24000, w, W=8, dtype=dtype, seed=3 * w)
+    A = sp_blocked(base, 3, rng, dtype)
+    A = A.tolil()
+    A[30:36, :] = 0  # two node rows without blocks
+    A = A.tocsc()
+    A.eliminate_zeros()
+    B = V.SparseMatrix1DVBC[8](A, V.EquiChunker(w))
+    inf = B.info(trans=False)
+    assert inf["planar_mask"] & 16 and inf["fwd_run"] == 3
+    R64 = ref_of(B, np.float64)
+    tol = TOL64 if dtype == np.float64 else TOL32
+    for alpha, beta in ((1.0, 0.0), (-0.5, 2.0)):
+        x = rng.uniform(-1, 1, B.n).astype(dtype)
+        y0 = rng.uniform(-1, 1, B.m).astype(dtype)
+        y = dev(y0.copy())
+        V.mul_(y, B, dev(x), alpha, beta)
+        ref = O.mul(R64, x.astype(np.float64), y0.astype(np.float64), alpha, beta, ref_semantics=False)
+        assert rel(y.cpu().numpy(), ref) <= tol, (alpha, beta)
+    y = dev(y0.copy())
+    V.mul_(y, B, dev(x), 3.0, 0.0, quirks=True)  # forward quirks: alpha dropped
+    assert rel(y.cpu().numpy(), O.mul(R64, x.astype(np.float64), np.zeros(B.m))) <= tol
+    Bi = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs,
+                             rng.integers(-30, 30, len(B.val)).astype(dtype))
+    xi = rng.integers(-20, 20, B.n).astype(dtype)
+    yi = torch.full((B.m,), 7.0, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+    V.mul_(yi, Bi, dev(xi))
+    assert np.array_equal(yi.cpu().numpy().astype(np.float64),
+                          O.mul(ref_of(Bi, np.float64), xi.astype(np.float64), np.zeros(B.m)))
+
+
+def test_forward_lanes_auto_fe3d(monkeypatch):
+    """The irregular 3-dof operator picks forward lane streams by default (>= 256 node rows per resident
+    wave: the wave count is cut to 256 so 10^5 node rows qualify) and matches the oracle."""
+    monkeypatch.setenv("VBC_TARGET_RANGES_L", "256")
+    B = V.synthetic.fe_stiffness_3d_1dvbc(300000, 3_000_000)
+    assert B.info(trans=False)["planar_mask"] & 16
+    x = np.random.default_rng(4).uniform(-1, 1, B.n)
+    y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(y, B, dev(x))
+    assert rel(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(B.m))) <= TOL64

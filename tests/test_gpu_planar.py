@@ -413,6 +413,60 @@ def _to_csc(B):
     return sp.csc_matrix((vals, (rows, cols)), shape=(B.m, B.n))
 
 
+@pytest.mark.parametrize("P", ["2", "4", "8"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("w,R", [(3, 3), (2, 2), (4, 3)])
+def test_forward_split(monkeypatch, P, dtype, w, R):
+    """Split planar forward product (spmv_planar_fwd_split, planar_mask bit 3): P waves per chunk of
+    node-blocked output rows, partial sums met in LDS.  Random x within tolerance of the oracle's
+    forward product (multiply_1DVBC.jl:9-83), alpha / beta, quirks; integer values bit for bit (any
+    summation order is exact)."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", P)
+    monkeypatch.setenv("VBC_SLOTS_PAD", "100")  # keep the natural order (the split product needs it)
+    rng = np.random.default_rng(10 * w + R + int(P))
+    base = V.synthetic.vbr_1dvbc(3000, 900, 20000, w, W=8, dtype=dtype, seed=w * R)
+    B = V.SparseMatrix1DVBC[8](sp_blocked(base, R, rng, dtype), V.EquiChunker(w))
+    inf = B.info(trans=False)
+    assert inf["fwd_run"] == R and inf["planar_mask"] & 8
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    tol = TOL64 if dtype == np.float64 else TOL32
+    for alpha, beta in ((1.0, 0.0), (0.5, -1.5)):
+        x = rng.uniform(-1, 1, B.n).astype(dtype)
+        y0 = rng.uniform(-1, 1, B.m).astype(dtype)
+        y = dev(y0.copy())
+        V.mul_(y, B, dev(x), alpha, beta)
+        ref = O.mul(R64, x.astype(np.float64), y0.astype(np.float64), alpha, beta, ref_semantics=False)
+        assert rel(y.cpu().numpy(), ref) <= tol, (alpha, beta)
+    y = dev(y0.copy())
+    V.mul_(y, B, dev(x), 3.0, 0.0, quirks=True)
+    assert rel(y.cpu().numpy(), O.mul(R64, x.astype(np.float64), np.zeros(B.m))) <= tol
+    Bi = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs,
+                             rng.integers(-30, 30, len(B.val)).astype(dtype))
+    xi = rng.integers(-20, 20, B.n).astype(dtype)
+    yi = torch.zeros(B.m, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+    V.mul_(yi, Bi, dev(xi))
+    Ri = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, Bi.val.astype(np.float64))
+    assert np.array_equal(yi.cpu().numpy().astype(np.float64), O.mul(Ri, xi.astype(np.float64), np.zeros(B.m)))
+
+
+def test_forward_split_auto_small_matrix(monkeypatch):
+    """The ct20stif stand-in's forward product (273 chunks of node rows) picks the split product by
+    default and matches the oracle; VBC_CREATE_SERIAL (serial=True) keeps one wave per chunk."""
+    import bench
+    B = bench.build_matrix("ct20stif", np.float64)
+    assert B.info(trans=False)["planar_mask"] & 8
+    x = np.random.default_rng(2).uniform(-1, 1, B.n)
+    y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(y, B, dev(x))
+    ref = O.mul(ref_of(B), x, np.zeros(B.m))
+    assert rel(y.cpu().numpy(), ref) <= TOL64
+    B.release()
+    B.serial = True
+    assert not B.info(trans=False)["planar_mask"] & 8
+    V.mul_(y, B, dev(x))
+    assert rel(y.cpu().numpy(), ref) <= TOL64
+
+
 def test_forward_row_runs_fallback():
     """One row outside its run's pattern: the forward product keeps the row-by-row layout."""
     import scipy.sparse as sp
