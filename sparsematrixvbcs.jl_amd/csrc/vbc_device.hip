@@ -1179,7 +1179,12 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
             while (split < 8 && (double)nch * split * 2 <= 2 * share && avg / (split * 2) >= minrows) split *= 2;
         }
     }
-    const int64_t nr = split > 1 ? nch : std::max<int64_t>(1, std::min<int64_t>(h->target_ranges_p, nch));
+    // ranges of >= fwd_min_rows chunk rows: the kernel's two-stage pipeline loads up to 3U rows past a
+    // short range's end (clamped duplicates); ldoor's 1/8 stripe shard (4.8 rows per range at 3072
+    // ranges) ran 30.8 us, 16.0 us as 1024 ranges (profiles/r03_fwdshard2.log)
+    const int64_t nr = split > 1 ? nch
+                                 : std::max<int64_t>(1, std::min<int64_t>({(int64_t)h->target_ranges_p, nch,
+                                                                           rows / std::max(1, h->fwd_min_rows)}));
     std::vector<int32_t> rrow{0}, rchunk{0};
     int64_t acc = 0;
     for (int64_t c = 0; c < nch; c++) {
@@ -1190,6 +1195,10 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
         }
     }
     rrow.push_back((int32_t)rows);
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] forward runs bin w %d R %d segments %lld chunks %lld rows %lld (real %lld) mask %d sorted %d "
+                "split %d ranges %zu\n", w, R, (long long)nseg, (long long)nch, (long long)rows, (long long)real, (int)mask,
+                (int)(!order.empty() && !mask), split, rchunk.size());
     ps = PendingSlot{};
     SlotBin &b = ps.b;
     b.kind = 1;
@@ -1909,6 +1918,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
