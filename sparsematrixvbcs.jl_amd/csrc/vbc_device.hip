@@ -459,6 +459,11 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         const double bytes = (double)rows * RPI * (w * esz + 4);
         if (bytes / share < (double)h->range_bytes) nr = (int64_t)std::llround(share / 2);
     }
+    // plain planar bins: at most planar_wps waves per SIMD (fewer, longer ranges keep the resident
+    // waves' x window in L2: ldoor fp64 lane pairs 3 -> 2 waves per SIMD 67.8 -> 65.4 us, fp32 4 -> 2
+    // 36.5 -> 34.7 us, the C4 CSC product 36.7 -> 34.6 us; 1.5 or 2.5 per SIMD are slower,
+    // profiles/r03_bxranges2_*.log, r03_wps_*.log)
+    if (planar && split == 1 && h->planar_wps > 0) nr = std::min<int64_t>(nr, std::max<int64_t>(1, std::llround(quantum * h->planar_wps)));
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
     // fewer chunks than wave slots: whole waves per SIMD (ldoor's 1/4 shard: 2500 pair chunks as 2500
     // ranges 33.0 us, as 2048 ranges 27.7 us)
@@ -1182,6 +1187,8 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
     // ranges of >= fwd_min_rows chunk rows: the kernel's two-stage pipeline loads up to 3U rows past a
     // short range's end (clamped duplicates); ldoor's 1/8 stripe shard (4.8 rows per range at 3072
     // ranges) ran 30.8 us, 16.0 us as 1024 ranges (profiles/r03_fwdshard2.log)
+    // (the B'x rule of at most planar_wps waves per SIMD does not carry over: ldoor fp32 B·x 34.3 ->
+    // 37.9 us with it, profiles/r03_wps_fwd_*.log)
     const int64_t nr = split > 1 ? nch
                                  : std::max<int64_t>(1, std::min<int64_t>({(int64_t)h->target_ranges_p, nch,
                                                                            rows / std::max(1, h->fwd_min_rows)}));
@@ -1919,6 +1926,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
