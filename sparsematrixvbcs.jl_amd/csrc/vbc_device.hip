@@ -330,6 +330,11 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
     if (nseg >= (int64_t(1) << 31)) return 0;
     const int RPI = slot_rpi(h, kind, w);
     double pad_limit = 0;
+    // (not for buckets small enough for the split product, which folds every padding row: build_slots)
+    const double share_p = (double)h->target_ranges_p * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    // (P >= 4; a masked bucket skips P = 2: ldoor's 1/8 stripe shard, 615 chunks, masked lane pairs
+    // 15.3 us vs split P = 2 16.3 us; the ct20stif stand-in, 273 chunks, keeps P = 4: 10.9 vs 12.8 us)
+    const bool split_likely = h->planar_split != 0 && (double)((nseg + RPI - 1) / RPI) * 8 <= share_p;
     auto fits = [&](const std::vector<int64_t> &sb, bool force) {
         const std::vector<int32_t> cr = chunk_rows(sb, RPI);
         int64_t rows = 0, longest = 0;
@@ -339,15 +344,12 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
         const double ratio = (double)(rows * RPI) / (double)real;
         const double share = (double)h->target_ranges_s[kind] * (double)real / (double)std::max<int64_t>(total_entries, 1);
         const double rows_per_range = (double)rows / std::max(1.0, share);
+        // (chunks are atomic: a planar w = 6 bucket of the ldoor stand-in with chunks up to 2x the rows
+        // per range ran 193 us against the merge kernel's 171 us, profiles/r03_fork_ab2.log)
         return ratio <= (pad_limit > 0 ? pad_limit : h->slots_pad) && (double)longest <= std::max(64.0, 0.5 * rows_per_range);
     };
     if (h->slots_sort != 2 && fits(sbeg, h->slots_mode == 1)) return 1;
     if (h->slots_sort == 0) return 0;
-    // (not for buckets small enough for the split product, which folds every padding row: build_slots)
-    const double share_p = (double)h->target_ranges_p * (double)real / (double)std::max<int64_t>(total_entries, 1);
-    // (P >= 4; a masked bucket skips P = 2: ldoor's 1/8 stripe shard, 615 chunks, masked lane pairs
-    // 15.3 us vs split P = 2 16.3 us; the ct20stif stand-in, 273 chunks, keeps P = 4: 10.9 vs 12.8 us)
-    const bool split_likely = h->planar_split != 0 && (double)((nseg + RPI - 1) / RPI) * 8 <= share_p;
     if (mask && kind == 0 && h->planar_mask != 0 && slot_planar(h, 0, w) && !split_likely) {
         order = chunk_sorted_order(sbeg, RPI * h->mask_window);
         pad_limit = kMaskPad;
@@ -855,7 +857,7 @@ static void commit_launch_keys(const vbc_handle *h, std::vector<PendingSlot> &ps
 
 struct PendingSweep {
     SweepBin b;
-    size_t o_tstep, o_key, o_loc, o_val, o_out;
+    size_t o_tstep, o_key, o_loc, o_val, o_out, o_sbase;
 };
 
 // Whether a bucket lacks x locality: the gathers of windows of 64 consecutive segments (the segments
@@ -954,9 +956,38 @@ static int build_sweep(vbc_handle *h, int kind, int w, const std::vector<int64_t
         if ((int64_t)keys.size() / 64 >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "bucket too large");
         tstep.push_back((int32_t)(keys.size() / 64));
     }
+    // Packed keys: a step's 64 entries are consecutive picks of the ascending heap, so their gather
+    // indices lie within a narrow window above the first lane's: key = PAD | segment << lbits | delta,
+    // one 32-bit load per lane instead of the 32-bit index plus the 16-bit segment (6 -> 4 B per entry
+    // and one load instruction less per step), the base read once per step through the scalar cache.
+    const int64_t nsteps = (int64_t)keys.size() / 64;
+    int sbits = 1;
+    while ((1 << sbits) < S) sbits++;
+    const int lbits = 31 - sbits;
+    bool packed = h->sweep_pack != 0 && lbits >= 8;
+    std::vector<uint32_t> sbase;
+    if (packed) {
+        sbase.resize((size_t)nsteps);
+        for (int64_t st = 0; st < nsteps && packed; st++) {
+            const uint32_t b0 = keys[st * 64];  // the smallest pick: never padding
+            sbase[st] = b0 & kSlotIdx;
+            for (int l = 0; l < 64; l++) {
+                const uint32_t k = keys[st * 64 + l];
+                if (k & kPad) continue;
+                if (k < b0 || ((k - b0) >> lbits) != 0) { packed = false; break; }
+            }
+        }
+    }
+    if (packed)
+        for (int64_t e = 0; e < (int64_t)keys.size(); e++) {
+            const uint32_t k = keys[e];
+            keys[e] = (k & kPad) ? kPad : ((uint32_t)locs[e] << lbits) | (k - sbase[e / 64]);
+        }
     pw = PendingSweep{};
     SweepBin &b = pw.b;
     b.kind = kind;
+    b.packed = packed ? 1 : 0;
+    b.lbits = packed ? lbits : 0;
     b.w = w;
     b.tile0 = tile0;
     b.ntiles = (int32_t)ntiles;
@@ -971,12 +1002,14 @@ static int build_sweep(vbc_handle *h, int kind, int w, const std::vector<int64_t
     const int64_t E = (int64_t)keys.size();
     pw.o_tstep = ar.reserve(tstep.size() * 4);
     pw.o_key = ar.reserve(E * 4);
-    pw.o_loc = ar.reserve(E * 2);
+    pw.o_loc = ar.reserve(packed ? 4 : E * 2);
+    pw.o_sbase = ar.reserve(packed ? (size_t)nsteps * 4 : 4);
     pw.o_val = ar.reserve(E * w * esz);
     pw.o_out = ar.reserve(out.size() * 4);
     std::memcpy(ar.at<int32_t>(pw.o_tstep), tstep.data(), tstep.size() * 4);
     std::memcpy(ar.at<uint32_t>(pw.o_key), keys.data(), E * 4);
-    std::memcpy(ar.at<uint16_t>(pw.o_loc), locs.data(), E * 2);
+    if (packed) std::memcpy(ar.at<uint32_t>(pw.o_sbase), sbase.data(), (size_t)nsteps * 4);
+    else std::memcpy(ar.at<uint16_t>(pw.o_loc), locs.data(), E * 2);
     std::memcpy(ar.at<int32_t>(pw.o_out), out.data(), out.size() * 4);
     char *vv = ar.at<char>(pw.o_val);
     for (int64_t e = 0; e < E; e++) {
@@ -984,7 +1017,8 @@ static int build_sweep(vbc_handle *h, int kind, int w, const std::vector<int64_t
         else std::memset(vv + e * w * esz, 0, (size_t)w * esz);
     }
     (kind == 0 ? h->bytes_t : h->bytes_f) +=
-        E * (6 + (int64_t)w * esz) + (int64_t)tstep.size() * 4 + (b.out_affine ? 0 : nseg * 4);
+        E * ((packed ? 4 : 6) + (int64_t)w * esz) + (packed ? nsteps * 4 : 0) + (int64_t)tstep.size() * 4 +
+        (b.out_affine ? 0 : nseg * 4);
     return VBC_OK;
 }
 
@@ -1708,6 +1742,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         b.tstep = reinterpret_cast<const int32_t *>(base + pw.o_tstep);
         b.key = reinterpret_cast<const uint32_t *>(base + pw.o_key);
         b.loc = reinterpret_cast<const uint16_t *>(base + pw.o_loc);
+        b.sbase = reinterpret_cast<const uint32_t *>(base + pw.o_sbase);
         b.val = base + pw.o_val;
         b.out = reinterpret_cast<const int32_t *>(base + pw.o_out);
         L.wbins.push_back(b);
@@ -1779,6 +1814,8 @@ static void release(vbc_handle *h)
     for (void *p : h->d_stage)
         if (p) (void)hipFree(p);
     if (h->order_ev) (void)hipEventDestroy(h->order_ev);
+    for (hipStream_t q : h->lt.fork_streams) (void)hipStreamDestroy(q);
+    for (hipEvent_t e : h->lt.fork_events) (void)hipEventDestroy(e);
     delete h;
 }
 
@@ -1904,6 +1941,11 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_DEDUP")) h->slot_dedup = atoi(e) != 0;
     if (const char *e = getenv("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     h->sweep_tile = (h->esz == 8 ? 4 : 2) * kSweepTileBytes;  // measured on NS: fp64 32 KB 473 us (16 KB 508), fp32 16 KB 313 us (32 KB 353)
+    // packed swept keys: NS fp64 464.5 -> 456.2 us, mixed widths 553 -> 539 us; fp32 311 -> 316 us, so
+    // fp64 only (profiles/r03_sweeppack_*.log)
+    h->sweep_pack = h->esz == 8;
+    if (const char *e = getenv("VBC_FORK")) h->fork = atoi(e) != 0;
+    if (const char *e = getenv("VBC_SWEEP_PACK")) h->sweep_pack = atoi(e) != 0;
     if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
     if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
@@ -1999,6 +2041,19 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         return fail(VBC_HIP_ERROR, "hipMemcpy of the matrix arena failed");
     }
     if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt, sw_t))) { release(h); return st; }
+    if (h->has_t && h->fork && launch_groups(h->lt) >= 2) {  // side streams for the independent B'x groups
+        const int ns = std::min(launch_groups(h->lt) - 1, 3);
+        for (int i = 0; i < ns; i++) {
+            hipStream_t q = nullptr;
+            if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipStreamCreate failed"); }
+            h->lt.fork_streams.push_back(q);
+        }
+        for (int i = 0; i <= ns; i++) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipEventCreate failed"); }
+            h->lt.fork_events.push_back(e);
+        }
+    }
     if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
     if (h->has_mf && (st = finalize_panel(h, pmf, h->lmf))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)

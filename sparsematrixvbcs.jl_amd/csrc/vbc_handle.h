@@ -40,6 +40,12 @@ struct Launch {
     int sweep_tiles = 0;
     int sweep_tile_bytes = 0;      // LDS accumulator bytes per wave the layout was cut for
     int sweep_diag = 0;            // VBC_SWEEP_DIAG ablation (tools/ab.py only)
+    // B'x with several independent launch groups (swept, slotted, each planar bucket, merge + fix-up:
+    // disjoint stripes of y): the groups after the first run on side streams forked from the caller's
+    // stream by an event and joined back, so small buckets overlap instead of queueing one after the
+    // other (graph capture records them as parallel branches).  Empty when one group or VBC_FORK=0.
+    std::vector<hipStream_t> fork_streams;
+    std::vector<hipEvent_t> fork_events;  // [0]: the fork, [1 + i]: side stream i done
 };
 
 // The panel layout of the MFMA multi-RHS transposed product (vbc_panel.h): one launch.
@@ -121,6 +127,7 @@ struct vbc_handle {
     int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
     bool slot_dedup = true;           // VBC_SLOT_DEDUP=0: one stored delta pattern per compressed row
     int slot_keys16 = 1;              // VBC_SLOT_KEYS16: 0 keep 32-bit keys, 1 auto, 2 compress whenever possible
+    int fork = 1;                     // VBC_FORK=0: B'x launch groups queue on the caller's stream (Launch::fork_*)
     int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)
     int slot_planar = -1;             // VBC_SLOT_PLANAR: -1 auto (B'x, w = 3..8 wider than a lane vector), 0 never, 1 w >= 3
     int slot_runs = 1;                // VBC_SLOT_RUNS=0: no row-run gathers in planar buckets
@@ -149,6 +156,8 @@ struct vbc_handle {
     int occ_p = 4;                    // workgroups per CU of the planar kernel
     int sweep_mode = -1;              // VBC_SWEEP: -1 auto (no x locality), 0 never, 1 always (w <= 8)
     int sweep_tile = vbc::kSweepTileBytes;  // VBC_SWEEP_TILE=16: 16 KB of LDS accumulators per wave
+    int sweep_pack = 1;               // VBC_SWEEP_PACK=0/1: swept keys as gather index + 16-bit segment (6 B per
+                                      // entry, two loads) or one packed 32-bit key per entry (default: fp64)
 
     // Mutable per-handle state, guarded by `mu` (the layout itself is immutable after create):
     //  * host-pointer staging buffers, grown on demand and reused across calls (VBC_MEM_HOST);
@@ -157,6 +166,7 @@ struct vbc_handle {
     //    previous one first waits for that one's completion event, so concurrent products on
     //    distinct streams stay correct.  Slotted / swept / panel layouts hold no scratch and skip it.
     std::mutex mu;
+    std::mutex fork_mu;               // the fork / join event sequence of a forked B'x launch (Launch::fork_*)
     void *d_stage[4] = {nullptr, nullptr, nullptr, nullptr};  // x / X, y / Y staging; 2, 3: column temporaries
     size_t stage_bytes[4] = {0, 0, 0, 0};
     bool has_scratch = false;         // set at create: some launch of this handle uses carry slots
@@ -169,6 +179,7 @@ struct vbc_handle {
 namespace vbc {
 
 // vbc_launch.hip
+int launch_groups(const Launch &L);  // independent launch groups of a B'x launch (vbc_launch.hip)
 int mul_dispatch(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
                  hipStream_t stream);
 int mulmat_rowmajor(vbc_handle *h, int64_t nrhs, const char *X, int64_t ldx, char *Y, int64_t ldy, double alpha,

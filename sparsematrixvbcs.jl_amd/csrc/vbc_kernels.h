@@ -153,9 +153,12 @@ struct SweepBin {
     int32_t out_affine;  // 1: out[s] == out_base + s * out_stride
     int32_t out_base;
     int32_t out_stride;
+    int32_t packed;      // 1: key = PAD | segment << lbits | (gather index - sbase[step]), one 32-bit load
+    int32_t lbits;       // packed: bits of the gather-index delta (31 - bits of the segment)
     const int32_t *tstep;  // ntiles + 1: first step of each tile
-    const uint32_t *key;   // steps * 64: PAD | gather index (B'x: x row; Bx: first x column)
-    const uint16_t *loc;   // steps * 64: segment within the tile
+    const uint32_t *key;   // steps * 64: PAD | gather index (B'x: x row; Bx: first x column), or packed
+    const uint16_t *loc;   // steps * 64: segment within the tile (not packed)
+    const uint32_t *sbase; // packed: steps: the step's smallest gather index (its first lane's)
     const void *val;       // steps * 64 * w values
     const int32_t *out;    // per stripe: first y column (when not affine)
 };

@@ -10,13 +10,26 @@
 
 namespace vbc {
 
+// Independent launch groups of a B'x launch (each writes its own stripes of y): the swept bins, the
+// slotted bins, each planar bin, and the merge kernel with its fix-up (+ the fill list).
+int launch_groups(const Launch &L)
+{
+    return (L.sweep_tiles > 0) + (L.slot_ranges > 0) + (int)L.pbins.size() + (L.total_ranges > 0 || L.nfill > 0);
+}
+
+// The groups in order: group g of launch_groups() on stream `stream`; g < 0: every group on it.
 template <typename T>
-static int launch(const Launch &L, int kind, const void *x, void *y, double alpha, double beta, bool rd,
-                  hipStream_t stream, int xcd, int slot_stage)
+static int launch_group(const Launch &L, int kind, const void *x, void *y, double alpha, double beta, bool rd,
+                        hipStream_t stream, int xcd, int slot_stage, int g)
 {
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
-    if (L.sweep_tiles > 0) {
+    int gi = 0;  // index of the next group
+    auto mine = [&](bool present) {
+        if (!present) return false;
+        return g < 0 || gi++ == g;
+    };
+    if (mine(L.sweep_tiles > 0)) {
         const hipError_t e = (hipError_t)launch_sweep((int)sizeof(T), kind, L.d_wbins, (int)L.wbins.size(), L.sweep_tiles,
                                                       L.sweep_tile_bytes, L.sweep_diag, x, y, alpha, beta, rd, stream);
         if (e != hipSuccess) {
@@ -24,7 +37,7 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
             return VBC_HIP_ERROR;
         }
     }
-    if (L.slot_ranges > 0) {
+    if (mine(L.slot_ranges > 0)) {
         bool faste = !rd, contig = true;
         for (const SlotBin &sb : L.sbins) {
             faste = faste && sb.out_affine;
@@ -55,6 +68,7 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
         }
     }
     for (size_t i = 0; i < L.pbins.size(); i++) {  // planar buckets (vbc_planar.h): one launch each
+        if (!mine(true)) continue;
         const SlotBin &pb = L.pbins[i];
         const bool faste = !rd && pb.out_affine && !getenv("VBC_NO_FASTE");
         const bool staged = faste && pb.contig && slot_stage != 0;
@@ -65,6 +79,7 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
             return VBC_HIP_ERROR;
         }
     }
+    if (!mine(L.total_ranges > 0 || L.nfill > 0)) return VBC_OK;
     if (L.total_ranges > 0) {
         const int grid = (L.total_ranges + kWavesPerBlock - 1) / kWavesPerBlock;
         const int K = L.bins.empty() ? kTileKDefault : L.bins[0].tile_k;
@@ -121,12 +136,40 @@ static int launch(const Launch &L, int kind, const void *x, void *y, double alph
 }
 
 template <typename T>
+static int launch(const vbc_handle *h, const Launch &L, int kind, const void *x, void *y, double alpha, double beta,
+                  bool rd, hipStream_t stream)
+{
+    const int G = launch_groups(L);
+    const int nside = (int)L.fork_streams.size();
+    if (kind != 0 || G < 2 || nside == 0)
+        return launch_group<T>(L, kind, x, y, alpha, beta, rd, stream, h->xcd, h->slot_stage, -1);
+    // fork: the side streams wait for the caller's stream; group 0 stays on it, group g >= 1 goes to
+    // side stream (g - 1) % nside; every side stream that ran a group is joined back.  The event
+    // sequence is serialised per handle (products on several caller streams at once).
+    std::lock_guard<std::mutex> lk(const_cast<vbc_handle *>(h)->fork_mu);
+    VBC_HIP(hipEventRecord(L.fork_events[0], stream));
+    const int used = std::min(nside, G - 1);
+    for (int i = 0; i < used; i++) VBC_HIP(hipStreamWaitEvent(L.fork_streams[i], L.fork_events[0], 0));
+    int st = VBC_OK;
+    for (int g = 0; g < G && st == VBC_OK; g++)
+        st = launch_group<T>(L, kind, x, y, alpha, beta, rd, g == 0 ? stream : L.fork_streams[(g - 1) % nside],
+                             h->xcd, h->slot_stage, g);
+    for (int i = 0; i < used; i++) {  // joined even after a failed launch: no side stream is left dangling
+        if (hipEventRecord(L.fork_events[1 + i], L.fork_streams[i]) != hipSuccess ||
+            hipStreamWaitEvent(stream, L.fork_events[1 + i], 0) != hipSuccess) {
+            if (st == VBC_OK) st = fail(VBC_HIP_ERROR, "fork join failed");
+        }
+    }
+    return st;
+}
+
+template <typename T>
 static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, double alpha, double beta,
                       hipStream_t stream)
 {
     if (trans) {
         if (h->n == 0) return VBC_OK;
-        return launch<T>(h->lt, 0, x, y, alpha, beta, beta != 0.0, stream, h->xcd, h->slot_stage);
+        return launch<T>(h, h->lt, 0, x, y, alpha, beta, beta != 0.0, stream);
     }
     if (h->m == 0) return VBC_OK;
     if (h->f_scale) {
@@ -136,8 +179,8 @@ static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, do
     }
     for (size_t b = 0; b < h->lf.size(); b++) {
         const bool own_beta = !h->f_scale;
-        if (int st = launch<T>(h->lf[b], 1, x, y, alpha, own_beta ? beta : 1.0, own_beta ? beta != 0.0 : true,
-                               stream, h->xcd, h->slot_stage))
+        if (int st = launch<T>(h, h->lf[b], 1, x, y, alpha, own_beta ? beta : 1.0, own_beta ? beta != 0.0 : true,
+                               stream))
             return st;
     }
     return VBC_OK;

@@ -56,7 +56,9 @@ __device__ __forceinline__ void ld_row(gptr<const T> p, T (&r)[W_])
 // KIND 1 (Bx): a lane gathers the w-wide slice x[j ...] of its block's stripe and adds the block's
 // dot product to its output row's accumulator -- per row the blocks come in stripe order, as in the
 // reference's serial stripe loop (multiply_1DVBC.jl:62-71).
-template <typename T, int KIND, int W_, int U, int DIAG>
+// PK (SweepBin::packed): one 32-bit key per entry = PAD | segment << lbits | (gather index - the step's
+// base); the base is a scalar load per step.
+template <typename T, int KIND, int W_, int U, int DIAG, bool PK>
 __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, const T *__restrict__ x,
                                           T *__restrict__ y, T alpha, T beta, bool rd, T *acc)
 {
@@ -70,6 +72,10 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
     const gptr<const T> val = G(static_cast<const T *>(b.val));
     const gptr<const uint32_t> key = G(b.key);
     const gptr<const uint16_t> loc = G(b.loc);
+    typedef __attribute__((address_space(4))) const uint32_t *cptr;  // scalar (constant) loads
+    const cptr sbase = (cptr)b.sbase;
+    const int lb = b.lbits;
+    const uint32_t dmask = (1u << lb) - 1u;
     const gptr<const T> xg = G(x);
     // Three-phase software pipeline per half-iteration: values of stage i+1, gathers of stage i+1
     // (their keys arrived a half earlier), keys of stage i+2, then the fold of stage i -- so the gather
@@ -79,7 +85,8 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
         for (int u = 0; u < U; u++) {
             const size_t p = (size_t)min(s + u, S1 - 1) * 64 + lane;
             kk[u] = __builtin_nontemporal_load(key + p);
-            ll[u] = __builtin_nontemporal_load(loc + p);
+            if constexpr (PK) ll[u] = sbase[min(s + u, S1 - 1)];
+            else ll[u] = __builtin_nontemporal_load(loc + p);
         }
     };
     auto loadv = [&](int s, T (&v)[U][W_]) {
@@ -89,10 +96,10 @@ __device__ __forceinline__ void run_sweep(const SweepBin &b, int t, int lane, co
     auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&ll)[U], T (&xv)[U][XV], uint32_t (&fl)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t gi = (kk[u] & kSlotIdx) & (DIAG == 1 ? 0x1FFFFu : kSlotIdx);
+            const uint32_t gi = (PK ? ll[u] + (kk[u] & dmask) : kk[u] & kSlotIdx) & (DIAG == 1 ? 0x1FFFFu : kSlotIdx);
 #pragma unroll
             for (int e = 0; e < XV; e++) xv[u][e] = xg[gi + e];
-            fl[u] = ll[u] | (kk[u] & kPad);
+            fl[u] = PK ? (((kk[u] & ~kPad) >> lb) | (kk[u] & kPad)) : (ll[u] | (kk[u] & kPad));
             // materialise fl here: otherwise the compiler sinks it past the next key loads, keeps the
             // old keys alive across them, and the register copies at the back edge cost a vmcnt(0)
             // drain per iteration
@@ -178,14 +185,14 @@ __global__ __launch_bounds__(64) void spmv_sweep(const SweepBin *__restrict__ bi
     // Twice as many (up to 256 VGPRs; occupancy is set by the LDS tile anyway) measured the same.
 #define U(W) (16 / W < 2 ? 2 : 16 / W > 8 ? 8 : 16 / W)
     switch (b.w) {
-    case 1: run_sweep<T, KIND, 1, U(1), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 2: run_sweep<T, KIND, 2, U(2), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 3: run_sweep<T, KIND, 3, U(3), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 4: run_sweep<T, KIND, 4, U(4), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 5: run_sweep<T, KIND, 5, U(5), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 6: run_sweep<T, KIND, 6, U(6), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 7: run_sweep<T, KIND, 7, U(7), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
-    case 8: run_sweep<T, KIND, 8, U(8), DIAG>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 1: if (b.packed) run_sweep<T, KIND, 1, U(1), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 1, U(1), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 2: if (b.packed) run_sweep<T, KIND, 2, U(2), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 2, U(2), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 3: if (b.packed) run_sweep<T, KIND, 3, U(3), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 3, U(3), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 4: if (b.packed) run_sweep<T, KIND, 4, U(4), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 4, U(4), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 5: if (b.packed) run_sweep<T, KIND, 5, U(5), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 5, U(5), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 6: if (b.packed) run_sweep<T, KIND, 6, U(6), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 6, U(6), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 7: if (b.packed) run_sweep<T, KIND, 7, U(7), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 7, U(7), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
+    case 8: if (b.packed) run_sweep<T, KIND, 8, U(8), DIAG, true>(b, t, lane, x, y, alpha, beta, rd, acc); else run_sweep<T, KIND, 8, U(8), DIAG, false>(b, t, lane, x, y, alpha, beta, rd, acc); break;
     default: break;
     }
 #undef U

@@ -22,12 +22,14 @@ torch = pytest.importorskip("torch")
 DEV = "cuda:0"
 
 
-@pytest.fixture(params=["8k", "16k"])
+@pytest.fixture(params=["8k", "16k", "16k-unpacked"])
 def forced(request, monkeypatch):
     """Handles created inside the test use the swept layout for every B'x bucket of width <= 8, with
-    8 KB or 16 KB of LDS accumulators per wave."""
+    8 KB or 16 KB of LDS accumulators per wave; keys packed (one 32-bit word: segment and the gather
+    index's delta to the step's base) or, with VBC_SWEEP_PACK=0, the 32-bit index + 16-bit segment."""
     monkeypatch.setenv("VBC_SWEEP", "1")
-    monkeypatch.setenv("VBC_SWEEP_TILE", "16" if request.param == "16k" else "8")
+    monkeypatch.setenv("VBC_SWEEP_TILE", "8" if request.param == "8k" else "16")
+    monkeypatch.setenv("VBC_SWEEP_PACK", "0" if request.param.endswith("unpacked") else "1")
     return request.param
 
 
@@ -197,3 +199,43 @@ def test_auto_uniform_rows_use_sweep(dtype):
     assert rel(y.cpu().numpy(), yr) <= (TOL64 if dtype == np.float64 else TOL32)
     F = V.synthetic.fe_grid_2d(1000, dof=2, dtype=dtype)
     assert sweep_bins(F) == 0 and sweep_bins(F, trans=False) == 0
+
+
+def test_packed_keys_bytes_and_fallback(monkeypatch):
+    """Packed swept keys move 4 instead of 6 index bytes per entry (bytes_t) with the same y bit for bit;
+    a step whose gather indices span more than the delta field (2^21 rows at 1024 segments per tile)
+    keeps the unpacked form, and both forms match the oracle."""
+    monkeypatch.setenv("VBC_SWEEP", "1")
+    rng = np.random.default_rng(11)
+
+    def build(pack, A):
+        monkeypatch.setenv("VBC_SWEEP_PACK", pack)
+        B = V.SparseMatrix1DVBC[8](A, V.EquiChunker(1))
+        B.info(trans=True)  # the handle (and its layout) is made now, under this setting
+        return B
+
+    def run(B, x):
+        y = torch.full((B.n,), float("nan"), dtype=torch.float64, device=DEV)
+        V.mul_(y, B.T, dev(x))
+        return y.cpu().numpy()
+
+    # dense enough: every step's 64 rows lie within a few thousand rows
+    A = sp.random(200000, 4096, density=2e-3, format="csc", random_state=3, dtype=np.float64)
+    Bp, Bu = build("1", A), build("0", A)
+    assert sweep_bins(Bp) == 1 and sweep_bins(Bu) == 1
+    assert Bp.info(trans=True)["bytes_t"] < Bu.info(trans=True)["bytes_t"]
+    x = rng.uniform(-1, 1, A.shape[0])
+    yp, yu = run(Bp, x), run(Bu, x)
+    assert np.array_equal(yp, yu)
+    R = O.Ref1DVBC(Bp.m, Bp.n, Bp.W, Bp.Phi.spl, Bp.pos, Bp.idx, Bp.ofs, Bp.val)
+    assert np.array_equal(yp, O.mul(R, x, np.zeros(Bp.n), trans=True))
+    # sparse: 64 one-row stripes spread over 5e6 rows -- one step spans more than 2^21 rows
+    m = 5_000_000
+    rows = np.sort(rng.choice(m, 64, replace=False))
+    A2 = sp.csc_matrix((rng.uniform(-1, 1, 64), (rows, np.arange(0, 1024, 16))), shape=(m, 1024))
+    Bp2, Bu2 = build("1", A2), build("0", A2)
+    assert Bp2.info(trans=True)["bytes_t"] == Bu2.info(trans=True)["bytes_t"]  # fell back
+    x2 = rng.uniform(-1, 1, m)
+    y2 = run(Bp2, x2)
+    R2 = O.Ref1DVBC(Bp2.m, Bp2.n, Bp2.W, Bp2.Phi.spl, Bp2.pos, Bp2.idx, Bp2.ofs, Bp2.val)
+    assert np.array_equal(y2, O.mul(R2, x2, np.zeros(Bp2.n), trans=True))

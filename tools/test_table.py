@@ -28,6 +28,25 @@ def gpu_time(B, x, y, reps):
     op = V.adjoint(B)
     for _ in range(3):
         V.mul_(y, op, x, True, False)
+    torch.cuda.synchronize()
+    try:  # as bench.py: `reps` products captured in one HIP graph, the replay span / reps (a solver's
+        # back-to-back products; per-launch event pairs add their own gaps to a few-µs kernel)
+        g, s = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                V.mul_(y, op, x, True, False)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            g.replay()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b) / reps)
+        return float(np.median(ts)) * 1e-3
+    except RuntimeError:  # capture refused: per-launch event pairs
+        torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
         a.record()
