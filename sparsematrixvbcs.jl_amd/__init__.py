@@ -10,7 +10,7 @@ from ._lib import ArgumentError, DimensionMismatch, HIPError, UnsupportedDtype
 from .matrices import (DEFAULT_SIMD_SIZE, Adjoint, SparseMatrix1DVBC, SparseMatrixCSC, SparseMatrixVBC,
                        Transpose, adjoint, transpose)
 from .multiply import TrSpMV_, matmul, mul_, mulmat_
-from .costs import model_SparseMatrix1DVBC_TrSpMV_time
+from .costs import TimedChunker, model_SparseMatrix1DVBC_TrSpMV_time
 from .partition import (AlternatePacker, AlternatingPacker, ColumnBlockCostModel, ConstrainedCost, DynamicTotalChunker,
                         EquiChunker, OverlapChunker, SplitPartition, StrictChunker, VertexCount,
                         model_SparseMatrix1DVBC_blocks, model_SparseMatrix1DVBC_memory, pack_plaid,
@@ -25,7 +25,7 @@ __all__ = [
     "transpose", "mul_", "mulmat_", "matmul", "TrSpMV_", "SplitPartition", "EquiChunker",
     "StrictChunker", "OverlapChunker", "DynamicTotalChunker", "ConstrainedCost", "VertexCount",
     "AlternatingPacker", "AlternatePacker", "pack_stripe", "pack_plaid",
-    "model_SparseMatrix1DVBC_blocks", "model_SparseMatrix1DVBC_memory", "model_SparseMatrix1DVBC_TrSpMV_time",
+    "model_SparseMatrix1DVBC_blocks", "model_SparseMatrix1DVBC_memory", "model_SparseMatrix1DVBC_TrSpMV_time", "TimedChunker",
     "ColumnBlockCostModel", "DimensionMismatch",
     "ArgumentError", "HIPError", "UnsupportedDtype", "DEFAULT_SIMD_SIZE",
 ]

@@ -9,7 +9,15 @@ minimises sum(alpha[w] + beta[w]·rows) (DynamicTotalChunker over ColumnBlockCos
 Here the same protocol times libvbc's kernel on the GPU.  Sizes follow costs.jl's "exceed" branch
 scaled to this device's last-level cache (the 256 MiB MALL): the model describes the HBM-streaming
 regime the kernel runs in.  Fitted parameters are cached as JSON (the reference's DiskCache): key =
-(W, Tv, Ti, Tu, device name, libvbc version).
+(W, Tv, Ti, Tu, device name, libvbc version, locality).
+
+locality: "uniform" draws rows over all of x, exactly the reference's generator (costs.jl:63-83).  On
+the GPU those matrices run the row-swept kernel, whose cost is the x gathers (one per stored row,
+whatever the width), so the fitted model prices rows, not values, and its partitions trade fill for
+fewer rows ('min blocks'-like: the ct20stif stand-in 25.7 us against 5.4 us for 'strict',
+profiles/r03_table_ct20stif.log).  "banded" (the default) draws each stripe's rows from a window
+around its own position -- the x locality of the mesh operators the table is run on -- so the fit
+sees the streaming kernels the partition will actually run.
 """
 import json
 import os
@@ -24,18 +32,22 @@ CACHE_DIR = Path(os.environ.get("VBC_AUTOTUNE_DIR", Path.home() / ".cache" / "sp
 LLC_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MI355X_MICROARCH.md)
 
 
-def _key(W, Tv, Ti, Tu, device):
+def _key(W, Tv, Ti, Tu, device, locality="banded"):
     import torch
     name = torch.cuda.get_device_name(device).replace(" ", "_").replace("/", "_")
-    return f"1DVBC_TrSpMV_W{W}_{np.dtype(Tv).name}_{np.dtype(Ti).name}_{np.dtype(Tu).name}_{name}_v{_L.lib().vbc_version()}"
+    return (f"1DVBC_TrSpMV_W{W}_{np.dtype(Tv).name}_{np.dtype(Ti).name}_{np.dtype(Tu).name}_{name}"
+            f"_v{_L.lib().vbc_version()}_{locality}")
 
 
 def model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv=np.float64, Ti=np.int64, Tu=np.float64, device=0, reps=20,
-                                            llc_bytes=LLC_BYTES, seed=0xDEADBEEF):
-    """Time the transposed product on the reference's random VBR matrices (costs.jl:14-99).
+                                            llc_bytes=LLC_BYTES, seed=0xDEADBEEF, locality="banded", band=4096):
+    """Time the transposed product on the reference's random VBR matrices (costs.jl:14-99); with
+    locality="banded" each stripe's rows come from a `band`-row window around it.
     Returns (ms, ns, Ls, ws, qs, T) with T in seconds (median kernel time over `reps`)."""
     import torch
-    from .synthetic import vbr_1dvbc
+    from .synthetic import vbr_1dvbc, vbr_1dvbc_banded
+    if locality not in ("uniform", "banded"):
+        raise ValueError("locality must be 'uniform' or 'banded'")
     from .multiply import mul_
     ms, ns, Ls, ws, qs, T = [], [], [], [], [], []
     isz, vsz, usz = np.dtype(Ti).itemsize, np.dtype(Tv).itemsize, np.dtype(Tu).itemsize
@@ -46,7 +58,9 @@ def model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv=np.float64, Ti=np.int64, Tu=n
         m0 = L0 * w
         q0 = L0 * d
         for (m, L, q) in ((m0, L0, q0), (m0, 2 * L0, q0), (2 * m0, L0, q0), (m0, L0, 2 * q0)):
-            B = vbr_1dvbc(m, L, q, w, W=W, dtype=Tv, seed=seed + w * 131 + L + q)
+            sd = seed + w * 131 + L + q
+            B = (vbr_1dvbc(m, L, q, w, W=W, dtype=Tv, seed=sd) if locality == "uniform" else
+                 vbr_1dvbc_banded(m, L, q, w, band, W=W, dtype=Tv, seed=sd))
             x = torch.ones(B.m, dtype=torch.float64 if np.dtype(Tu) == np.float64 else torch.float32, device=device)
             y = torch.ones(B.n, dtype=x.dtype, device=device)
             for _ in range(3):
@@ -82,15 +96,74 @@ def fit_time_params(W, ms, Ls, ws, qs, T):
 
 
 def model_SparseMatrix1DVBC_TrSpMV_time(W, Tv=np.float64, Ti=np.int64, Tu=np.float64, device=0, refit=False,
-                                        **kwargs):
+                                        locality="banded", **kwargs):
     """ColumnBlockCostModel(alpha, beta) of this GPU's transposed product (cached; costs.jl:12)."""
     CACHE_DIR.mkdir(parents=True, exist_ok=True)
-    path = CACHE_DIR / (_key(W, Tv, Ti, Tu, device) + ".json")
+    path = CACHE_DIR / (_key(W, Tv, Ti, Tu, device, locality) + ".json")
     if path.exists() and not refit:
         d = json.loads(path.read_text())
         return ColumnBlockCostModel(d["alpha"], d["beta"])
-    ms, ns, Ls, ws, qs, T = model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv, Ti, Tu, device, **kwargs)
+    ms, ns, Ls, ws, qs, T = model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv, Ti, Tu, device, locality=locality, **kwargs)
     a_row, alpha, beta = fit_time_params(W, ms, Ls, ws, qs, T)
-    path.write_text(json.dumps({"W": W, "alpha": alpha.tolist(), "beta": beta.tolist(), "alpha_row": a_row,
+    path.write_text(json.dumps({"W": W, "locality": locality, "alpha": alpha.tolist(), "beta": beta.tolist(), "alpha_row": a_row,
                                 "data": {"m": ms, "n": ns, "L": Ls, "w": ws, "q": qs, "t": T}}, indent=1))
     return ColumnBlockCostModel(alpha, beta)
+
+
+class TimedChunker:
+    """Column partition chosen by timing: every candidate chunker's partition is built and its
+    mul!(y, B', x) timed on the GPU (one HIP-graph replay of `reps` products); the fastest wins.
+
+    The linear model above prices a stripe by its width and rows, but on the GPU the cost of a
+    partition is set by the layouts its width buckets get (a planar bucket streams at ~0.8 of HBM
+    peak, a bucket with chunks too long to balance falls back to the merge kernel at ~1/3 of that) and
+    by how many launches they need -- neither is a per-stripe term.  On the ct20stif stand-in the
+    fitted model's partition runs 28-36 us against 5.5 us for StrictChunker (profiles/r03_table_*).
+    Measuring the candidates is the GPU counterpart of the reference's autotuned 'min time' row.
+    `timings` keeps (candidate index, us) of the last call."""
+
+    def __init__(self, candidates, W, dtype=np.float64, device=0, reps=20):
+        if not candidates:
+            raise _L.ArgumentError("TimedChunker needs at least one candidate")
+        self.candidates, self.W, self.dtype, self.device, self.reps = list(candidates), int(W), dtype, device, reps
+        self.timings = []
+
+    def partition(self, A):
+        import torch
+        from .matrices import SparseMatrix1DVBC
+        from .multiply import mul_
+        from .partition import CSCFields, pack_stripe
+        F = A if isinstance(A, CSCFields) else CSCFields(A)
+        m, n = F.shape
+        dev = torch.device("cuda", self.device)
+        tdt = torch.float64 if np.dtype(self.dtype) == np.float64 else torch.float32
+        x = torch.ones(m, dtype=tdt, device=dev)
+        y = torch.empty(n, dtype=tdt, device=dev)
+        best, self.timings = None, []
+        for i, cand in enumerate(self.candidates):
+            Phi = pack_stripe(F, cand)
+            B = SparseMatrix1DVBC.from_csc(self.W, F.A, Phi, dtype=self.dtype)
+            s = torch.cuda.Stream(dev)
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    mul_(y, B.T, x)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(self.reps):
+                    mul_(y, B.T, x)
+            ts = []
+            for _ in range(3):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                g.replay()
+                b.record()
+                torch.cuda.synchronize(dev)
+                ts.append(a.elapsed_time(b) * 1e3 / self.reps)
+            t = float(np.median(ts))
+            self.timings.append((i, round(t, 2)))
+            B.release()
+            del g
+            if best is None or t < best[0]:
+                best = (t, Phi)
+        return best[1]

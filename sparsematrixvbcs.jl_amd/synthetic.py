@@ -45,6 +45,31 @@ def vbr_1dvbc(m, L, q, widths, W=8, dtype=np.float64, seed=0xDEADBEEF, pad=True)
     return SparseMatrix1DVBC(W, m, n, SplitPartition(spl), pos, row + 1, ofs, val)
 
 
+def vbr_1dvbc_banded(m, L, q, widths, band, W=8, dtype=np.float64, seed=0xDEADBEEF):
+    """vbr_1dvbc with x locality: stripe l draws its rows from a window of `band` rows centred on its
+    own position scaled to m (row l * m / L), as a mesh operator's column block does -- the GPU
+    kernels then stream the layout instead of gathering from all of x (costs.py, locality="banded")."""
+    rng = np.random.default_rng(seed)
+    w = np.broadcast_to(np.asarray(widths, dtype=np.int64), (L,)).copy()
+    if w.max(initial=1) > W:
+        raise ValueError("stripe width exceeds W")
+    band = int(max(1, min(band, m)))
+    stripe = rng.integers(0, L, size=int(q), dtype=np.int64)
+    lo = np.clip(stripe * m // max(L, 1) - band // 2, 0, m - band)
+    row = lo + rng.integers(0, band, size=int(q), dtype=np.int64)
+    keys = np.unique(stripe * m + row)  # sorted by (l, i), distinct
+    stripe = keys // m
+    row = keys - stripe * m
+    counts = np.bincount(stripe, minlength=L).astype(np.int64)
+    spl = np.concatenate([[1], 1 + np.cumsum(w)]).astype(np.int64)
+    pos = np.concatenate([[1], 1 + np.cumsum(counts)]).astype(np.int64)
+    ofs = np.concatenate([[1], 1 + np.cumsum(counts * w)]).astype(np.int64)
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + _simd_pad(W, dtype), dtype)
+    val[:nv] = rng.random(nv, dtype=np.float64 if dtype == np.float64 else np.float32)
+    return SparseMatrix1DVBC(W, m, int(spl[-1] - 1), SplitPartition(spl), pos, row + 1, ofs, val)
+
+
 def north_star(dtype=np.float64, scale=1.0, seed=0xDEADBEEF, mixed=False):
     """NS-1DVBC: 10^7 x 10^7, W = 8, w = 4, 2.5e6 stripes, 10 row-blocks per stripe
     on average -> q = 2.5e7 stored rows, nnz = 1.0e8, no fill.  `mixed`: w ~ U{1..8} per stripe with

@@ -104,6 +104,31 @@ def test_time_model_fit_recovers_parameters():
     assert np.allclose(a, alpha, rtol=1e-6) and np.allclose(b, beta, rtol=1e-6) and abs(r - a_row) < 1e-15
 
 
+def test_banded_generator_keeps_rows_near_their_stripe():
+    """The banded VBR generator of the GPU time-model fit (costs.py, locality="banded"): distinct
+    ascending rows per stripe, every row within `band` of the stripe's scaled position, a valid
+    1DVBC (the oracle's product equals scipy's on the same matrix)."""
+    B = V.synthetic.vbr_1dvbc_banded(50000, 3000, 20000, np.arange(3000) % 4 + 1, 1000, W=4, seed=7)
+    st = np.repeat(np.arange(3000), np.diff(B.pos))
+    rows = B.idx - 1
+    assert np.all(np.abs(rows - st * 50000 // 3000) <= 1000)
+    for l in range(0, 3000, 97):
+        r = rows[B.pos[l] - 1:B.pos[l + 1] - 1]
+        assert np.all(np.diff(r) > 0)
+    x = np.random.default_rng(2).uniform(-1, 1, B.m)
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    y = O.mul(R, x, np.zeros(B.n), trans=True)
+    import scipy.sparse as sp
+    w = np.diff(B.Phi.spl)
+    cnt = np.diff(B.pos)
+    wr = np.repeat(w, cnt)  # width of each stored row
+    I = np.repeat(rows, wr)
+    col0 = np.repeat(B.Phi.spl[:-1] - 1, cnt)
+    J = np.concatenate([c + np.arange(k) for c, k in zip(col0, wr)])
+    A = sp.csc_matrix((B.val[:int(B.ofs[-1] - 1)], (I, J)), shape=(B.m, B.n))
+    assert np.allclose(y, A.T @ x, rtol=1e-12, atol=1e-12)
+
+
 @pytest.mark.gpu
 def test_gpu_time_model_fit(tmp_path, monkeypatch):
     """The model fitted to the GPU kernel (small sizes) is positive, monotone and cached; its
@@ -142,3 +167,25 @@ def test_library_loaded_before_torch_shares_its_runtime():
             "print('ok')\n") % str(V._lib.PKG_DIR.parent)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_timed_chunker_picks_the_fastest_candidate():
+    """TimedChunker builds every candidate partition, times its product on the GPU and returns the
+    fastest; the matrix built from it multiplies like the oracle.  On the ct20stif stand-in the
+    'min blocks' partition (w = 6 stripes with fill, the merge kernel) is slower than 'strict'."""
+    import torch
+    A = V.synthetic.standin("Boeing/ct20stif").T.tocsc()
+    lim = V.ConstrainedCost(V.model_SparseMatrix1DVBC_blocks(), V.VertexCount(), 8)
+    tc = V.TimedChunker([V.DynamicTotalChunker(lim), V.StrictChunker(8)], 8)
+    B = V.SparseMatrix1DVBC[8](A, tc)
+    (i0, t0), (i1, t1) = tc.timings
+    assert (i0, i1) == (0, 1) and t0 > 0 and t1 > 0
+    S = V.SparseMatrix1DVBC[8](A, V.StrictChunker(8))
+    assert np.array_equal(B.Phi.spl, S.Phi.spl) == (t1 < t0)
+    x = np.random.default_rng(3).uniform(-1, 1, B.m)
+    y = torch.empty(B.n, dtype=torch.float64, device="cuda:0")
+    V.mul_(y, B.T, torch.from_numpy(x).cuda())
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+    yr = O.mul(R, x, np.zeros(B.n), trans=True, nthreads=8)
+    assert np.linalg.norm(y.cpu().numpy() - yr) <= 1e-12 * np.linalg.norm(yr)

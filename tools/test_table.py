@@ -5,8 +5,9 @@
 For each matrix (mdopen from $VBC_MATRIX_DIR, else the synthetic stand-in with the same n and nnz,
 synthetic.STANDINS) it builds A = permutedims(A) (test_table.jl:27) and reports, per method:
 setup time (host partition + layout build), memory (the reference's `mem` formula, Int64 indices),
-the GPU time of mul!(y, B', x, true, false) (median of HIP-event-timed launches), the oracle's CPU
-time of the same product (all host cores, as the reference's @threads loop), and the normwise error
+the GPU time of mul!(y, B', x, true, false) (one HIP-graph replay of --reps products, median of 5), the CPU
+time of the same product (the reference's SIMD kernel restated, all host cores, as its @threads loop), and the
+normwise error
 against scipy's A'x.  Row 'reference' is TrSpMV!(y, A, x) on the CSC matrix (test_table.jl:29-41).
 """
 import argparse
@@ -142,9 +143,12 @@ def main():
     methods = [("strict", V.StrictChunker(W)), ("overlap", V.OverlapChunker(0.9, W)),
                ("min blocks", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks()))),
                ("min memory", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_memory(dtype, np.int64))))]
-    if args.fit_time_model:
-        mdl = V.model_SparseMatrix1DVBC_TrSpMV_time(W, dtype, np.int64, dtype)
-        methods.append(("min time (GPU model)", V.DynamicTotalChunker(lim(mdl))))
+    if args.fit_time_model:  # the reference's generator (uniform rows) and the banded one (costs.py)
+        for loc in ("uniform", "banded"):
+            mdl = V.model_SparseMatrix1DVBC_TrSpMV_time(W, dtype, np.int64, dtype, locality=loc)
+            methods.append((f"min time (GPU, {loc})", V.DynamicTotalChunker(lim(mdl))))
+        # the candidates above and the two model partitions, timed on the GPU: the fastest wins
+        methods.append(("min time (GPU, timed)", V.TimedChunker([mt for _, mt in methods], W, dtype)))
     for name, method in methods:
         t0 = time.perf_counter()
         B = V.SparseMatrix1DVBC[W](A, method)
