@@ -130,9 +130,7 @@ class TimedChunker:
 
     def partition(self, A):
         import torch
-        from .matrices import SparseMatrix1DVBC
-        from .multiply import mul_
-        from .partition import CSCFields, pack_stripe
+        from .partition import CSCFields
         F = A if isinstance(A, CSCFields) else CSCFields(A)
         m, n = F.shape
         dev = torch.device("cuda", self.device)
@@ -140,30 +138,40 @@ class TimedChunker:
         x = torch.ones(m, dtype=tdt, device=dev)
         y = torch.empty(n, dtype=tdt, device=dev)
         best, self.timings = None, []
-        for i, cand in enumerate(self.candidates):
-            Phi = pack_stripe(F, cand)
-            B = SparseMatrix1DVBC.from_csc(self.W, F.A, Phi, dtype=self.dtype)
-            s = torch.cuda.Stream(dev)
-            with torch.cuda.stream(s):
-                for _ in range(3):
-                    mul_(y, B.T, x)
-            torch.cuda.synchronize(dev)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
-                for _ in range(self.reps):
-                    mul_(y, B.T, x)
-            ts = []
-            for _ in range(3):
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                g.replay()
-                b.record()
-                torch.cuda.synchronize(dev)
-                ts.append(a.elapsed_time(b) * 1e3 / self.reps)
-            t = float(np.median(ts))
-            self.timings.append((i, round(t, 2)))
-            B.release()
-            del g
-            if best is None or t < best[0]:
-                best = (t, Phi)
+        with torch.cuda.device(dev):
+            for i, cand in enumerate(self.candidates):
+                Phi, t = self._time_one(cand, F, x, y, dev)
+                self.timings.append((i, round(t, 2)))
+                if best is None or t < best[0]:
+                    best = (t, Phi)
         return best[1]
+
+    def _time_one(self, cand, F, x, y, dev):
+        """The candidate's partition and its product time (us): one HIP-graph replay of `reps`
+        products, median of 3 replays."""
+        import torch
+        from .matrices import SparseMatrix1DVBC
+        from .multiply import mul_
+        from .partition import pack_stripe
+        Phi = pack_stripe(F, cand)
+        B = SparseMatrix1DVBC.from_csc(self.W, F.A, Phi, dtype=self.dtype)
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                mul_(y, B.T, x)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(self.reps):
+                mul_(y, B.T, x)
+        ts = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            g.replay()
+            b.record()
+            torch.cuda.synchronize(dev)
+            ts.append(a.elapsed_time(b) * 1e3 / self.reps)
+        del g
+        B.release()
+        return Phi, float(np.median(ts))
