@@ -151,7 +151,10 @@ VBC_API int vbc_csc_create_ex(vbc_handle **out, int64_t m, int64_t n, const void
  * TrSpMV!(y, A, x) for a CSC handle, TrSpMV.jl:1-20).  Adjoint and Transpose are identical (real
  * eltypes only).  nx / ny are length(x) / length(y): a mismatch returns VBC_DIM_MISMATCH before any
  * work.  mem = VBC_MEM_DEVICE: x, y are device pointers on the handle's device, and the product is
- * enqueued on `stream` (a hipStream_t; NULL = null stream) without synchronising.
+ * enqueued on `stream` (a hipStream_t; NULL = null stream) without synchronising.  A transposed
+ * product whose buckets need several independent launches may run some of them on side streams the
+ * handle owns: they wait for an event recorded on `stream` and are joined back into it before the call
+ * returns, so every later operation on `stream` (and a HIP graph captured from it) sees the whole y.
  * mem = VBC_MEM_HOST: x, y are host pointers; the call stages them and returns when y is final.
  * x and y must not alias (the reference has the same precondition).  x and y are contiguous vectors of
  * the handle's compute eltype: this is the fast path for callers that know it (the Python mirror after
