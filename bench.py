@@ -91,7 +91,7 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
         try:
             A = V.io.mdopen(name, dtype=dtype).A
         except FileNotFoundError:
-            A = V.synthetic.standin(name, dtype=dtype, seed=seed)
+            A = V.synthetic.standin(name, dtype=dtype, seed=seed, scale=scale)
         if workload == "ldoor-csc":  # TrSpMV!(y, A, x) = A'x on the CSC itself (TrSpMV.jl:1-20)
             C = V.SparseMatrixCSC(A.tocsc())
             C.A = A.tocsc()  # the scipy operand, for the byte count and the oracle
@@ -377,7 +377,7 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
 
     def e2e():
         S.local_mul_t(y_local, x)
-        y_full.copy_(S.gather(y_local))
+        S.gather(y_local, out=y_full)
 
     e2e_steps = max(5, args.steps // 5)
     with torch.cuda.stream(stream):
@@ -391,6 +391,9 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
     torch.cuda.synchronize(device)
     e2e_elapsed = time.perf_counter() - t0
     dist.barrier()
+
+    par = sharded_parity(args, B, S, x_host, x, y_full, y_local, world, rank, local, device, stream) \
+        if not args.no_parity else None
 
     fwd = None
     if forward:  # mul!(y, B, x): partial y per rank + one RCCL all_reduce(sum)
@@ -409,6 +412,10 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
         fwd_elapsed = time.perf_counter() - t0
         dist.barrier()
         fwd = fwd_elapsed
+        if not args.no_parity:  # the all_reduced y of the last timed product against the oracle's B·x
+            xf_host = xf.cpu().numpy()
+            fpar = parity(B, xf_host, yf, trans=False) if rank == 0 else None
+            dist.barrier()
 
     stats = torch.tensor([elapsed, kernel_ms, e2e_elapsed, fwd or 0.0], dtype=torch.float64,
                          device=device if args.backend == "nccl" else "cpu")
@@ -441,14 +448,138 @@ def measure_sharded(args, workload, dtype, world, rank, local, device, forward=F
         },
         "dtype": "f64" if dtype == np.float64 else "f32",
     }
+    if par is not None:
+        out["parity"] = par
     if forward:
         out["forward_allreduce"] = {"value": round(bytes_total * e2e_steps / fwd_elapsed / 1e9, 2), "unit": "GB/s",
                                     "ms_per_step": round(fwd_elapsed / e2e_steps * 1e3, 4),
                                     "what": "mul!(y, B, x): partial y per rank + RCCL all_reduce(sum) of y"}
+        if not args.no_parity:
+            out["forward_allreduce"]["parity"] = fpar
     S.local.release()
     del x, y_local, y_full
     torch.cuda.empty_cache()
     return out
+
+
+def sharded_parity(args, B, S, x_host, x, y_full, y_local, world, rank, local, device, stream):
+    """Correctness of the N > 1 measurement (after its timed region):
+    * the timed product's y -- every rank's disjoint B'x slice, gathered to rank 0 over the process
+      group -- against the CPU oracle on the whole matrix (normwise rel-err, tolerance of BASELINE), and
+      each rank's slice bit for bit;
+    * the same shards rebuilt with VBC_CREATE_SERIAL (B.serial: the reference's serial per-stripe order
+      in every layout, no split planar product): their gathered y must equal the oracle -- and so the
+      single-GPU product, which matches it bit for bit -- exactly.
+    Returns rank 0's dict (None on the other ranks)."""
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as O
+    from oracle import simd as Sd
+    y_ser = torch.empty_like(y_local)
+    S.local.serial = True  # a second handle (layout flags are part of the handle key)
+    with torch.cuda.stream(stream):
+        S.local_mul_t(y_ser, x)
+    torch.cuda.synchronize(device)
+    y_ser_full = S.gather(y_ser, out=torch.empty_like(y_full))
+    torch.cuda.synchronize(device)
+    S.local.release()  # both handles; the caller's later products rebuild what they use
+    S.local.serial = False
+    res = None
+    if rank == 0:
+        t0 = time.perf_counter()
+        R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+        ref = O.mul(R, x_host, np.zeros(B.n, B.val.dtype), trans=True, nthreads=Sd.host_threads())
+        g, gs = y_full.cpu().numpy(), y_ser_full.cpu().numpy()
+        err = float(np.linalg.norm(g.astype(np.float64) - ref) / max(np.linalg.norm(ref), 1e-300))
+        tol = PARITY_TOL[np.dtype(B.val.dtype)]
+        slices = [bool(np.array_equal(g[a:b], ref[a:b])) for a, b in zip(S.splits[:-1], S.splits[1:])]
+        ser = bool(np.array_equal(gs, ref))
+        res = {"rel_err": float(f"{err:.3e}"), "tol": tol, "bitwise_equal": bool(all(slices)),
+               "slices_bitwise": slices, "serial_bitwise_equal": ser, "pass": bool(err <= tol and ser),
+               "oracle": "oracle/vbc_oracle.c orc_1dvbc_mul_t (multiply_1DVBC.jl:90-180) on the whole matrix",
+               "what": ("timed product: rank slices gathered to rank 0 vs the oracle; serial: shards built with "
+                        "VBC_CREATE_SERIAL, gathered y must equal the oracle bit for bit"),
+               "oracle_s": round(time.perf_counter() - t0, 2)}
+    dist.barrier()
+    return res
+
+
+def abi_sharded_child(args):
+    """One process driving devices 0..N-1 through the C ABI's sharded handle (vbc1d_create_sharded /
+    vbc_sharded_mul_ex, distributed.MultiGPUSparseMatrix1DVBC) -- the configuration the Julia shim
+    binds (julia/SparseMatrixVBCsHIP.jl): x broadcast over RCCL, the shards' products on their own
+    devices, the disjoint y slices sent back to devices[0]; the forward product scatters x slices and
+    ncclReduce(sum)s y.  Times K products of each direction (eager: the exchange spans devices) and
+    checks both against the oracle.  Prints one JSON line."""
+    import torch
+
+    import sparsematrixvbcs_amd as V
+    from sparsematrixvbcs_amd import distributed as D
+    devices = [int(d) for d in args.abi_sharded_child.split(",")]
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    esz = np.dtype(dtype).itemsize
+    B = build_matrix(args.workload, dtype, args.scale)
+    t0 = time.perf_counter()
+    S = D.MultiGPUSparseMatrix1DVBC(B, devices=devices, split="stripes")
+    build_s = time.perf_counter() - t0
+    dev0 = torch.device("cuda", devices[0])
+    torch.cuda.set_device(dev0)
+    rng = np.random.default_rng(0xC0FFEE)
+    out = {"devices": devices, "split": "stripes", "build_s": round(build_s, 1),
+           "rccl": len(set(devices)) > 1 or len(devices) == 1,
+           "what": ("one process, C ABI vbc1d_create_sharded + vbc_sharded_mul_ex (the Julia drop-in's multi-GPU "
+                    "configuration): x and y on devices[0]")}
+    bytes_total = algorithmic_bytes(B, esz)
+    for trans, key in ((True, "transposed"), (False, "forward")):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        xh = rng.uniform(-1, 1, nx).astype(dtype)
+        x = torch.from_numpy(xh).to(dev0)
+        y = torch.empty(ny, dtype=x.dtype, device=dev0)
+        op = S.T if trans else S
+        for _ in range(max(1, args.warmup)):
+            V.mul_(y, op, x)
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for _ in range(args.steps):
+            V.mul_(y, op, x)
+        ev1.record()
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+        el = time.perf_counter() - t0
+        out[key] = {"value": round(bytes_total * args.steps / el / 1e9, 2), "unit": "GB/s",
+                    "ms_per_step": round(el / args.steps * 1e3, 5),
+                    "event_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 5),
+                    "op": "mul!(y, B', x): x broadcast, y slices gathered" if trans else
+                          "mul!(y, B, x): x slices, ncclReduce(sum) of y",
+                    "parity": parity(B, xh, y, trans=trans) if not args.no_parity else None}
+    S.release()
+    out["pass"] = all(out[k]["parity"] is None or out[k]["parity"]["pass"] for k in ("transposed", "forward"))
+    print(json.dumps(out), flush=True)
+
+
+def run_abi_sharded(args, world):
+    """Start abi_sharded_child in a fresh process once the rank processes are done with their GPUs
+    (devices 0..N-1 when the box has them, else every shard on device 0), return its JSON."""
+    import subprocess
+    import torch
+    nd = torch.cuda.device_count()
+    devices = list(range(world)) if (nd >= world and not args.same_device) else [0] * world
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--abi-sharded-child", ",".join(map(str, devices)),
+           "--workload", args.workload, "--dtype", args.dtype, "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--scale", str(args.scale)] + (["--no-parity"] if args.no_parity else [])
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                                             "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out", "pass": False}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}: {r.stderr[-1500:]}", "pass": False}
+    return json.loads(lines[-1])
 
 
 def launch_ranks(n):
@@ -500,7 +631,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary workloads")
+    ap.add_argument("--no-abi-sharded", action="store_true",
+                    help="N > 1: skip the one-process C-ABI sharded leg (secondary.abi_sharded)")
+    ap.add_argument("--abi-sharded-child", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.abi_sharded_child:
+        abi_sharded_child(args)
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # plain `python bench.py --gpus N`: start the N ranks ourselves, one process per GPU (what
@@ -563,14 +701,20 @@ def main():
         p = measure_sharded(args, args.workload, dtype, world, rank, local, device)
         out = dict(head, value=p["value"], unit=p["unit"], ms_per_step=p["ms_per_step"], scaling="strong",
                    dtype=p["dtype"], config=p["config"], gflops=p["gflops"], roofline=p["roofline"], e2e=p["e2e"],
-                   cpu_baseline=None)
+                   cpu_baseline=None, parity=p.get("parity"))
+        if p.get("parity"):
+            out["rel_err"] = p["parity"]["rel_err"]
+        out["secondary"] = {}
         if not args.no_secondary and args.workload != "ldoor":
             c3 = measure_sharded(args, "ldoor", dtype, world, rank, local, device, forward=True)
-            out["secondary"] = {"c3_ldoor": {k: c3[k] for k in ("value", "unit", "ms_per_step", "e2e",
-                                                                "forward_allreduce")}}
+            out["secondary"]["c3_ldoor"] = {k: c3.get(k) for k in ("value", "unit", "ms_per_step", "e2e",
+                                                                   "forward_allreduce", "parity")}
             out["secondary"]["c3_ldoor"]["workload"] = c3["config"]["workload"]
             out["secondary"]["c3_ldoor"]["roofline_frac_rank0"] = c3["roofline"]["frac"]
+        dist.barrier()  # every rank is done with its GPU before the one-process leg starts
         dist.destroy_process_group()
+        if rank == 0 and not args.no_abi_sharded:
+            out["secondary"]["abi_sharded"] = run_abi_sharded(args, world)
     if rank == 0:
         print(json.dumps(out), flush=True)
 

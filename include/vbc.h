@@ -71,11 +71,15 @@ typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
                                       SparseMatrixVBC; runs of rows with identical stripe lists of a
                                       1DVBC, <= 16) as stripes, every tile column a stored row -- so the
                                       matrix is read once for all right-hand sides. */
-#define VBC_CREATE_SERIAL 0x8u     /* keep the reference's serial per-stripe summation order in every
-                                      B'x layout (multiply_1DVBC.jl:101-104): no split planar product
-                                      (vbc_info.planar_split stays 1), so every output is bit-identical
-                                      to the oracle whatever the matrix size.  Default: small matrices
-                                      may fold a chunk's rows in P slices (rounding differs ~1 ulp). */
+#define VBC_CREATE_SERIAL 0x8u     /* keep the reference's serial summation order in every layout of
+                                      both directions: no split planar B'x product (per-stripe row
+                                      order, multiply_1DVBC.jl:101-104; vbc_info.planar_split stays 1)
+                                      and no split forward product (stripe order per output row,
+                                      :62-71; planar_mask bit 3 stays clear), so every output is
+                                      bit-identical to the oracle whatever the matrix size.  Default:
+                                      small matrices may fold a chunk's rows (B'x) or blocks (B·x) in
+                                      P slices whose partial sums meet in LDS (rounding differs ~1 ulp);
+                                      vbc_info reports it as planar_split > 1 / planar_mask bit 3. */
 
 /* mul flags */
 #define VBC_MAT_ROWMAJOR 0x2u         /* vbc_mul_mat: X, Y row-major (right-hand sides interleaved,
@@ -203,6 +207,11 @@ VBC_API int vbc_mul_mat_ex(vbc_handle *h, int trans, int64_t nrhs, const void *X
  *     root (disjoint; each stripe summed in stored row order, bit-identical to one GPU and to the
  *     reference, unless a shard's layout runs the split planar product -- vbc_info.planar_split > 1,
  *     small shards only -- which sums a chunk's rows in P slices; VBC_CREATE_SERIAL forbids it).
+ *     The disjoint B·x slices of VBC_SPLIT_ROWS keep each output row's stripe order
+ *     (multiply_1DVBC.jl:62-71) but a shard may run another forward kernel family than the whole
+ *     matrix (vbc_info fwd_run / planar_mask bits 1, 3, 4 / slot_bins): the slotted and planar forward
+ *     kernels associate a block's w-term dot product differently (~1 ulp), and a small shard may run
+ *     the split forward product (planar_mask bit 3), which VBC_CREATE_SERIAL forbids.
  *     Bx: x slices scattered, ncclReduce(sum) of y.
  *   VBC_SPLIT_ROWS: GPU g owns the stored rows [r_g, r_g+1) of every stripe.  Bx: x broadcast, y slices
  *     gathered (disjoint).  B'x: x slices, ncclReduce(sum) of y.

@@ -57,6 +57,19 @@ VBC_API int vbcx_partition_dynamic_table(int64_t m, int64_t n, const int64_t *co
                                          int64_t W, const double *alpha, const double *beta, int64_t *spl,
                                          int64_t *L);
 
+/* DynamicTotalChunker over a BlockComponentCostModel (costs.jl:138-142, the SparseMatrixVBC models):
+ * the columns of A are partitioned while its rows are grouped into G block rows (grp[i] = 1-based
+ * block row of row i, the other dimension's partition; NULL = every row its own group, G = m):
+ *     cost(stripe of width w) = alpha[w-1] + Σ_r colw[r·W + w-1] · Σ_{block rows g it touches} gw[r·G + g]
+ * i.e. the stripe's own cost plus, for every u_g × w block it stores, Σ_r β_row[r](u_g)·β_col[r](w)
+ * (gw = β_row[r] evaluated at each group's height, colw = β_col[r] at each width; R <= 64 components,
+ * the rank of the time model's SVD).  The row partition of pack_plaid's alternation is this call on
+ * Aᵀ with the permuted model (permutedims swaps the row and column terms).  Optimal by dynamic
+ * programming, width <= W. */
+VBC_API int vbcx_partition_block(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval,
+                                 const int64_t *grp, int64_t G, int64_t R, const double *gw, int64_t W,
+                                 const double *alpha, const double *colw, int64_t *spl, int64_t *L);
+
 /* SparseMatrix1DVBC{W}(A, Φ) (constructors_1DVBC.jl:9-92): pass 1 fills pos[L+1], ofs[L+1]. */
 VBC_API int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
                      const int64_t *spl, int64_t *pos, int64_t *ofs);

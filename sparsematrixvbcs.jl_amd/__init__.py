@@ -10,11 +10,12 @@ from ._lib import ArgumentError, DimensionMismatch, HIPError, UnsupportedDtype
 from .matrices import (DEFAULT_SIMD_SIZE, Adjoint, SparseMatrix1DVBC, SparseMatrixCSC, SparseMatrixVBC,
                        Transpose, adjoint, transpose)
 from .multiply import TrSpMV_, matmul, mul_, mulmat_
-from .costs import TimedChunker, model_SparseMatrix1DVBC_TrSpMV_time
-from .partition import (AlternatePacker, AlternatingPacker, ColumnBlockCostModel, ConstrainedCost, DynamicTotalChunker,
-                        EquiChunker, OverlapChunker, SplitPartition, StrictChunker, VertexCount,
-                        model_SparseMatrix1DVBC_blocks, model_SparseMatrix1DVBC_memory, pack_plaid,
-                        pack_stripe)
+from .costs import TimedChunker, model_SparseMatrix1DVBC_TrSpMV_time, model_SparseMatrixVBC_TrSpMV_time
+from .partition import (AlternatePacker, AlternatingPacker, BlockComponentCostModel, ColumnBlockCostModel,
+                        ConstrainedCost, DynamicTotalChunker, EquiChunker, Line, OverlapChunker, SplitPartition,
+                        StrictChunker, VertexCount, model_SparseMatrix1DVBC_blocks, model_SparseMatrix1DVBC_memory,
+                        model_SparseMatrixVBC_blocks, model_SparseMatrixVBC_memory, pack_plaid, pack_stripe,
+                        permutedims, total_value_2d)
 
 # Julia spellings
 globals()["mul!"] = mul_
@@ -26,6 +27,8 @@ __all__ = [
     "StrictChunker", "OverlapChunker", "DynamicTotalChunker", "ConstrainedCost", "VertexCount",
     "AlternatingPacker", "AlternatePacker", "pack_stripe", "pack_plaid",
     "model_SparseMatrix1DVBC_blocks", "model_SparseMatrix1DVBC_memory", "model_SparseMatrix1DVBC_TrSpMV_time", "TimedChunker",
-    "ColumnBlockCostModel", "DimensionMismatch",
+    "ColumnBlockCostModel", "BlockComponentCostModel", "Line", "permutedims", "total_value_2d",
+    "model_SparseMatrixVBC_blocks", "model_SparseMatrixVBC_memory", "model_SparseMatrixVBC_TrSpMV_time",
+    "DimensionMismatch",
     "ArgumentError", "HIPError", "UnsupportedDtype", "DEFAULT_SIMD_SIZE",
 ]

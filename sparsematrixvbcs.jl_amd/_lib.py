@@ -32,7 +32,7 @@ ABI_SYMBOLS = (
     "vbc1d_create_sharded", "vbc2d_create_sharded", "vbc_sharded_mul", "vbc_sharded_mul_ex", "vbc_sharded_destroy",
     "vbc_sharded_count", "vbc_sharded_shard",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
-    "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
+    "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_partition_block", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
     "vbcx_vbc_fill", "vbcx_transpose_pattern",
 )
 
@@ -125,6 +125,7 @@ def lib():
         L.vbcx_partition_overlap.argtypes = [I64, I64, P, P, D, I64, P, P]
         L.vbcx_partition_dynamic.argtypes = [I64, I64, P, P, I64, D, D, D, D, D, P, P]
         L.vbcx_partition_dynamic_table.argtypes = [I64, I64, P, P, I64, P, P, P, P]
+        L.vbcx_partition_block.argtypes = [I64, I64, P, P, P, I64, I64, P, I64, P, P, P, P]
         L.vbcx_1dvbc_count.argtypes = [I64, I64, P, P, I64, P, P, P]
         L.vbcx_1dvbc_fill.argtypes = [I64, I64, I64, P, P, P, INT, I64, P, P, P, P, P, I64]
         L.vbcx_vbc_count.argtypes = [I64, I64, P, P, I64, P, I64, P, P, P]

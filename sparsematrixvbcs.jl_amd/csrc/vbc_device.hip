@@ -1693,9 +1693,25 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
             const int64_t row = at[b.g]++;
             c.rows[row] = (int32_t)(s.col0[l] + cc);
             char *dst = cv.data() + (c.voff[b.g] + (row - c.rbeg[b.g]) * u) * esz;
-            for (int64_t q = b.q0; q < s.rbeg[l + 1] && gof[s.rows[q]] == b.g; q++)
-                std::memcpy(dst + (s.rows[q] - a[b.g]) * esz, val + (s.voff[l] + (q - s.rbeg[l]) * wl + cc) * esz,
-                            (size_t)esz);
+            // a stripe that stores one row twice (hand-built input; the reference's constructors never do)
+            // contributes both copies: they are added into the slot, not overwritten
+            for (int64_t q = b.q0; q < s.rbeg[l + 1] && gof[s.rows[q]] == b.g; q++) {
+                char *d = dst + (s.rows[q] - a[b.g]) * esz;
+                const char *v = val + (s.voff[l] + (q - s.rbeg[l]) * wl + cc) * esz;
+                if (esz == 8) {
+                    double t, u2;
+                    std::memcpy(&t, d, 8);
+                    std::memcpy(&u2, v, 8);
+                    t += u2;
+                    std::memcpy(d, &t, 8);
+                } else {
+                    float t, u2;
+                    std::memcpy(&t, d, 4);
+                    std::memcpy(&u2, v, 4);
+                    t += u2;
+                    std::memcpy(d, &t, 4);
+                }
+            }
         }
     }
     int32_t widest = 0;

@@ -314,6 +314,46 @@ int vbcx_partition_dynamic_table(int64_t m, int64_t n, const int64_t *colptr, co
     return VBC_OK;
 }
 
+int vbcx_partition_block(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, const int64_t *grp,
+                         int64_t G, int64_t R, const double *gw, int64_t W, const double *alpha, const double *colw,
+                         int64_t *spl, int64_t *L)
+{
+    if (int st = check_csc(m, n, colptr, rowval)) return st;
+    if (W < 1 || R < 1 || R > 64 || !gw || !alpha || !colw)
+        return fail(VBC_INVALID_ARG, "block cost model: need W > 0, 1 <= R <= 64 components and their tables");
+    if (!grp && G != m) return fail(VBC_INVALID_ARG, "without a row grouping every row is its own group (G == m)");
+    if (grp)
+        for (int64_t i = 0; i < m; i++)
+            if (grp[i] < 1 || grp[i] > G) return fail(VBC_INVALID_ARG, "row group id out of 1..G");
+    const double inf = std::numeric_limits<double>::infinity();
+    std::vector<double> f(n + 1, inf), S(R);
+    std::vector<int64_t> back(n + 1, 0), stamp(std::max<int64_t>(G, 1), -1);
+    f[0] = 0.0;
+    for (int64_t e = 1; e <= n; e++) {
+        std::fill(S.begin(), S.end(), 0.0);
+        for (int64_t w = 1; w <= W && w <= e; w++) {
+            const int64_t j = e - w;  // add column j (0-based) to the stripe [j, e)
+            for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; p++) {
+                const int64_t g = grp ? grp[rowval[p] - 1] - 1 : rowval[p] - 1;
+                if (stamp[g] != e) {  // a block row the stripe did not touch yet: one more u x w block
+                    stamp[g] = e;
+                    for (int64_t r = 0; r < R; r++) S[r] += gw[r * G + g];
+                }
+            }
+            double c = alpha[w - 1];
+            for (int64_t r = 0; r < R; r++) c += colw[r * W + w - 1] * S[r];
+            if (f[j] + c < f[e]) { f[e] = f[j] + c; back[e] = j; }
+        }
+    }
+    std::vector<int64_t> cuts;
+    for (int64_t e = n; e > 0; e = back[e]) cuts.push_back(back[e]);
+    int64_t l = 0;
+    for (auto it = cuts.rbegin(); it != cuts.rend(); ++it) spl[l++] = *it + 1;
+    spl[l] = n + 1;
+    *L = l;
+    return VBC_OK;
+}
+
 int vbcx_1dvbc_count(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowval, int64_t L,
                      const int64_t *spl, int64_t *pos, int64_t *ofs)
 {

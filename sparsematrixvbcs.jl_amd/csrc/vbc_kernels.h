@@ -404,7 +404,11 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     };
     // Stage 2: the x gathers of a tile whose keys have arrived (kind 0: one x per entry).
     constexpr int XV = KIND == 0 ? 1 : V;
-    auto gather = [&](int t, const uint32_t (&kk)[K], T (&xv)[K][XV]) {
+    // `ok` = the tile lies inside the range (wave-uniform).  A tile past the range is gathered at x[0]
+    // and reduced as a tile of zeros without HEADs -- a no-op on every output and on the carried sum --
+    // so the pipelined loops below have one exit and straight-line bodies: no branch around a stage,
+    // hence no vmcnt(0) drain at the loop header (the slotted kernels' rule).
+    auto gather = [&](int t, const uint32_t (&kk)[K], T (&xv)[K][XV], bool ok = true) {
         (void)t;
         if constexpr (DIAG == 2) {
 #pragma unroll
@@ -414,7 +418,7 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         } else {
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                const uint32_t gi = kk[k] & ~kHead;
+                const uint32_t gi = ok ? kk[k] & ~kHead : 0u;
                 if constexpr (KIND == 0) {
                     xv[k][0] = xg_[gi];
                 } else {
@@ -426,7 +430,17 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
     };
     T diag_acc = T(0);
     // Stage 3: segmented reduction of a tile.
-    auto compute = [&](const uint32_t (&kk)[K], const T (&v)[K][V], const T (&xv)[K][XV]) {
+    auto compute = [&](const uint32_t (&kk0)[K], const T (&v0)[K][V], const T (&xv0)[K][XV], bool ok = true) {
+        uint32_t kk[K];
+        T v[K][V], xv[K][XV];
+#pragma unroll
+        for (int k = 0; k < K; k++) {  // selects, not a branch (see gather)
+            kk[k] = ok ? kk0[k] : 0u;
+#pragma unroll
+            for (int e = 0; e < V; e++) v[k][e] = ok ? v0[k][e] : T(0);
+#pragma unroll
+            for (int e = 0; e < XV; e++) xv[k][e] = ok ? xv0[k][e] : T(0);
+        }
         if constexpr (DIAG == 1) {
 #pragma unroll
             for (int k = 0; k < K; k++)
@@ -580,13 +594,13 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         T vA[K][V], vB[K][V], xv[K][XV];
         load_stream(t0, kA, vA);
         for (int t = t0; t < t1; t += 2) {
+            const bool ok1 = t + 1 < t1;
             gather(t, kA, xv);
             load_stream(t + 1, kB, vB);
             compute(kA, vA, xv);
-            if (t + 1 >= t1) break;
-            gather(t + 1, kB, xv);
+            gather(t + 1, kB, xv, ok1);
             load_stream(t + 2, kA, vA);
-            compute(kB, vB, xv);
+            compute(kB, vB, xv, ok1);
         }
     } else {
         // Three stages, rotating buffers: in step t the stream loads of tile t+2 and the gathers of
@@ -598,17 +612,16 @@ __device__ __forceinline__ void run_range(const Bin &b, int r, int lane, const T
         gather(t0, k0, x0);
         load_stream(t0 + 1, k1, v1);
         for (int t = t0; t < t1; t += 3) {
-            gather(t + 1, k1, x1);
+            const bool ok1 = t + 1 < t1, ok2 = t + 2 < t1, ok3 = t + 3 < t1;
+            gather(t + 1, k1, x1, ok1);
             load_stream(t + 2, k2, v2);
             compute(k0, v0, x0);
-            if (t + 1 >= t1) break;
-            gather(t + 2, k2, x2);
+            gather(t + 2, k2, x2, ok2);
             load_stream(t + 3, k0, v0);
-            compute(k1, v1, x1);
-            if (t + 2 >= t1) break;
-            gather(t + 3, k0, x0);
+            compute(k1, v1, x1, ok1);
+            gather(t + 3, k0, x0, ok3);
             load_stream(t + 4, k1, v1);
-            compute(k2, v2, x2);
+            compute(k2, v2, x2, ok2);
         }
     }
     if constexpr (DIAG == 1) {

@@ -147,8 +147,29 @@ static int launch(const vbc_handle *h, const Launch &L, int kind, const void *x,
     // side stream (g - 1) % nside; every side stream that ran a group is joined back.  The event
     // sequence is serialised per handle (products on several caller streams at once).
     std::lock_guard<std::mutex> lk(const_cast<vbc_handle *>(h)->fork_mu);
-    VBC_HIP(hipEventRecord(L.fork_events[0], stream));
     const int used = std::min(nside, G - 1);
+    // A fork pulls the side streams into the caller's graph capture until that capture ends.  A product
+    // whose caller stream is in another capture state than a side stream (an eager product while a
+    // capture on another stream holds them, or a capture of a second graph) must not queue work there:
+    // it runs its groups one after another on its own stream instead (same results, no fork).
+    {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        unsigned long long cid = 0;
+        bool same = hipStreamGetCaptureInfo(stream, &cs, &cid) == hipSuccess &&
+                    cs != hipStreamCaptureStatusInvalidated;
+        for (int i = 0; i < used && same; i++) {
+            hipStreamCaptureStatus ss = hipStreamCaptureStatusNone;
+            unsigned long long sid = 0;
+            same = hipStreamGetCaptureInfo(L.fork_streams[i], &ss, &sid) == hipSuccess &&
+                   (ss == hipStreamCaptureStatusNone || (ss == hipStreamCaptureStatusActive &&
+                                                         cs == hipStreamCaptureStatusActive && sid == cid));
+        }
+        if (!same) {
+            (void)hipGetLastError();  // a refused query leaves no sticky error behind
+            return launch_group<T>(L, kind, x, y, alpha, beta, rd, stream, h->xcd, h->slot_stage, -1);
+        }
+    }
+    VBC_HIP(hipEventRecord(L.fork_events[0], stream));
     for (int i = 0; i < used; i++) VBC_HIP(hipStreamWaitEvent(L.fork_streams[i], L.fork_events[0], 0));
     int st = VBC_OK;
     for (int g = 0; g < G && st == VBC_OK; g++)

@@ -134,18 +134,36 @@ class ShardedSparseMatrix1DVBC:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 
-    def gather(self, y_local):
+    def _gather_bufs(self, dtype, dev):
+        """The padded send slice and the world x max-slice receive buffer of `gather`, allocated once
+        per (eltype, device) and reused by every later call (no allocation in a solver's loop)."""
+        import torch
+        key = (dtype, str(dev))
+        bufs = getattr(self, "_gbufs", None)
+        if bufs is None:
+            bufs = self._gbufs = {}
+        if key not in bufs:
+            ms = max(self.splits[r + 1] - self.splits[r] for r in range(self.world))
+            bufs[key] = (torch.zeros(ms, dtype=dtype, device=dev), torch.empty(self.world * ms, dtype=dtype, device=dev))
+        return bufs[key]
+
+    def gather(self, y_local, out=None):
         """Replicated vector from every rank's slice of the split dimension: one all_gather of
-        equal-length padded slices."""
+        equal-length padded slices into a preallocated buffer; written into `out` when given (the
+        product loop then allocates nothing), else into a new tensor."""
         import torch
         import torch.distributed as dist
         sizes = [self.splits[r + 1] - self.splits[r] for r in range(self.world)]
-        dev = "cpu" if self.comm == "cpu" else y_local.device
-        buf = torch.zeros(max(sizes), dtype=y_local.dtype, device=dev)
-        buf[:len(y_local)] = y_local.to(dev)
-        outs = [torch.empty_like(buf) for _ in range(self.world)]
-        dist.all_gather(outs, buf, group=self.group)
-        return torch.cat([o[:s] for o, s in zip(outs, sizes)]).to(y_local.device)
+        dev = torch.device("cpu") if self.comm == "cpu" else y_local.device
+        buf, flat = self._gather_bufs(y_local.dtype, dev)
+        buf[:len(y_local)].copy_(y_local)
+        dist.all_gather_into_tensor(flat, buf, group=self.group)
+        if out is None:
+            out = torch.empty(self.splits[-1] - self.splits[0], dtype=y_local.dtype, device=y_local.device)
+        ms = buf.shape[0]
+        for r, s in enumerate(sizes):
+            out[self.splits[r] - self.splits[0]:self.splits[r] - self.splits[0] + s].copy_(flat[r * ms:r * ms + s])
+        return out
 
     # --- mul!(y, B', x) ---------------------------------------------------------------------------
     def local_mul_t(self, y_local, x, alpha=1.0, beta=0.0):
@@ -161,8 +179,7 @@ class ShardedSparseMatrix1DVBC:
         if self.split == "stripes":
             part = y[self.col0:self.col0 + self.n_local].clone()
             self.local_mul_t(part, x, alpha, beta)
-            y.copy_(self.gather(part))
-            return y
+            return self.gather(part, out=y)
         self.local_mul_t(y, x, alpha, beta)
         return self._all_reduce(y)
 
@@ -180,8 +197,7 @@ class ShardedSparseMatrix1DVBC:
         if self.split == "rows":
             part = y[self.row0:self.row0 + self.m_local].clone()
             self.local_mul(part, x, alpha, beta)
-            y.copy_(self.gather(part))
-            return y
+            return self.gather(part, out=y)
         self.local_mul(y, x, alpha, beta)
         return self._all_reduce(y)
 
@@ -252,6 +268,17 @@ class MultiGPUSparseMatrix1DVBC:
             _L.check(_L.lib().vbc_sharded_shard(self._h, g, None, C.byref(lo), C.byref(hi), C.byref(dev)), "shard")
             out.append((lo.value, hi.value, dev.value))
         return out
+
+    def shard_info(self, g):
+        """vbc_get_info of shard g's single-GPU handle (its layouts: planar_split, planar_mask, ...)."""
+        import ctypes as C
+        from . import _lib as _L
+        h = C.c_void_p()
+        lo, hi, dev = C.c_int64(), C.c_int64(), C.c_int()
+        _L.check(_L.lib().vbc_sharded_shard(self._h, g, C.byref(h), C.byref(lo), C.byref(hi), C.byref(dev)), "shard")
+        inf = _L.vbc_info()
+        _L.check(_L.lib().vbc_get_info(h, C.byref(inf)), "info")
+        return {f: getattr(inf, f) for f, _ in _L.vbc_info._fields_}
 
     def _mul(self, y, x, trans, alpha, beta, stream, quirks):
         from . import _lib as _L

@@ -96,10 +96,12 @@ def cached_build(builder, path):
 
 
 def memory_bytes(B, ti=8):
-    """The reference's `mem` column (bin/test_table.jl:80,122): sizeof(B.Φ) + [sizeof(B.Π)] + sizeof of
-    pos, idx, ofs, val.  Φ / Π are SplitPartition structs holding one array reference, so Julia's
-    sizeof counts 8 bytes for each, not the spl arrays; index arrays are Ti (Int64 in the reference)."""
-    n = 8 + ti * (len(B.pos) + len(B.idx) + len(B.ofs)) + B.val.nbytes
+    """The reference's `mem` column (bin/test_table.jl:78,120): sizeof(B.Φ) + [sizeof(B.Π)] + sizeof of
+    pos, idx, ofs, val, index arrays of Ti (Int64 in the reference).  The partitions count their spl
+    arrays (Ti·(L+1), Ti·(K+1)): that is what reproduces src/ref.out exactly -- thermal1's
+    StrictChunker(8) row, 11,175,112 B = 24·(L+1) + 8·q + 8·|val| with L = n, q = nnz and the 8-value
+    SIMD tail pad (ref.out:123; tests/test_io_costs.py pins it)."""
+    n = ti * (len(B.Phi.spl) + len(B.pos) + len(B.idx) + len(B.ofs)) + B.val.nbytes
     if isinstance(B, SparseMatrixVBC):
-        n += 8
+        n += ti * len(B.Pi.spl)
     return n

@@ -12,8 +12,9 @@ import numpy as np
 import scipy.sparse as sp
 
 from . import _lib as _L
-from .partition import (DynamicTotalChunker, SplitPartition, model_SparseMatrix1DVBC_memory,
-                        pack_plaid, pack_stripe, AlternatingPacker, EquiChunker)
+from .partition import (AlternatingPacker, ConstrainedCost, DynamicTotalChunker, EquiChunker, SplitPartition,
+                        VertexCount, model_SparseMatrix1DVBC_memory, model_SparseMatrixVBC_memory, pack_plaid,
+                        pack_stripe, permutedims)
 
 DEFAULT_SIMD_SIZE = 64  # CpuId.simdbytes() on the AVX-512 hosts the reference was run on
 
@@ -128,7 +129,7 @@ class SparseMatrix1DVBC(_DeviceMatrix):
     """SparseMatrix1DVBC{W,Tv,Ti} (SparseMatrixVBCs.jl:36-53).
 
     Construct like the reference:
-        SparseMatrix1DVBC[W](A)                 default partitioner (constructors_1DVBC.jl:1-7)
+        SparseMatrix1DVBC[W](A)                 default: min memory for its Tv (constructors_1DVBC.jl:1-7)
         SparseMatrix1DVBC[W](A, method)         pack_stripe(A, method)
         SparseMatrix1DVBC[W](A, Φ)              given SplitPartition (constructors_1DVBC.jl:9)
         SparseMatrix1DVBC(W, m, n, Φ, pos, idx, ofs, val)   inner constructor (:44)
@@ -156,10 +157,11 @@ class SparseMatrix1DVBC(_DeviceMatrix):
 
     @classmethod
     def from_csc(cls, W, A, method=None, dtype=None):
-        if method is None:
-            method = DynamicTotalChunker(model_SparseMatrix1DVBC_memory(np.float64, np.int64), W)
         from .partition import CSCFields
         A = CSCFields(A)  # one conversion for the partitioner and the builder
+        if method is None:  # constructors_1DVBC.jl:1-2: the memory model of the matrix's own Tv (Ti = Int64)
+            Tv = dtype if dtype is not None else _value_dtype(A.A)
+            method = DynamicTotalChunker(model_SparseMatrix1DVBC_memory(Tv, np.int64), W)
         Phi = method if isinstance(method, SplitPartition) else pack_stripe(A, method)
         (m, n), colptr, rowval, nzval = _csc_fields(A)
         if dtype is not None:
@@ -191,10 +193,21 @@ class SparseMatrix1DVBC(_DeviceMatrix):
                 f"{len(self.Phi)} stripes, {len(self.idx)} row-blocks)")
 
 
+def default_partitioner_vbc(U, W, Tv, Ti=np.int64):
+    """default_partitioner(SparseMatrixVBC{U,W,Tv,Ti}) (constructors_VBC.jl:1-8): the 5-phase
+    AlternatePacker -- unit columns, unit rows, then the 2D memory model (costs.jl:140) on the
+    columns (width <= W), its permutation on the rows (height <= U) and again on the columns."""
+    mdl = model_SparseMatrixVBC_memory(Tv, Ti)
+    return AlternatingPacker(EquiChunker(1), EquiChunker(1),
+                             DynamicTotalChunker(ConstrainedCost(mdl, VertexCount(), W)),
+                             DynamicTotalChunker(ConstrainedCost(permutedims(mdl), VertexCount(), U)),
+                             DynamicTotalChunker(ConstrainedCost(mdl, VertexCount(), W)))
+
+
 class SparseMatrixVBC(_DeviceMatrix):
     """SparseMatrixVBC{U,W,Tv,Ti} (SparseMatrixVBCs.jl:62-82); idx holds block-row ids.
 
-        SparseMatrixVBC[U, W](A)            default packer (constructors_VBC.jl:1-8)
+        SparseMatrixVBC[U, W](A)            default 5-phase packer, 2D memory model (constructors_VBC.jl:1-8)
         SparseMatrixVBC[U, W](A, method)    pack_plaid(A, method)
         SparseMatrixVBC[U, W](A, Π, Φ)      given partitions (constructors_VBC.jl:15)
     """
@@ -230,7 +243,7 @@ class SparseMatrixVBC(_DeviceMatrix):
                 raise _L.ArgumentError("SparseMatrixVBC(A, Π, Φ) needs both partitions")
         else:
             if method is None:
-                method = AlternatingPacker(EquiChunker(1), EquiChunker(1))
+                method = default_partitioner_vbc(U, W, dtype if dtype is not None else _value_dtype(sp.csc_matrix(A)))
             Pi, Phi = pack_plaid(A, method)
         (m, n), colptr, rowval, nzval = _csc_fields(A)
         if dtype is not None:

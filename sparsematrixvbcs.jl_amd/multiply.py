@@ -161,17 +161,36 @@ def mulmat_(Y, A, X, alpha=1.0, beta=0.0, *, stream=None, quirks=False, engine="
     return Y
 
 
+def promote_op_matprod(ta, tx):
+    """Julia's promote_op(matprod, Ta, Tx) for the eltypes the kernels take (multiply_1DVBC.jl:182-183):
+    matprod(a, b) = a*b + a*b, so a float on either side gives the wider float (Julia's
+    promote_type(Float32, Int64) is Float32, unlike numpy's result_type), two integers the wider integer,
+    and Bool*Bool + Bool*Bool is an Int64."""
+    ta, tx = np.dtype(ta), np.dtype(tx)
+    floats = [t for t in (ta, tx) if t.kind == "f"]
+    if floats:
+        return max(floats, key=lambda t: t.itemsize)
+    ints = [t for t in (ta, tx) if t.kind in "iu"]
+    if not ints:  # Bool * Bool: the sum of two Bools is an Int
+        return np.dtype(np.int64)
+    return max(ints, key=lambda t: t.itemsize)
+
+
 def matmul(A, x):
-    """Base.:*(A, x): allocate y = similar(x, T, size(A, 1)) and mul!(y, A, x, true, false)."""
+    """Base.:*(A, x): y = similar(x, promote_op(matprod, eltype(A), eltype(x)), size(A, 1)), then
+    mul!(y, A, x, true, false) (multiply_1DVBC.jl:182-183, multiply_VBC.jl:194-195)."""
     m = A.shape[0]
+    B, _ = _unwrap(A)
     if _is_torch(x):
         import torch
-        y = torch.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)  # same layout as x
+        xt = np.dtype(str(x.dtype).replace("torch.", "").replace("bool", "bool_"))
+        T = getattr(torch, promote_op_matprod(B.dtype, xt).name)
+        y = torch.empty((m,) + tuple(x.shape[1:]), dtype=T, device=x.device)  # same layout as x
         if x.dim() == 2 and x.stride(0) == 1 and x.shape[1] > 1:
-            y = torch.empty((x.shape[1], m), dtype=x.dtype, device=x.device).T
+            y = torch.empty((x.shape[1], m), dtype=T, device=x.device).T
     else:
         order = "F" if (x.ndim == 2 and x.flags.f_contiguous and not x.flags.c_contiguous) else "C"
-        y = np.empty((m,) + tuple(x.shape[1:]), dtype=x.dtype, order=order)
+        y = np.empty((m,) + tuple(x.shape[1:]), dtype=promote_op_matprod(B.dtype, x.dtype), order=order)
     return mul_(y, A, x, True, False)
 
 

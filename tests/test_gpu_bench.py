@@ -30,10 +30,26 @@ def run_bench(*args, timeout=110):
 
 def test_bench_self_launches_two_ranks():
     d = run_bench("--gpus", "2", "--backend", "gloo", "--same-device", "--scale", "0.01", "--no-secondary",
-                  "--steps", "3", "--warmup", "1")
+                  "--no-abi-sharded", "--steps", "3", "--warmup", "1")
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["warmup"] == 1
     assert d["value"] > 0 and d["unit"] == "GB/s" and d["scaling"] == "strong"
     assert "stripe split x2" in d["config"]["parallelism"]
+    assert d["parity"]["pass"] and d["parity"]["serial_bitwise_equal"]
+
+
+def test_bench_multi_gpu_line_checks_itself():
+    """the N > 1 line proves its numbers: the primary's gathered y, the C3 secondary's B'x
+    and its forward all_reduce, and the one-process C-ABI sharded leg (vbc1d_create_sharded, devices
+    [0, 0] on a one-GPU box) are all compared with the oracle."""
+    d = run_bench("--gpus", "2", "--backend", "gloo", "--same-device", "--scale", "0.01", "--steps", "3",
+                  "--warmup", "1", timeout=300)
+    assert d["parity"]["pass"] and len(d["parity"]["slices_bitwise"]) == 2
+    c3 = d["secondary"]["c3_ldoor"]
+    assert c3["parity"]["pass"] and c3["forward_allreduce"]["parity"]["pass"]
+    abi = d["secondary"]["abi_sharded"]
+    assert abi["pass"] and abi["devices"] == [0, 0], abi
+    for k in ("transposed", "forward"):
+        assert abi[k]["parity"]["pass"] and abi[k]["value"] > 0
 
 
 def test_bench_single_gpu_line():

@@ -190,3 +190,27 @@ def test_concurrent_products_on_two_streams(monkeypatch, layout):
     torch.cuda.synchronize()
     for a, b in zip(outs, serial):
         assert torch.equal(a, b)
+
+
+def test_star_promotes_eltype_like_promote_op_matprod():
+    """Base.:*(A, x) allocates y of promote_op(matprod, eltype(A), eltype(x)) (multiply_1DVBC.jl:182-183):
+    a Float64 matrix times a Float32 x returns a Float64 y computed in Float64 (the oracle at 1e-12);
+    a Float32 matrix times a Float64 x, too; an Int32 matrix times a Float32 x returns Float32."""
+    rng = np.random.default_rng(11)
+    A = sp.random(300, 200, 0.05, format="csc", random_state=5)
+    B = V.SparseMatrix1DVBC[4](A, V.StrictChunker(4))
+    for trans in (True, False):
+        nx = B.m if trans else B.n
+        x32 = rng.uniform(-1, 1, nx).astype(np.float32)
+        op = B.T if trans else B
+        y = op @ dev(x32)
+        assert y.dtype == torch.float64
+        R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+        ref = O.mul(R, x32.astype(np.float64), np.zeros(B.n if trans else B.m), trans=trans)
+        assert np.linalg.norm(y.cpu().numpy() - ref) <= 1e-12 * np.linalg.norm(ref)
+        yh = op @ x32  # host operands take the same rule
+        assert yh.dtype == np.float64 and np.linalg.norm(yh - ref) <= 1e-12 * np.linalg.norm(ref)
+    B32 = V.SparseMatrix1DVBC[4](A.astype(np.float32), V.StrictChunker(4))
+    assert (B32.T @ dev(rng.uniform(-1, 1, B32.m))).dtype == torch.float64
+    Bi = V.SparseMatrix1DVBC[4](int_matrix(40, 30, "i32", rng), V.StrictChunker(4))
+    assert (Bi.T @ dev(rng.uniform(-1, 1, 40).astype(np.float32))).dtype == torch.float32

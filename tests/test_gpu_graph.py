@@ -111,3 +111,18 @@ def test_forked_groups_bitwise_eager_graph_and_two_streams(monkeypatch):
             V.mul_(yb, Bf.T, xb)
     torch.cuda.synchronize()
     assert torch.equal(ya, ys) and torch.equal(yb, ys2)
+    # an eager product on a second stream while a capture on the first holds the side streams: it must
+    # not queue work on them (it runs its groups on its own stream), and both results stay exact
+    s3 = torch.cuda.Stream()
+    ye = torch.full((B0.n,), float("nan"), dtype=torch.float64, device="cuda")
+    yc = torch.full((B0.n,), float("nan"), dtype=torch.float64, device="cuda")
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=s, capture_error_mode="relaxed"):
+        V.mul_(yc, Bf.T, x)
+        with torch.cuda.stream(s3):
+            V.mul_(ye, Bf.T, x2)
+    torch.cuda.synchronize()
+    assert torch.equal(ye, ys2)
+    g2.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(yc, ys)

@@ -118,3 +118,24 @@ def test_forward_nonfinite_x():
     fin = np.isfinite(ref)
     assert np.array_equal(np.isinf(got), np.isinf(ref))
     assert rel(got[fin], ref[fin]) <= TOL64
+
+
+def test_forward_duplicate_row_in_stripe_adds_both():
+    """A hand-built 1DVBC whose stripe stores one row twice (the reference's constructors never do, but
+    its forward loop y[idx[Q]] += ... takes both, multiply_1DVBC.jl:33-36): the forward panel layout
+    must add the two copies, not keep the last one."""
+    W = 4
+    spl = np.array([1, 3, 5], np.int64)            # two stripes of width 2
+    pos = np.array([1, 4, 6], np.int64)            # stripe 1: rows 2, 2, 5; stripe 2: rows 1, 5
+    idx = np.array([2, 2, 5, 1, 5], np.int64)
+    ofs = np.array([1, 7, 11], np.int64)
+    val = np.zeros(10 + 8)
+    val[:10] = np.random.default_rng(4).uniform(-1, 1, 10)
+    B = V.SparseMatrix1DVBC(W, 6, 4, V.SplitPartition(spl), pos, idx, ofs, val)
+    R = ref_1d(B)
+    X = np.random.default_rng(5).uniform(-1, 1, (4, 16))
+    ref = ref_cols_fwd(R, X, np.zeros((6, 16)), 1.0, 0.0)
+    for layout in ("R", "C"):
+        Y = as_dev(np.zeros((6, 16)), layout)
+        V.mul_(Y, B, as_dev(X, layout), engine="mfma")
+        assert rel(Y.cpu().numpy(), ref) <= TOL64, layout

@@ -245,8 +245,8 @@ def test_sharded_serial_flag_bit_identical_on_split_product_sizes():
     """a small stripe shard may choose the split planar product (P slices per chunk) while
     the whole matrix does not.  With serial=True (VBC_CREATE_SERIAL) every shard keeps the
     reference's serial per-stripe order: the stripe-sharded B'x equals the single-GPU product and
-    the oracle bit for bit on the ct20stif stand-in, whose own default layout splits."""
-    A = V.synthetic.standin("Boeing/ct20stif", dtype=np.float64, seed=5)
+    the oracle bit for bit on a 3-dof stiffness matrix of ct20stif's size, whose default layout splits."""
+    A = V.synthetic.fe_stiffness_3d(52329, 2600295, 3, np.float64, seed=5)  # one-width 3-dof (rounds 1-3 stand-in)
     B = V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
     assert B.info(0, True)["planar_split"] > 1  # the default layout folds chunks in slices
     B.release()
@@ -289,3 +289,41 @@ def test_sharded_distinct_devices_rccl(mat, split):
         if (split == "stripes") == trans:  # disjoint slices: the single-GPU result bit for bit
             assert torch.equal(y, y1)
     S.release()
+
+
+def test_sharded_serial_flag_forward_rows():
+    """the forward counterpart.  Small forward layouts run the split forward product by
+    default (P waves per chunk, partial sums meeting in LDS: vbc_info planar_mask bit 3); serial=True
+    (VBC_CREATE_SERIAL) turns it off in every shard too, so each output row sums its blocks in the
+    reference's stripe order (multiply_1DVBC.jl:62-71).  The row-sharded B·x -- disjoint y slices --
+    matches the oracle, and equals the single-GPU serial product bit for bit wherever a shard runs the
+    same forward kernel family (the slotted and planar forward kernels associate a block's w-term dot
+    product differently, vbc.h VBC_SPLIT_ROWS note)."""
+    A = V.synthetic.fe_stiffness_3d(52329, 2600295, 3, np.float64, seed=5)  # one-width 3-dof (rounds 1-3 stand-in)
+    B = V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
+    assert B.info(0, False)["planar_mask"] & 8  # the default forward layout splits chunks
+    B.release()
+    B.serial = True
+    whole = B.info(0, False)
+    assert not whole["planar_mask"] & 8
+    x = np.random.default_rng(4).uniform(-1, 1, B.n)
+    y1 = dev(np.zeros(B.m))
+    V.mul_(y1, B, dev(x))
+    ref = O.mul(ref_of(B), x, np.zeros(B.m), trans=False)
+    assert rel(y1.cpu().numpy(), ref) <= TOL64
+    fam = lambda inf: (inf["fwd_run"], inf["planar_mask"] & 0b11010, inf["slot_bins"] > 0, inf["bins_f"])
+    same_family_seen = False
+    for nsh in (2, 8):
+        S = D.MultiGPUSparseMatrix1DVBC(B, devices=[0] * nsh, split="rows", transposed=False, serial=True)
+        yk = dev(np.full(B.m, np.nan))
+        V.mul_(yk, S, dev(x))
+        assert rel(yk.cpu().numpy(), ref) <= TOL64
+        infos = [S.shard_info(g) for g in range(nsh)]
+        assert not any(i["planar_mask"] & 8 for i in infos)
+        for g, (lo, hi, _) in enumerate(S.shards()):
+            if fam(infos[g]) == fam(whole):
+                same_family_seen = True
+                assert torch.equal(y1[lo:hi], yk[lo:hi]), (nsh, g)
+        S.release()
+    assert same_family_seen
+    B.release()

@@ -93,7 +93,7 @@ def test_golden_random_vs_oracle(golden, alpha, beta):
         A = g["A"]
         m, n = A.shape
         for B in (V.SparseMatrix1DVBC[8](A, V.DynamicTotalChunker(V.model_SparseMatrix1DVBC_memory(), 8)),
-                  V.SparseMatrixVBC[3, 5](A, V.AlternatingPacker(V.EquiChunker(3), V.EquiChunker(5)))):
+                  V.SparseMatrixVBC[3, 5](A, V.AlternatingPacker(V.EquiChunker(5), V.EquiChunker(3)))):
             for trans, nx, ny in ((False, n, m), (True, m, n)):
                 x = rng.uniform(-1, 1, nx)
                 y0 = rng.uniform(-1, 1, ny)

@@ -117,3 +117,14 @@ def test_constructor_argument_errors():
         V.SparseMatrix1DVBC[2](A, V.SplitPartition([1, 5]))
     with pytest.raises(V.UnsupportedDtype):
         V.SparseMatrix1DVBC[2](sp.csc_matrix(np.ones((2, 2), dtype=np.complex128)), V.EquiChunker(1))
+
+
+def test_promote_op_matprod_follows_julia():
+    """promote_op(matprod, Ta, Tx) (multiply_1DVBC.jl:182-183): Julia's promotion, not numpy's --
+    Float32 with Int64 stays Float32, Bool*Bool sums to Int64."""
+    from sparsematrixvbcs_amd.multiply import promote_op_matprod as P
+    f64, f32, i64, i32, b = np.float64, np.float32, np.int64, np.int32, np.bool_
+    table = {(f64, f32): f64, (f32, f64): f64, (f32, f32): f32, (f32, i64): f32, (i64, f32): f32,
+             (i32, i64): i64, (i32, i32): i32, (b, b): i64, (b, i32): i32, (b, f32): f32, (i64, f64): f64}
+    for (a, x), want in table.items():
+        assert P(a, x) == np.dtype(want), (a, x)

@@ -107,7 +107,7 @@ def main():
         source = "SuiteSparse file"
     except FileNotFoundError:
         A = V.synthetic.standin(args.matrix)
-        source = "synthetic stand-in (synthetic.STANDINS: same n, nnz)"
+        source = "synthetic stand-in (synthetic.STANDINS / STANDIN_MODEL: same n, nnz; calibrated to src/ref.out)"
     A = A.T.tocsc().astype(dtype)  # permutedims(sparse(mdopen(mtx).A)), test_table.jl:27
     A.sort_indices()
     m, n = A.shape
@@ -120,7 +120,7 @@ def main():
     lim = lambda mdl: V.ConstrainedCost(mdl, V.VertexCount(), W)
     rows = []
 
-    def record(name, setup, mem, B=None, R=None, trsp=None):
+    def record(name, setup, mem, B=None, R=None, trsp=None, model_us=None):
         t_gpu = gpu_time(B, x, y, args.reps)
         err = float(np.linalg.norm(y.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref))
         t_cpu, th, t_cpu1, kind = cpu_time(R, xh, n, trsp=trsp, B=B)
@@ -128,7 +128,13 @@ def main():
         row = dict(method=name, setup_s=round(setup, 4), memory=int(mem), gpu_us=round(t_gpu * 1e6, 2),
                    cpu_us=round(t_cpu * 1e6, 1), cpu_threads=th, cpu_1core_us=round(t_cpu1 * 1e6, 1), cpu_kind=kind,
                    speedup=round(t_cpu / t_gpu, 1),
-                   gpu_GBs=round(bytes_ / t_gpu / 1e9, 1) if bytes_ else None, rel_err=err)
+                   gpu_GBs=round(bytes_ / t_gpu / 1e9, 1) if bytes_ else None, rel_err=err, model_us=model_us)
+        if hasattr(B, "Phi"):
+            wd = np.diff(B.Phi.spl)
+            row["widths"] = {int(k): int(v) for k, v in zip(*np.unique(wd, return_counts=True))}
+            if hasattr(B, "Pi"):
+                ud = np.diff(B.Pi.spl)
+                row["heights"] = {int(k): int(v) for k, v in zip(*np.unique(ud, return_counts=True))}
         rows.append(row)
         print(f"{name:22s} setup {setup:8.3f}s  mem {mem:12d}  gpu {t_gpu * 1e6:9.2f} us  cpu {t_cpu * 1e6:10.1f} us"
               f"  x{t_cpu / t_gpu:7.1f}  err {err:.1e}", flush=True)
@@ -156,17 +162,35 @@ def main():
         R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
         record(name, setup, V.io.memory_bytes(B), B, R)
     if not args.no_2d:
-        for name, method in [
+        b2, m2 = V.model_SparseMatrixVBC_blocks(), V.model_SparseMatrixVBC_memory(dtype, np.int64)
+        methods2 = [
                 ("1D 2D", V.AlternatingPacker(V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks())), V.EquiChunker(1))),
                 ("strict 2D", V.AlternatingPacker(V.StrictChunker(W), V.StrictChunker(W))),
                 ("overlap 2D 0.9", V.AlternatingPacker(V.OverlapChunker(0.9, W), V.OverlapChunker(0.9, W))),
                 ("overlap 2D 0.8", V.AlternatingPacker(V.OverlapChunker(0.8, W), V.OverlapChunker(0.8, W))),
-                ("overlap 2D 0.7", V.AlternatingPacker(V.OverlapChunker(0.7, W), V.OverlapChunker(0.7, W)))]:
+                ("overlap 2D 0.7", V.AlternatingPacker(V.OverlapChunker(0.7, W), V.OverlapChunker(0.7, W))),
+                # test_table.jl:94-111: the 2D block cost models, alternated over columns and rows
+                ("dynamic blocks 2D", V.AlternatingPacker(V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks())),
+                                                          V.DynamicTotalChunker(lim(V.permutedims(b2))),
+                                                          V.DynamicTotalChunker(lim(b2)))),
+                ("dynamic memory 2D", V.AlternatingPacker(V.EquiChunker(1), V.EquiChunker(1),
+                                                          V.DynamicTotalChunker(lim(m2)),
+                                                          V.DynamicTotalChunker(lim(V.permutedims(m2))),
+                                                          V.DynamicTotalChunker(lim(m2))))]
+        t2 = None
+        if args.fit_time_model:  # costs.jl:142 with R = 3 (test_table.jl:56), fitted on this GPU
+            t2 = V.model_SparseMatrixVBC_TrSpMV_time(3, W, W, dtype, np.int64, dtype)
+            methods2.append(("dynamic time 2D", V.AlternatingPacker(V.EquiChunker(1), V.EquiChunker(1),
+                                                                    V.DynamicTotalChunker(lim(t2)),
+                                                                    V.DynamicTotalChunker(lim(V.permutedims(t2))),
+                                                                    V.DynamicTotalChunker(lim(t2)))))
+        for name, method in methods2:
             t0 = time.perf_counter()
             B = V.SparseMatrixVBC[W, W](A, method)
             setup = time.perf_counter() - t0
             R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
-            record(name, setup, V.io.memory_bytes(B), B, R)
+            model = round(V.total_value_2d(B, t2) * 1e6, 2) if t2 is not None else None  # test_table.jl:124, us
+            record(name, setup, V.io.memory_bytes(B), B, R, model_us=model)
     out = dict(matrix=args.matrix, source=source, m=m, n=n, nnz=int(A.nnz), dtype=args.dtype, W=W,
                device=torch.cuda.get_device_name(0), rows=rows)
     if args.json:
