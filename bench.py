@@ -46,6 +46,8 @@ WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
              "fe3d": "FE-3D-stiffness-dof3-1e7x1e7-1e8nnz-w3 (irregular: random 18-neighbour subsets)",
              "c5": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS (costs.jl:200-220 generator)",
              "c5-fwd": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS forward Y = B*X (costs.jl:200-220 generator)",
+             "c5-mesh": "C5-VBC2D-3x3-node-tiles-2Mx2M-1e8nnz-16RHS (structured: 3D stiffness stand-in, "
+                        "AlternatingPacker(StrictChunker(8), StrictChunker(8)) tiles)",
              "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
              "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)",
              "ldoor-csc": "C4 TrSpMV!(y, A, x) on the GHS_psdef/ldoor stand-in (CSC, 952203^2, 42.5M nnz)"}
@@ -86,6 +88,8 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
         return V.synthetic.fe_stiffness_3d_1dvbc(n, int(round(1e8 * scale)), 3, dtype=dtype, seed=seed)
     if workload in ("c5", "c5-fwd"):
         return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
+    if workload == "c5-mesh":
+        return V.synthetic.c5_mesh(dtype=dtype, scale=scale, seed=seed)
     if workload in ("ldoor", "ct20stif", "ldoor-csc"):
         name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ldoor-csc": "GHS_psdef/ldoor"}[workload]
         try:
@@ -271,7 +275,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     B = build_matrix(workload, dtype, args.scale)
     csc = not hasattr(B, "ofs")
     rng = np.random.default_rng(0xC0FFEE)
-    k = args.nrhs if workload in ("c5", "c5-fwd") else 1
+    k = args.nrhs if workload in ("c5", "c5-fwd", "c5-mesh") else 1
     trans = workload != "c5-fwd"
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
     x_host = rng.uniform(-1, 1, (nx, k) if k > 1 else nx).astype(dtype)
@@ -332,6 +336,9 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
         },
         "dtype": "f64" if dtype == np.float64 else "f32",
     }
+    if traffic:  # the same launch time priced on the HBM bytes the PMC counters saw (the bytes moved)
+        out["roofline"]["achieved_traffic"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 1)
+        out["roofline"]["frac_traffic"] = round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if csc:
         out["roofline"]["bytes_csc_formula"] = bytes_launch
         out["csc_equivalent_GBs"] = round(bytes_launch * steps / elapsed / 1e9, 2)
@@ -677,7 +684,8 @@ def main():
         if not args.no_secondary:
             sec = {}
             for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("c5-fwd", np.float32),
-                           ("ct20stif", np.float64), ("ldoor", np.float64), ("ldoor-csc", np.float32)):
+                           ("c5-mesh", np.float32), ("ct20stif", np.float64), ("ldoor", np.float64),
+                           ("ldoor-csc", np.float32)):
                 if wl == args.workload:
                     continue
                 s = measure(args, wl, dt, device, local, with_cpu=False, with_parity=not args.no_parity)

@@ -295,7 +295,9 @@ typedef struct vbc_info {
                                length order (padding lanes fetch nothing); bit 2: a B'x planar bucket in
                                per-lane compacted streams (tiles of stripes dealt to the lanes); bit 3:
                                the forward planar bucket runs the split product (P waves per chunk);
-                               bit 4: the forward bucket in lane streams (node blocks transposed) */
+                               bit 4: the forward bucket in lane streams (node blocks transposed);
+                               bit 5: a small matrix's B'x buckets of every width (1..8) laid out planar
+                               and split, run by ONE fused launch (planar_split = its P) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

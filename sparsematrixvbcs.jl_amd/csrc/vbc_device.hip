@@ -245,6 +245,7 @@ static int slot_spl(const vbc_handle *h, int kind, int w)
 // fp32 w = 3 (12-B rows, no padding to 4).
 static bool slot_planar(const vbc_handle *h, int kind, int w)
 {
+    if (kind == 0 && h->small_split > 1 && w >= 1 && w <= 8) return true;  // fused small-matrix split (below)
     if (kind != 0 || h->slot_planar == 0 || w < 3 || w > 8) return false;
     return h->esz == 8 || w != 4;
 }
@@ -317,6 +318,8 @@ static std::vector<int64_t> chunk_sorted_order(const std::vector<int64_t> &sbeg,
 
 // Padded / real rows a masked planar bucket may carry: padding costs instructions, not lines.
 constexpr double kMaskPad = 3.0;
+// Padded / real rows a bucket of the fused small-matrix split may carry in length-sorted order.
+constexpr double kSmallPad = 1.5;
 
 static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
                       int64_t total_entries, int64_t gather_limit, std::vector<int64_t> &order,
@@ -348,6 +351,25 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
         // per range ran 193 us against the merge kernel's 171 us, profiles/r03_fork_ab2.log)
         return ratio <= (pad_limit > 0 ? pad_limit : h->slots_pad) && (double)longest <= std::max(64.0, 0.5 * rows_per_range);
     };
+    if (kind == 0 && h->small_split > 1 && h->slots_mode != 0) {
+        // fused small-matrix split (build_transposed): P waves fold every chunk, so a chunk longer than
+        // the rows of a range does not unbalance anything; padding rows cost instructions and a few
+        // cached lines of a matrix that stays in L2, so a sorted order may pad up to kSmallPad
+        auto pad = [&](const std::vector<int64_t> &sb) {
+            int64_t rows = 0;
+            for (int32_t c : chunk_rows(sb, RPI)) rows += c;
+            return (double)(rows * RPI) / (double)real;
+        };
+        // a bucket's padding counts against the whole launch: a few-chunk bucket (one chunk of 5 stripes,
+        // one of them long) may pad far beyond kSmallPad and still add only a few workgroups' rows
+        auto ok = [&](double p) { return p <= kSmallPad || (p - 1.0) * (double)real <= 0.05 * (double)total_entries; };
+        if (h->slots_sort != 2 && (pad(sbeg) <= h->slots_pad || (h->slots_sort == 0 && ok(pad(sbeg))))) return 1;
+        if (h->slots_sort == 0) return 0;
+        order = sorted_order(sbeg, RPI);
+        if (ok(pad(permuted_sbeg(sbeg, order)))) return 2;
+        order.clear();
+        return 0;
+    }
     if (h->slots_sort != 2 && fits(sbeg, h->slots_mode == 1)) return 1;
     if (h->slots_sort == 0) return 0;
     if (mask && kind == 0 && h->planar_mask != 0 && slot_planar(h, 0, w) && !split_likely) {
@@ -430,7 +452,9 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         for (int32_t c : cr) rows += c;
         // planar buckets with fewer chunks than wave slots: one chunk per workgroup of `split` waves
         split = 1;
-        if (planar && h->planar_split != 0) {
+        if (planar && kind == 0 && h->small_split > 1) {
+            split = h->small_split;  // fused small-matrix split: one P for every bucket of the launch
+        } else if (planar && h->planar_split != 0) {
             if (h->planar_split > 1) split = h->planar_split;
             else if ((double)nch / (pair ? 2 : 1) * 2 <= share) {  // in 64-stripe chunks
                 // few chunks (at most half the wave slots): P waves per chunk while the grid stays within
@@ -512,6 +536,14 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.split = split;
     b.pair = pair ? 1 : 0;
     b.mask = (mask && planar && split == 1 && (!pair || h->planar_mask_pair)) ? 1 : 0;
+    if (planar && split > 1) {
+        // split bins: the pipelined slice loop when a wave's slice averages >= split_pipe_steps steps of
+        // ~VBC_SPLIT_VALS values (medium matrices; VBC_SPLIT_PIPE=0 / 1 forces it off / on)
+        const double rows_per_wave = (double)rows / (double)std::max<int64_t>(nch, 1) / split;
+        const int u0 = (9 / w) / run * run;  // planar_split_step (vbc_planar.h, VBC_SPLIT_VALS = 9)
+        const double step_rows = (double)std::min(8 * run, std::max(run, u0));
+        b.deep = h->split_pipe >= 0 ? h->split_pipe : (rows_per_wave >= 3.0 * step_rows ? 1 : 0);
+    }
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
@@ -1056,6 +1088,34 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     for (int64_t l = 0; l < s.L; l++) buckets[s.w[l]].push_back(l);
     const int64_t total = (int64_t)s.rows.size();
     int range0 = 0, srange0 = 0, tile0 = 0;
+    // Small matrices with several width buckets (a SuiteSparse operator's strict stripes: ct20stif's are
+    // 1..6 wide; filled / mixed partitions): every bucket planar (any width 1..8, one stripe per lane)
+    // and split, P waves per 64-stripe chunk, all buckets in ONE launch (Launch::fuse_split) -- instead
+    // of a slotted launch, one launch per planar bucket and the merge kernel for the buckets whose
+    // chunks are too long to balance one wave each.  Taken when the chunks of all buckets together fill
+    // at most half the wave slots (the split rule of build_slots) and every chunk keeps >= split_rows
+    // (fp64) rows per wave; P is common to the launch.  VBC_SMALL_FUSE=0 turns it off.
+    h->small_split = 0;
+    if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar != 0 && h->slots_mode != 0 && buckets.size() >= 2 &&
+        (int)buckets.size() <= kSplitParts && buckets.rbegin()->first <= 8 && !sweep_possible(h, 1, s.m)) {
+        int64_t nch = 0, rows = 0;
+        for (auto &kv : buckets) {
+            nch += ((int64_t)kv.second.size() + 63) / 64;
+            for (int64_t l : kv.second) rows += s.rbeg[l + 1] - s.rbeg[l];
+        }
+        const double slots = (double)h->target_ranges_p;
+        const double avg = (double)rows / (double)std::max<int64_t>(nch, 1) / 64.0 * 1.1;  // rows per chunk (sorted)
+        const double minrows = (double)h->split_rows * h->esz / 8.0;
+        if ((double)nch * 2 <= slots) {
+            int P = 1;
+            while (P < 8 && (double)nch * P * 2 <= 2 * slots && avg / (P * 2) >= minrows) P *= 2;
+            if (h->planar_split > 1) P = h->planar_split;
+            if (P > 1) h->small_split = P;
+        }
+        if (getenv("VBC_VERBOSE"))
+            fprintf(stderr, "[vbc] small fused split: %d buckets, %lld chunks, %.1f rows per chunk -> P = %d\n",
+                    (int)buckets.size(), (long long)nch, avg, h->small_split);
+    }
     for (auto &kv : buckets) {
         const int w = kv.first;
         if (sweep_possible(h, w, s.m)) {
@@ -1797,6 +1857,30 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
         VBC_HIP(hipMalloc(&L.d_pbins, L.pbins.size() * sizeof(SlotBin)));
         VBC_HIP(hipMemcpy(L.d_pbins, L.pbins.data(), L.pbins.size() * sizeof(SlotBin), hipMemcpyHostToDevice));
     }
+    // the fused small-matrix split (build_transposed): every planar bin a split bin of the common P, all
+    // of them one launch of spmv_split_multi (their chunks concatenated)
+    L.fuse_split = 0;
+    if (h->small_split > 1 && !L.pbins.empty() && (int)L.pbins.size() <= kSplitParts) {
+        bool all = true;
+        for (const SlotBin &b : L.pbins)
+            all = all && b.kind == 0 && b.split == h->small_split && !b.kc && !b.lanes && !b.pair && !b.mask &&
+                  b.diag == 0 && b.wkey >= 1 && b.wkey <= 8 && b.w == b.wkey && b.run >= 1 && b.run <= 3;
+        if (all) {
+            SplitMulti M{};
+            int c0 = 0;
+            for (size_t i = 0; i < L.pbins.size(); i++) {
+                const SlotBin &b = L.pbins[i];
+                M.p[i] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst,
+                                   b.rrow, b.key, b.val, b.out};
+                c0 += b.nranges;  // a split bin's ranges are its chunks
+            }
+            M.nparts = (int)L.pbins.size();
+            M.nchunks = c0;
+            M.pad0 = L.pbins[0].deep;  // the pipelined slice loop (build_slots)
+            L.multi = M;
+            L.fuse_split = h->small_split;
+        }
+    }
     L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);
     if (!L.bins.empty()) {
         VBC_HIP(hipMalloc(&L.d_bins, L.bins.size() * sizeof(Bin)));
@@ -1983,6 +2067,8 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
+    if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
@@ -2322,6 +2408,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
             info->planar_mask = std::max<int32_t>(info->planar_mask & 1, b.mask) | (info->planar_mask & ~1);
             if (b.lanes) info->planar_mask |= 4;
         }
+    if (h->has_t && h->lt.fuse_split) info->planar_mask |= 32;  // the B'x planar bins run as one fused split launch
     info->fwd_run = 1;
     if (h->has_f)
         for (const auto &l : h->lf)

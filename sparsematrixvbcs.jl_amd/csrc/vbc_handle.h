@@ -44,6 +44,10 @@ struct Launch {
     // disjoint stripes of y): the groups after the first run on side streams forked from the caller's
     // stream by an event and joined back, so small buckets overlap instead of queueing one after the
     // other (graph capture records them as parallel branches).  Empty when one group or VBC_FORK=0.
+    // small mixed-width B'x (vbc_device.hip build_transposed): every planar split bin in ONE launch of
+    // spmv_split_multi with fuse_split waves per chunk (0: one launch per planar bin)
+    int fuse_split = 0;
+    SplitMulti multi{};
     std::vector<hipStream_t> fork_streams;
     std::vector<hipEvent_t> fork_events;  // [0]: the fork, [1 + i]: side stream i done
 };
@@ -144,6 +148,9 @@ struct vbc_handle {
     int target_ranges_l = 4096;       // resident waves of the lane-stream planar kernel
     int slot_wonly = 1;               // VBC_SLOT_WONLY=0: the all-width slotted kernel even for one-width launches
     int split_kc = 0;                 // VBC_SPLIT_KC=1: compressed keys for split planar bins too
+    int small_split = 0;              // > 1: this B'x layout is the fused small-matrix split with P waves per chunk
+    int small_fuse = 1;               // VBC_SMALL_FUSE: 0 = never fuse the buckets of a small matrix
+    int split_pipe = -1;              // VBC_SPLIT_PIPE: split bins' pipelined slice loop (-1 auto, 0 off, 1 on)
     int split_rows = 12;              // VBC_SPLIT_ROWS: fewest chunk rows per wave of an automatic split
     int fwd_min_rows = 16;            // VBC_FWD_MIN_ROWS: fewest chunk rows per range of the forward run layout
     int planar_wps = 2;               // VBC_PLANAR_WPS: most resident waves per SIMD of a plain planar bin (0: occupancy)

@@ -118,6 +118,21 @@ struct SlotBin {
     const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)
 };
 
+// The parts of a fused split launch (vbc_planar.h spmv_split_multi): up to kSplitParts planar split
+// bins of a small matrix, their chunks concatenated (part k owns chunks [chunk0, next chunk0)).
+constexpr int kSplitParts = 8;
+struct SplitPart {
+    int32_t w, run, chunk0, nseg, out_affine, out_base, out_stride, wst;
+    const int32_t *rrow;
+    const uint32_t *key;
+    const void *val;
+    const int32_t *out;
+};
+struct SplitMulti {
+    int32_t nparts, nchunks, pad0, pad1;
+    SplitPart p[kSplitParts];
+};
+
 // XCD-aware workgroup order: the hardware deals workgroups round-robin over the 8 XCDs, so logical
 // block xcd * (nb / 8) + i -- a contiguous run of ranges, whose x gathers overlap -- is given to the
 // workgroups of one XCD, which share its L2.  Blocks past the last full round keep their index.
@@ -177,6 +192,8 @@ int occupancy_slots(int esz, int kind);
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                   double alpha, double beta, bool rd, hipStream_t s);
 int occupancy_planar(int esz);
+int launch_split_multi(int esz, const SplitMulti &M, int P, const void *x, void *y, double alpha, double beta, bool rd,
+                       hipStream_t s);
 int occupancy_lanes(int esz);
 
 __host__ __device__ constexpr int vec_elems(int esz, int w)

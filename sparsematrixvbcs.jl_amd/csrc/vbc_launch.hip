@@ -14,7 +14,8 @@ namespace vbc {
 // slotted bins, each planar bin, and the merge kernel with its fix-up (+ the fill list).
 int launch_groups(const Launch &L)
 {
-    return (L.sweep_tiles > 0) + (L.slot_ranges > 0) + (int)L.pbins.size() + (L.total_ranges > 0 || L.nfill > 0);
+    const int planar = L.fuse_split ? (int)!L.pbins.empty() : (int)L.pbins.size();  // fused: one launch
+    return (L.sweep_tiles > 0) + (L.slot_ranges > 0) + planar + (L.total_ranges > 0 || L.nfill > 0);
 }
 
 // The groups in order: group g of launch_groups() on stream `stream`; g < 0: every group on it.
@@ -67,7 +68,17 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
             return VBC_HIP_ERROR;
         }
     }
-    for (size_t i = 0; i < L.pbins.size(); i++) {  // planar buckets (vbc_planar.h): one launch each
+    if (L.fuse_split && !L.pbins.empty()) {  // the small-matrix split bins: one launch for all of them
+        if (mine(true)) {
+            const hipError_t e = (hipError_t)launch_split_multi((int)sizeof(T), L.multi, L.fuse_split, x, y, alpha, beta,
+                                                                rd, stream);
+            if (e != hipSuccess) {
+                set_error("spmv_split_multi launch failed: %s", hipGetErrorString(e));
+                return VBC_HIP_ERROR;
+            }
+        }
+    }
+    for (size_t i = 0; i < (L.fuse_split ? 0 : L.pbins.size()); i++) {  // planar buckets (vbc_planar.h): one launch each
         if (!mine(true)) continue;
         const SlotBin &pb = L.pbins[i];
         const bool faste = !rd && pb.out_affine && !getenv("VBC_NO_FASTE");

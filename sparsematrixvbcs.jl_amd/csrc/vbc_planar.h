@@ -1051,18 +1051,32 @@ __host__ __device__ constexpr int planar_split_step()
     return u < RUN ? RUN : (u > cap ? cap / RUN * RUN : u);
 }
 
+// The split product's view of a bin: what one chunk's workgroup reads (SlotBin fields, or a part of a
+// fused launch, SplitMulti below).
+struct SplitView {
+    const int32_t *rrow;
+    const uint32_t *key;
+    const void *val;
+    const uint32_t *base;
+    const uint32_t *kdoff;
+    const int32_t *out;
+    int32_t nseg, out_affine, out_base, out_stride, wst;
+};
+
 // Keys and values are CACHED loads here (the streaming kernels use non-temporal ones): a split bucket
 // is small by construction, and its layout stays in L2 / MALL from one product to the next (ct20stif
 // stand-in, 25 MB, graph-timed: 8.8 -> 6.2 us; ldoor's 1/8 stripe shard, 52 MB: 11.5 -> 11.0 us).
 // DIAG (A/B ablations, tools/ab.py VBC_DIAG): 1 no x gathers, 2 gathers confined to 2 KB of x,
 // 3 no y store, 4 non-temporal key / value loads.
-template <typename T, int W_, bool KC, int RUN, int P, int DIAG = 0>
-__global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, const T *__restrict__ x,
-                                                            T *__restrict__ y, T alpha, T beta, int rd_i)
+// One chunk c by the P waves of a workgroup (wave wv); `part` = (P - 1) x 64 x W_ LDS partials.
+// PIPE: a two-stage pipeline over the wave's slice (the keys and values of step i+1 are issued before
+// the fold of step i, the gathers of step i right after its keys arrive) -- for slices of several
+// steps (medium matrices of a fused split launch, where each wave streams tens of rows); the one-phase
+// form issues a step's loads, gathers and fold back to back.
+template <typename T, int W_, bool KC, int RUN, int P, int DIAG = 0, bool PIPE = false>
+__device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, int lane, const T *__restrict__ x,
+                                            T *__restrict__ y, T alpha, T beta, int rd_i, T *part)
 {
-    const int c = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    if (c >= b.nranges) return;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     constexpr int U = planar_split_step<T, W_, RUN>(), NR = U / RUN;
     const int R0 = G(b.rrow)[c], R1 = G(b.rrow)[c + 1];
     const int S = ((R1 - R0 + P - 1) / P + RUN - 1) / RUN * RUN;
@@ -1080,11 +1094,55 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
     // NS steps at a time go through three phases -- all keys and values, then all gathers, then the
     // folds in stored order.  NS = 1 measured fastest (ct20stif stand-in P = 2: NS 1 / 2 / 3 / 4 =
     // 8.7 / 8.8 / 9.5 / 11.1 us; ldoor 1/8 shard 11.4 / 13.1 / 13.7 / 16.3 us,
-    // profiles/r03_splitns_*.log): a longer phase only adds clamped duplicate rows at the slice end.
+    // profiles/archive/r03_splitns_*.log): a longer phase only adds clamped duplicate rows at the slice end.
 #ifndef VBC_SPLIT_NS
 #define VBC_SPLIT_NS 1
 #endif
     constexpr int NS = VBC_SPLIT_NS;
+    if constexpr (PIPE && !KC && DIAG == 0) {
+        uint32_t kA[NR], kB[NR];
+        T vA[U][W_], vB[U][W_], xv[NR][RUN];
+        // rows past the slice are clamped to its last run (loaded, folded as no-ops): no branch in the
+        // loop body, so the compiler's waits stay counted
+        auto load = [&](int R, uint32_t (&kk)[NR], T (&v)[U][W_]) {
+#pragma unroll
+            for (int j = 0; j < NR; j++) {
+                kk[j] = key[(size_t)min(R + j * RUN, e - RUN) * 64 + lane];
+#pragma unroll
+                for (int d = 0; d < RUN; d++)
+                    ld_row<T, W_, 0, false>(val + (size_t)min(R + j * RUN + d, e - 1) * 64 * W_, lane, v[j * RUN + d]);
+            }
+        };
+        auto gather = [&](const uint32_t (&kk)[NR]) {
+#pragma unroll
+            for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & kSlotIdx), xv[j]);
+        };
+        auto fold = [&](int R, const uint32_t (&kk)[NR], const T (&v)[U][W_]) {
+#pragma unroll
+            for (int j = 0; j < NR; j++) {
+                const bool live = R + j * RUN < e;
+                const bool pad = (kk[j] & kPad) != 0;
+#pragma unroll
+                for (int d = 0; d < RUN; d++) {
+                    const T xe = pad ? T(0) : xv[j][d];
+#pragma unroll
+                    for (int k = 0; k < W_; k++) {
+                        const T nv = fmadd(v[j * RUN + d][k], xe, acc[k]);
+                        acc[k] = live ? nv : acc[k];
+                    }
+                }
+            }
+        };
+        load(a, kA, vA);
+        for (int R = a; R < e; R += 2 * U) {
+            gather(kA);
+            load(R + U, kB, vB);
+            fold(R, kA, vA);
+            gather(kB);
+            load(R + 2 * U, kA, vA);
+            fold(R + U, kB, vB);
+        }
+    } else
     for (int R = a; R < e; R += NS * U) {
         uint32_t kk[NS][NR], bs[NS][NR];
         T v[NS][U][W_], xv[NS][NR][RUN];
@@ -1133,17 +1191,16 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
                 }
             }
     }
-    __shared__ T part[P > 1 ? P - 1 : 1][64 * W_];
     if (wv > 0) {
 #pragma unroll
-        for (int k = 0; k < W_; k++) part[wv - 1][k * 64 + lane] = acc[k];
+        for (int k = 0; k < W_; k++) part[((wv - 1) * W_ + k) * 64 + lane] = acc[k];
     }
     __syncthreads();
     if (wv != 0) return;
 #pragma unroll
     for (int q = 0; q < P - 1; q++)
 #pragma unroll
-        for (int k = 0; k < W_; k++) acc[k] += part[q][k * 64 + lane];
+        for (int k = 0; k < W_; k++) acc[k] += part[(q * W_ + k) * 64 + lane];
     const int seg = c * 64 + lane;
     if (seg >= b.nseg) return;
     if (DIAG == 3 && acc[0] != T(-12345.678)) return;
@@ -1157,6 +1214,61 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
             yo[k] = q;
         }
     }
+}
+
+template <typename T, int W_, bool KC, int RUN, int P, int DIAG = 0>
+__global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, const T *__restrict__ x,
+                                                            T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const int c = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    if (c >= b.nranges) return;
+    __shared__ T part[(P > 1 ? P - 1 : 1) * 64 * W_];
+    const SplitView v{b.rrow, b.key, b.val, b.base, b.kdoff, b.out, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst};
+    if (!KC && DIAG == 0 && b.deep)  // SlotBin::deep on a split bin: the pipelined slice loop
+        split_chunk<T, W_, KC, RUN, P, DIAG, true>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
+    else
+        split_chunk<T, W_, KC, RUN, P, DIAG>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
+}
+
+// ONE launch for every split bin of a small mixed-width matrix (Launch::fuse_split): workgroup c is
+// chunk c of the concatenated bins; the part holding it is found by a scalar scan of the (<= 8) parts,
+// all kernel arguments, so no descriptor load precedes the chunk's first key load.  Each wave runs
+// the split body of its part's width and row run (a switch, every workgroup one case).  A matrix of
+// several width buckets then costs one launch instead of one per planar bucket plus the slotted and
+// merge launches (the ct20stif stand-in's strict stripes have widths 1..6).
+template <typename T, int P, bool PIPE>
+__global__ __launch_bounds__(64 * P) void spmv_split_multi(const SplitMulti M, const T *__restrict__ x,
+                                                           T *__restrict__ y, T alpha, T beta, int rd_i)
+{
+    const int c = blockIdx.x;
+    if (c >= M.nchunks) return;
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kSplitParts; k++) i = (k < M.nparts && M.p[k].chunk0 <= c) ? k : i;
+    i = __builtin_amdgcn_readfirstlane(i);
+    int w = 0, run = 0, chunk0 = 0;
+    SplitView v{};
+    // a switch over the part index keeps every field a kernel argument (no dynamic indexing)
+#define VBC_PART(K)                                                                                               \
+    case K: {                                                                                                     \
+        const SplitPart &q = M.p[K];                                                                              \
+        w = q.w; run = q.run; chunk0 = q.chunk0;                                                                  \
+        v = SplitView{q.rrow, q.key, q.val, nullptr, nullptr, q.out, q.nseg, q.out_affine, q.out_base, q.out_stride, q.wst}; \
+        break;                                                                                                    \
+    }
+    switch (i) { VBC_PART(0) VBC_PART(1) VBC_PART(2) VBC_PART(3) VBC_PART(4) VBC_PART(5) VBC_PART(6) VBC_PART(7) }
+#undef VBC_PART
+    __shared__ T part[(P > 1 ? P - 1 : 1) * 64 * 8];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = c - chunk0;
+#define VBC_WR(W, R) \
+    case W * 4 + R: split_chunk<T, W, false, R, P, 0, PIPE>(v, cc, wv, lane, x, y, alpha, beta, rd_i, part); break;
+    switch (w * 4 + run) {
+        VBC_WR(1, 1) VBC_WR(2, 1) VBC_WR(3, 1) VBC_WR(4, 1) VBC_WR(5, 1) VBC_WR(6, 1) VBC_WR(7, 1) VBC_WR(8, 1)
+        VBC_WR(1, 2) VBC_WR(2, 2) VBC_WR(3, 2) VBC_WR(4, 2) VBC_WR(5, 2) VBC_WR(6, 2) VBC_WR(7, 2) VBC_WR(8, 2)
+        VBC_WR(1, 3) VBC_WR(2, 3) VBC_WR(3, 3) VBC_WR(4, 3) VBC_WR(5, 3) VBC_WR(6, 3) VBC_WR(7, 3) VBC_WR(8, 3)
+    default: break;
+    }
+#undef VBC_WR
 }
 
 }  // namespace vbc

@@ -61,6 +61,8 @@ static int launch_r(const SlotBin &hb, const SlotBin *d_b, bool faste, bool stag
 {
     if (hb.split > 1) {
         switch (hb.wkey) {
+        case 1: launch_split<T, 1, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
+        case 2: launch_split<T, 2, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
         case 3: launch_split<T, 3, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
         case 4: launch_split<T, 4, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
         case 5: launch_split<T, 5, KC, RUN>(hb, d_b, x, y, alpha, beta, rd, s); break;
@@ -249,6 +251,35 @@ int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bo
                      : launch_t<double, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
     return hb.kc ? launch_t<float, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
                  : launch_t<float, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+}
+
+template <typename T>
+static int launch_split_multi_t(const SplitMulti &M, int P, const void *x, void *y, double alpha, double beta, bool rd,
+                                hipStream_t s)
+{
+    const T *xs = static_cast<const T *>(x);
+    T *ys = static_cast<T *>(y);
+    const dim3 grid(M.nchunks);
+    const bool pipe = M.pad0 != 0;  // SplitMulti::pad0: the pipelined slice loop (vbc_device.hip finalize_launch)
+#define VBC_MULTI(PP)                                                                                                   \
+    if (pipe) hipLaunchKernelGGL((spmv_split_multi<T, PP, true>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd); \
+    else hipLaunchKernelGGL((spmv_split_multi<T, PP, false>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd);
+    switch (P) {
+    case 2: VBC_MULTI(2) break;
+    case 4: VBC_MULTI(4) break;
+    case 8: VBC_MULTI(8) break;
+    default: return (int)hipErrorInvalidValue;
+    }
+#undef VBC_MULTI
+    return (int)hipGetLastError();
+}
+
+int launch_split_multi(int esz, const SplitMulti &M, int P, const void *x, void *y, double alpha, double beta, bool rd,
+                       hipStream_t s)
+{
+    if (M.nchunks <= 0) return (int)hipSuccess;
+    return esz == 8 ? launch_split_multi_t<double>(M, P, x, y, alpha, beta, rd, s)
+                    : launch_split_multi_t<float>(M, P, x, y, alpha, beta, rd, s);
 }
 
 int occupancy_planar(int esz)

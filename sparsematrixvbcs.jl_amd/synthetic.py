@@ -268,6 +268,33 @@ def fe_stiffness_3d_1dvbc(n, nnz, dof=3, W=8, dtype=np.float64, seed=0xDEADBEEF)
     return SparseMatrix1DVBC(W, n, n, SplitPartition(spl), pos, rows, ofs, val)
 
 
+def fe_stiffness_3d_vbc(n, nnz, dof=3, U=8, W=8, dtype=np.float32, seed=0xDEADBEEF):
+    """fe_stiffness_3d(n, nnz, dof) directly as SparseMatrixVBC{U,W} with dof x dof node tiles: block
+    row k = mesh node k's rows, stripe l = node l's columns (what AlternatingPacker(StrictChunker,
+    StrictChunker) finds on that matrix -- a node's dof columns share a pattern, and so do its dof
+    rows -- unless two consecutive nodes happen to share theirs).  Per stripe the coupled nodes'
+    tiles in ascending block row, each tile row-major (constructors_VBC.jl:95-105).  The structured
+    (mesh) counterpart of c5's random tiles: neighbouring stripes gather neighbouring X block rows."""
+    N, bi, bj, vals = _stiffness_blocks(n, nnz, dof, seed)
+    order = np.lexsort((bi, bj))
+    bi, bj, vals = bi[order], bj[order], vals[order]
+    cnt = np.bincount(bj, minlength=N).astype(np.int64)
+    spl = 1 + np.arange(N + 1, dtype=np.int64) * dof
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)]).astype(np.int64)
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * dof * dof)]).astype(np.int64)
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + _simd_pad(W, dtype, U), dtype)
+    val[:nv] = vals.reshape(-1)
+    return SparseMatrixVBC(U, W, n, n, SplitPartition(spl.copy()), SplitPartition(spl), pos, bi + 1, ofs, val)
+
+
+def c5_mesh(dtype=np.float32, scale=1.0, seed=0xDEADBEEF):
+    """C5 on a STRUCTURED input: the 3D stiffness stand-in of c5's size (2,097,152 rows, 1.0e8
+    stored values) as a SparseMatrixVBC of 3 x 3 node tiles (fe_stiffness_3d_vbc)."""
+    n = 3 * int(round(699051 * scale))
+    return fe_stiffness_3d_vbc(n, int(round(1e8 * scale)), 3, dtype=dtype, seed=seed)
+
+
 def _sym_uniform(r, c, seed):
     """U[-1, 1) value of entry (r, c), symmetric in (r, c): a 64-bit mix of (min, max, seed)."""
     lo = np.minimum(r, c).astype(np.uint64)

@@ -236,9 +236,10 @@ def test_split_chunks(monkeypatch, P, dtype, w, R):
 
 
 def test_split_auto_small_matrix():
-    """The ct20stif stand-in (17443 3-dof stripes, 273 planar chunks) picks the split product."""
-    import bench
-    B = bench.build_matrix("ct20stif", np.float64)
+    """A one-width 3-dof operator of ct20stif's size (17443 stripes, 273 planar chunks: the rounds 1-3
+    stand-in) picks the split product."""
+    A = V.synthetic.fe_stiffness_3d(52329, 2600295, 3, np.float64)
+    B = V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
     inf = B.info(trans=True)
     assert inf["planar_bins"] >= 1 and inf["planar_split"] > 1
     x = np.random.default_rng(1).uniform(-1, 1, B.m)
@@ -450,10 +451,11 @@ def test_forward_split(monkeypatch, P, dtype, w, R):
 
 
 def test_forward_split_auto_small_matrix(monkeypatch):
-    """The ct20stif stand-in's forward product (273 chunks of node rows) picks the split product by
-    default and matches the oracle; VBC_CREATE_SERIAL (serial=True) keeps one wave per chunk."""
-    import bench
-    B = bench.build_matrix("ct20stif", np.float64)
+    """A one-width 3-dof operator of ct20stif's size (273 chunks of node rows: the rounds 1-3 stand-in)
+    picks the split forward product by default and matches the oracle; VBC_CREATE_SERIAL
+    (serial=True) keeps one wave per chunk."""
+    A = V.synthetic.fe_stiffness_3d(52329, 2600295, 3, np.float64)
+    B = V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))
     assert B.info(trans=False)["planar_mask"] & 8
     x = np.random.default_rng(2).uniform(-1, 1, B.n)
     y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
@@ -622,3 +624,60 @@ def test_forward_masked_order(monkeypatch, dtype, w, R):
         (TOL64 if dtype == np.float64 else TOL32)
     Ri = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, vi.astype(np.float64))
     assert np.array_equal(outs["1i"].astype(np.float64), O.mul(Ri, xi.astype(np.float64), np.zeros(B.m)))
+
+
+def test_small_mixed_widths_fused_split(golden):
+    """A small matrix with several width buckets (the ct20stif stand-in's strict stripes are 1..6 wide,
+    calibrated to src/ref.out) runs every bucket planar and split, in ONE launch (vbc_info planar_mask
+    bit 5): the product matches the oracle (the P slices reorder a chunk's sum: normwise 1e-12),
+    bit-for-bit on one-hot probes of the reference corpus cut into mixed widths, with non-finite x where
+    the reference puts it, alpha / beta, fp32; VBC_SMALL_FUSE=0 and serial=True keep the unfused
+    layouts and the oracle's bits."""
+    import bench
+    B = bench.build_matrix("ct20stif", np.float64)
+    inf = B.info(trans=True)
+    assert inf["planar_mask"] & 32 and inf["planar_split"] > 1 and inf["bins_t"] == 0
+    rng = np.random.default_rng(21)
+    R = ref_of(B)
+    for alpha, beta in ((1.0, 0.0), (0.5, -1.5)):
+        x = rng.uniform(-1, 1, B.m)
+        y0 = rng.uniform(-1, 1, B.n)
+        y = dev(y0.copy())
+        V.mul_(y, B.T, dev(x), alpha, beta)
+        ref = O.mul(R, x, y0.copy(), alpha, beta, trans=True, ref_semantics=False)
+        assert rel(y.cpu().numpy(), ref) <= TOL64, (alpha, beta)
+    x = rng.uniform(-1, 1, B.m)
+    x[[3, 999]] = [np.inf, np.nan]
+    y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    ref = O.mul(R, x, np.zeros(B.n), trans=True)
+    got = y.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    assert rel(got[fin], ref[fin]) <= TOL64
+    B.serial = True  # VBC_CREATE_SERIAL: no split, the oracle's bits
+    yS = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    x = rng.uniform(-1, 1, B.m)
+    V.mul_(yS, B.T, dev(x))
+    assert not B.info(trans=True)["planar_mask"] & 32
+    assert np.array_equal(yS.cpu().numpy(), O.mul(R, x, np.zeros(B.n), trans=True))
+    B32 = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val.astype(np.float32))
+    assert B32.info(trans=True)["planar_mask"] & 32
+    x32 = x.astype(np.float32)
+    y32 = torch.zeros(B.n, dtype=torch.float32, device=DEV)
+    V.mul_(y32, B32.T, dev(x32))
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B32.val.astype(np.float64))
+    assert rel(y32.cpu().numpy(), O.mul(R64, x32.astype(np.float64), np.zeros(B.n), trans=True)) <= TOL32
+    # one-hot probes (runtests.jl:42-53, exact) on the corpus cut into mixed widths 1..8
+    seen = 0
+    for key, g in golden.items():
+        A = g["A"]
+        n = A.shape[1]
+        w, tot = [], 0
+        while tot < n:
+            w.append(min(len(w) % 8 + 1, n - tot))
+            tot += w[-1]
+        Bm = V.SparseMatrix1DVBC[8](A, V.SplitPartition(np.concatenate([[1], 1 + np.cumsum(w)])))
+        seen += bool(Bm.info(trans=True)["planar_mask"] & 32)
+        one_hot_probes(Bm, A)
+    assert seen > 0

@@ -333,3 +333,21 @@ def test_time_model_2d_fit_recovers_parameters():
     for u in range(1, U + 1):
         for w in range(1, W + 1):
             assert np.isclose(mdl.block_cost([u], [w])[0], beta[u - 1, w - 1], rtol=1e-6)
+
+
+def test_mesh_vbc_generator_equals_strict_2d_packer():
+    """synthetic.fe_stiffness_3d_vbc (the structured C5 input, bench workload c5-mesh) builds exactly
+    the SparseMatrixVBC that AlternatingPacker(StrictChunker(8), StrictChunker(8)) makes of the same
+    stiffness matrix (constructors_VBC.jl:15-133 via the oracle's builder): 3 x 3 node tiles."""
+    n, nnz = 3000, 120000
+    A = V.synthetic.fe_stiffness_3d(n, nnz, 3, np.float64, seed=7)
+    Bd = V.synthetic.fe_stiffness_3d_vbc(n, nnz, 3, dtype=np.float64, seed=7)
+    Bp = V.SparseMatrixVBC[8, 8](A, V.AlternatingPacker(V.StrictChunker(8), V.StrictChunker(8)))
+    assert Bd.Pi == Bp.Pi and Bd.Phi == Bp.Phi
+    for f in ("pos", "idx", "ofs"):
+        assert np.array_equal(getattr(Bd, f), getattr(Bp, f)), f
+    nv = int(Bd.ofs[-1] - 1)
+    assert np.array_equal(Bd.val[:nv], Bp.val[:nv])
+    R = O.RefVBC(Bd.m, Bd.n, Bd.U, Bd.W, Bd.Pi.spl, Bd.Phi.spl, Bd.pos, Bd.idx, Bd.ofs, Bd.val)
+    x = np.random.default_rng(1).uniform(-1, 1, n)
+    assert np.allclose(O.mul(R, x, np.zeros(n), trans=True), A.T @ x, rtol=1e-12, atol=1e-12)

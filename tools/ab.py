@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--nrhs", type=int, default=0, help=">0: time the multi-RHS product (row-major X / Y)")
     ap.add_argument("--shard", default="", help="R/N: time stripe shard R of the N-way split (distributed.stripe_split)")
+    ap.add_argument("--method", default="", help="ct20stif / ldoor / 3dtube / thermal1: build the stand-in with this "
+                    "bin/test_table.jl method instead of StrictChunker(8): overlap | blocks | memory | overlap2d07")
     ap.add_argument("--graph", action="store_true",
                     help="time each variant as one HIP-graph replay of --reps products (span / reps), as bench.py "
                          "does: per-launch event brackets inflate small kernels")
@@ -43,6 +45,18 @@ def main():
     dtype = np.float64 if args.dtype == "f64" else np.float32
     if args.workload == "ldoor-csc":
         B = V.SparseMatrixCSC(V.synthetic.standin("GHS_psdef/ldoor").T.tocsc().astype(dtype))
+    elif args.method or args.workload in ("3dtube", "thermal1", "chesapeake"):
+        names = {"ct20stif": "Boeing/ct20stif", "ldoor": "GHS_psdef/ldoor", "3dtube": "Rothberg/3dtube",
+                 "thermal1": "Schmid/thermal1", "chesapeake": "DIMACS10/chesapeake"}
+        A = V.synthetic.standin(names[args.workload], dtype=dtype).T.tocsc()
+        lim = lambda mdl: V.ConstrainedCost(mdl, V.VertexCount(), 8)
+        meth = {"": V.StrictChunker(8), "strict": V.StrictChunker(8), "overlap": V.OverlapChunker(0.9, 8),
+                "blocks": V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks())),
+                "memory": V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_memory(dtype, np.int64)))}
+        if args.method == "overlap2d07":
+            B = V.SparseMatrixVBC[8, 8](A, V.AlternatingPacker(V.OverlapChunker(0.7, 8), V.OverlapChunker(0.7, 8)))
+        else:
+            B = V.SparseMatrix1DVBC[8](A, meth[args.method])
     else:  # fe | fe3d | ns | ns-mixed | c5 | ldoor | ct20stif: the bench's own matrices
         B = bench.build_matrix(args.workload, dtype, args.scale)
         if args.shard:
