@@ -254,6 +254,9 @@ def box_info(device):
     p = torch.cuda.get_device_properties(device)
     out = {"name": p.name, "cus": p.multi_processor_count, "hbm_gib": round(p.total_memory / 2 ** 30, 1),
            "arch": getattr(p, "gcnArchName", None)}
+    if any(k.startswith("ROCPROF") for k in os.environ):  # under rocprofv3 a child (rocm-smi, a python
+        out["clocks"] = "not queried under rocprofv3"     # script) would re-exec an instrumented interpreter
+        return out
     try:
         r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=30)
         card = next(iter(json.loads(r.stdout).values()))

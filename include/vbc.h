@@ -73,10 +73,12 @@ typedef enum vbc_mem { VBC_MEM_DEVICE = 0, VBC_MEM_HOST = 1 } vbc_mem;
                                       matrix is read once for all right-hand sides. */
 #define VBC_CREATE_SERIAL 0x8u     /* keep the reference's serial summation order in every layout of
                                       both directions: no split planar B'x product (per-stripe row
-                                      order, multiply_1DVBC.jl:101-104; vbc_info.planar_split stays 1)
-                                      and no split forward product (stripe order per output row,
-                                      :62-71; planar_mask bit 3 stays clear), so every output is
-                                      bit-identical to the oracle whatever the matrix size.  Default:
+                                      order, multiply_1DVBC.jl:101-104; vbc_info.planar_split stays 1),
+                                      no merge layout where a slotted one can hold the bucket (its
+                                      segmented scan joins per-slot partial sums), and no split
+                                      forward product (stripe order per output row, :62-71; planar_mask
+                                      bit 3 stays clear), so every B'x output is bit-identical to the
+                                      oracle whatever the matrix size (B·x: see VBC_SPLIT_ROWS).  Default:
                                       small matrices may fold a chunk's rows (B'x) or blocks (B·x) in
                                       P slices whose partial sums meet in LDS (rounding differs ~1 ulp);
                                       vbc_info reports it as planar_split > 1 / planar_mask bit 3. */

@@ -75,6 +75,7 @@ def model_SparseMatrix1DVBC_TrSpMV_time_data(W, Tv=np.float64, Ti=np.int64, Tu=n
             t = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e-3
             ms.append(m); ns.append(B.n); Ls.append(L); ws.append(w); qs.append(int(B.pos[-1] - 1)); T.append(t)
             B.release()
+            print(f"[costs] 1DVBC time data ({locality}): w {w} m {m} L {L} q {q} t {t * 1e6:.1f} us", flush=True)  # costs.jl:91
     return ms, ns, Ls, ws, qs, T
 
 
@@ -235,6 +236,8 @@ def model_SparseMatrixVBC_TrSpMV_time_data(U, W, Tv=np.float64, Ti=np.int64, Tu=
                 for lst, v in zip(out, (B.m, B.n, K, L, u, w, int(B.pos[-1] - 1), float(np.median(ts)))):
                     lst.append(v)
                 B.release()
+                print(f"[costs] VBC time data: u {u} w {w} K {K} L {L} q {q} t {np.median(ts) * 1e6:.1f} us",
+                      flush=True)  # costs.jl:241
     return out
 
 

@@ -318,8 +318,9 @@ static std::vector<int64_t> chunk_sorted_order(const std::vector<int64_t> &sbeg,
 
 // Padded / real rows a masked planar bucket may carry: padding costs instructions, not lines.
 constexpr double kMaskPad = 3.0;
-// Padded / real rows a bucket of the fused small-matrix split may carry in length-sorted order.
-constexpr double kSmallPad = 1.5;
+// Padded / real rows a bucket of the fused small-matrix split may carry in length-sorted order: a chunk
+// costs its longest stripe's rows / P whatever its padding, and the padding rows read cached zeros.
+constexpr double kSmallPad = 4.0;
 
 static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
                       int64_t total_entries, int64_t gather_limit, std::vector<int64_t> &order,
@@ -355,10 +356,12 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
         // fused small-matrix split (build_transposed): P waves fold every chunk, so a chunk longer than
         // the rows of a range does not unbalance anything; padding rows cost instructions and a few
         // cached lines of a matrix that stays in L2, so a sorted order may pad up to kSmallPad
-        auto pad = [&](const std::vector<int64_t> &sb) {
-            int64_t rows = 0;
-            for (int32_t c : chunk_rows(sb, RPI)) rows += c;
-            return (double)(rows * RPI) / (double)real;
+        auto pad = [&](const std::vector<int64_t> &sb) {  // rows the chunks' lanes that hold a segment step through
+            const std::vector<int32_t> cr = chunk_rows(sb, RPI);
+            int64_t padded = 0;
+            for (size_t c = 0; c < cr.size(); c++)
+                padded += (int64_t)cr[c] * std::min<int64_t>(RPI, nseg - (int64_t)c * RPI);
+            return (double)padded / (double)real;
         };
         // a bucket's padding counts against the whole launch: a few-chunk bucket (one chunk of 5 stripes,
         // one of them long) may pad far beyond kSmallPad and still add only a few workgroups' rows
@@ -430,6 +433,10 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     const int64_t real = sbeg[nseg] - sbeg[0];
     const bool planar = slot_planar(h, kind, w);
     const int run = planar ? slot_runs(h, ents, sbeg0) : 1;  // sbeg0: the input order ents is in
+    // runs with holes (build_transposed, hole_runs): absent rows are entries with voff < 0
+    bool holes = false;
+    for (const Entry &en : ents) holes = holes || en.voff < 0;
+    if (holes && !(planar && run > 1 && kind == 0)) return fail(VBC_INVALID_ARG, "internal: runs with holes outside a planar B'x bin");
     // pair layout (vbc_planar.h run_pair): fp64 3-wide stripes with runs of 3, a lane pair per stripe
     // (for long segments: FE-3D's ~3 runs per stripe measured slower with 32-stripe chunks, 304 -> 315
     // us, ldoor's ~15 faster, 92 -> 81 us)
@@ -536,13 +543,20 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.split = split;
     b.pair = pair ? 1 : 0;
     b.mask = (mask && planar && split == 1 && (!pair || h->planar_mask_pair)) ? 1 : 0;
+    b.holes = holes ? 1 : 0;
+    if (holes && (split == 1 || pair)) return fail(VBC_INVALID_ARG, "internal: runs with holes need the split product");
     if (planar && split > 1) {
-        // split bins: the pipelined slice loop when a wave's slice averages >= split_pipe_steps steps of
-        // ~VBC_SPLIT_VALS values (medium matrices; VBC_SPLIT_PIPE=0 / 1 forces it off / on)
+        // split bins' slice loop (vbc_planar.h split_chunk): 0 one step at a time, 1 pipelined, 2 batched;
+        // auto: the plain loop when a wave's slice is at most two steps of ~VBC_SPLIT_VALS values, else
+        // batched (VBC_SPLIT_PIPE=0 / 1 / 2 forces one)
         const double rows_per_wave = (double)rows / (double)std::max<int64_t>(nch, 1) / split;
         const int u0 = (9 / w) / run * run;  // planar_split_step (vbc_planar.h, VBC_SPLIT_VALS = 9)
         const double step_rows = (double)std::min(8 * run, std::max(run, u0));
-        b.deep = h->split_pipe >= 0 ? h->split_pipe : (rows_per_wave >= 3.0 * step_rows ? 1 : 0);
+        b.deep = h->split_pipe >= 0 ? h->split_pipe : (rows_per_wave > 2.0 * step_rows ? 2 : 0);
+        // VBC_SPLIT_NT_MB: above that many value bytes the batched loop reads keys and values non-temporally
+        // (mode 3).  Off by default: slower on every table partition, the 300 MB ldoor 'min blocks' too
+        // (68.3 -> 77.7 us; ct20stif strict 8.9 -> 12.3 us; profiles/r04_ab4_*.log)
+        if (b.deep == 2 && h->split_nt_bytes > 0 && (double)h->nval * h->esz > (double)h->split_nt_bytes) b.deep = 3;
     }
     b.out_affine = 1;
     b.out_base = out.empty() ? 0 : out[0];
@@ -634,11 +648,16 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
                 const Entry *en = real_row ? &ents[pstart[seg] + qr] : nullptr;
                 // padding rows gather x[0] (m >= 1: the bucket has entries), taken as 0
                 key[e] = real_row ? (en->key | last) : (kPad | last);
+                if (holes && real_row && qr % run == 0) {  // a run's first key: which of its rows are stored
+                    uint32_t mk = 0;
+                    for (int d = 0; d < run; d++) mk |= (en[d].voff >= 0 ? 1u : 0u) << (kHoleShift + d);
+                    key[e] |= mk;
+                }
                 if (planar) {  // column-group-major chunk row (vbc_planar.h)
                     char *rowp = vv + row * RPI * w * esz;
                     for (int cc = 0; cc < w; cc++) {
                         char *dst = rowp + planar_off(esz, w, sl, cc) * esz;
-                        if (real_row && cc < wsrc) std::memcpy(dst, val + (en->voff + cc) * esz, (size_t)esz);
+                        if (real_row && cc < wsrc && en->voff >= 0) std::memcpy(dst, val + (en->voff + cc) * esz, (size_t)esz);
                         else std::memset(dst, 0, (size_t)esz);
                     }
                 } else if (real_row) {
@@ -1077,6 +1096,60 @@ static int padded_width(const vbc_handle *h, int w)
     return wp;
 }
 
+// Runs with holes (SlotBin::holes) for a bucket of the fused small-matrix split: when the stripes' rows do
+// not all come in aligned runs of R consecutive rows (slot_runs) but grouping every stripe's rows by
+// row / R adds at most kHoleFill padding rows, each group becomes a whole run of R entries -- the absent
+// rows with voff = -1 (zero values; their x is taken as 0 by the kernel, so a non-finite x of a row the
+// stripe does not store never reaches it, as in the reference).  One key and one R-wide x gather per
+// run instead of one per row.  Fills hents / hsbeg (empty: no runs worth it).
+constexpr double kHoleFill = 0.15;
+static void hole_runs(const vbc_handle *h, const Stripes &s, const std::vector<int64_t> &stripes, int w,
+                      std::vector<Entry> &hents, std::vector<int64_t> &hsbeg)
+{
+    hents.clear();
+    hsbeg.clear();
+    if (h->slot_runs == 0 || s.m >= (int64_t)kHoleIdx - 3) return;
+    int64_t real = 0;
+    for (int64_t l : stripes) real += s.rbeg[l + 1] - s.rbeg[l];
+    if (real == 0) return;
+    for (int R = 3; R >= 2; R--) {
+        int64_t expanded = 0;
+        bool exact = true;
+        for (int64_t l : stripes) {
+            int64_t prev = -1, groups = 0;
+            for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) {
+                const int64_t k = s.rows[r] / R;
+                if (k != prev) { groups++; prev = k; }
+            }
+            expanded += groups * R;
+            exact = exact && groups * R == s.rbeg[l + 1] - s.rbeg[l];
+        }
+        if (exact) return;  // whole runs already: slot_runs finds them
+        if ((double)(expanded - real) > kHoleFill * (double)real) continue;
+        hsbeg.assign(1, 0);
+        hents.reserve(expanded);
+        for (int64_t l : stripes) {
+            for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1];) {
+                const int64_t k = s.rows[r] / R;
+                for (int d = 0; d < R; d++) {
+                    const int64_t row = k * R + d;
+                    if (r < s.rbeg[l + 1] && s.rows[r] == row) {
+                        hents.push_back({(uint32_t)row, s.voff[l] + (r - s.rbeg[l]) * w});
+                        r++;
+                    } else {
+                        hents.push_back({(uint32_t)row, -1});  // a hole of the run
+                    }
+                }
+            }
+            hsbeg.push_back((int64_t)hents.size());
+        }
+        if (getenv("VBC_VERBOSE"))
+            fprintf(stderr, "[vbc] runs with holes: w %d R %d rows %lld -> %lld\n", w, R, (long long)real,
+                    (long long)expanded);
+        return;
+    }
+}
+
 // Transposed layout: segments = stripes of each width, entries = their stored rows.  A bucket runs
 // slotted (vbc_slots.h, every stripe of the width a segment, empty ones included) when its row counts
 // are near-uniform, else merged (non-empty stripes; empty ones go to the fill list).
@@ -1096,7 +1169,8 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     // at most half the wave slots (the split rule of build_slots) and every chunk keeps >= split_rows
     // (fp64) rows per wave; P is common to the launch.  VBC_SMALL_FUSE=0 turns it off.
     h->small_split = 0;
-    if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar != 0 && h->slots_mode != 0 && buckets.size() >= 2 &&
+    // (auto layouts only: a forced VBC_SLOTS / VBC_SLOT_PLANAR keeps the layout the tests ask for)
+    if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar < 0 && h->slots_mode < 0 && buckets.size() >= 2 &&
         (int)buckets.size() <= kSplitParts && buckets.rbegin()->first <= 8 && !sweep_possible(h, 1, s.m)) {
         int64_t nch = 0, rows = 0;
         for (auto &kv : buckets) {
@@ -1105,7 +1179,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         }
         const double slots = (double)h->target_ranges_p;
         const double avg = (double)rows / (double)std::max<int64_t>(nch, 1) / 64.0 * 1.1;  // rows per chunk (sorted)
-        const double minrows = (double)h->split_rows * h->esz / 8.0;
+        // (the batched slice loop costs a round trip per batch, not per step: thinner slices than the
+        // single-bucket rule's split_rows pay off -- ct20stif 'min blocks' P = 4 / 8: 15.7 / 14.7 us)
+        const double minrows = (double)h->small_rows * h->esz / 8.0;
         if ((double)nch * 2 <= slots) {
             int P = 1;
             while (P < 8 && (double)nch * P * 2 <= 2 * slots && avg / (P * 2) >= minrows) P *= 2;
@@ -1143,14 +1219,25 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         std::vector<int64_t> sbeg{0}, order;
         for (int64_t l : kv.second) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
         bool mask = false;
-        if (want_slots(h, 0, wps, sbeg, total, s.m, order, &mask)) {
+        // fused small split: rows that ALMOST come in aligned runs (a stiffness operator's dof rows, some
+        // stripes missing one of a node's rows -- the structural zeros of ct20stif-like matrices) are
+        // padded to whole runs, the absent rows marked in the run's key (hole_runs)
+        std::vector<Entry> hents;
+        std::vector<int64_t> hsbeg;
+        if (h->small_split > 1 && slot_planar(h, 0, w)) hole_runs(h, s, kv.second, w, hents, hsbeg);
+        const std::vector<int64_t> &sb = hsbeg.empty() ? sbeg : hsbeg;
+        if (want_slots(h, 0, wps, sb, hsbeg.empty() ? total : total + (hsbeg.back() - sbeg.back()), s.m, order, &mask)) {
             std::vector<Entry> ents;
             std::vector<int32_t> out;
-            ents.reserve(sbeg.back());
-            for (int64_t l : kv.second) {
-                out.push_back((int32_t)s.col0[l]);
-                for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
-                    ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+            for (int64_t l : kv.second) out.push_back((int32_t)s.col0[l]);
+            if (!hsbeg.empty()) {
+                ents.swap(hents);
+                sbeg.swap(hsbeg);
+            } else {
+                ents.reserve(sbeg.back());
+                for (int64_t l : kv.second)
+                    for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
+                        ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
             }
             PendingSlot ps;
             if (want_lanes(h, wps, w, sbeg, out, total, mask)) {
@@ -1870,13 +1957,13 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
             int c0 = 0;
             for (size_t i = 0; i < L.pbins.size(); i++) {
                 const SlotBin &b = L.pbins[i];
-                M.p[i] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst,
+                M.p[i] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst, b.holes, 0,
                                    b.rrow, b.key, b.val, b.out};
                 c0 += b.nranges;  // a split bin's ranges are its chunks
             }
             M.nparts = (int)L.pbins.size();
             M.nchunks = c0;
-            M.pad0 = L.pbins[0].deep;  // the pipelined slice loop (build_slots)
+            for (const SlotBin &b : L.pbins) M.pad0 = std::max<int32_t>(M.pad0, b.deep);  // slice loop (build_slots)
             L.multi = M;
             L.fuse_split = h->small_split;
         }
@@ -2058,7 +2145,10 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
     }
-    if (flags & VBC_CREATE_SERIAL) h->planar_split = 0;  // every stripe summed serially in stored row order
+    if (flags & VBC_CREATE_SERIAL) {  // every stripe summed serially in stored row order:
+        h->planar_split = 0;            // no split planar product (P slices meeting in LDS),
+        if (h->slots_mode < 0) h->slots_mode = 1;  // and no merge layout (its segmented scan joins slot sums)
+    }
     h->occ_p = std::max(1, std::min(occupancy_planar(h->esz), 8));
     h->target_ranges_l = prop.multiProcessorCount * std::max(1, std::min(occupancy_lanes(h->esz), 8)) * kWavesPerBlock;
     if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
@@ -2069,6 +2159,8 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
+    if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;

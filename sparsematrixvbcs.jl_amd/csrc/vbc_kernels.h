@@ -95,6 +95,8 @@ struct SlotBin {
     int32_t pair;        // planar fp64 w = 3, run = 3: a lane pair per stripe, 32 stripes per chunk, rows =
                          // run-rows of 288 values (vbc_planar.h run_pair)
     int32_t xcd;         // planar: XCD-contiguous workgroup order (xcd_block)
+    int32_t holes;       // planar split runs with holes: a run's first key holds, in bits 27..29, which of its
+                         // RUN rows the stripe stores (the others: zero values, x taken as 0); index bits 0..26
     int32_t mask;        // planar: chunk-local length order (lanes of a chunk by decreasing length, the chunk's
                          // 64 stripes kept) and nlive[row] = live lanes of the chunk row; dead lanes read
                          // lane 0's key and values (no extra lines fetched) and fold nothing (vbc_planar.h)
@@ -118,11 +120,15 @@ struct SlotBin {
     const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)
 };
 
+// Runs with holes (SlotBin::holes): the run's stored-row mask above the gather index of its first key.
+constexpr uint32_t kHoleIdx = (1u << 27) - 1;
+constexpr int kHoleShift = 27;
+
 // The parts of a fused split launch (vbc_planar.h spmv_split_multi): up to kSplitParts planar split
 // bins of a small matrix, their chunks concatenated (part k owns chunks [chunk0, next chunk0)).
 constexpr int kSplitParts = 8;
 struct SplitPart {
-    int32_t w, run, chunk0, nseg, out_affine, out_base, out_stride, wst;
+    int32_t w, run, chunk0, nseg, out_affine, out_base, out_stride, wst, holes, pad;
     const int32_t *rrow;
     const uint32_t *key;
     const void *val;

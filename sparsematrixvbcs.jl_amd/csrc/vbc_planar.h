@@ -1060,7 +1060,7 @@ struct SplitView {
     const uint32_t *base;
     const uint32_t *kdoff;
     const int32_t *out;
-    int32_t nseg, out_affine, out_base, out_stride, wst;
+    int32_t nseg, out_affine, out_base, out_stride, wst, holes;
 };
 
 // Keys and values are CACHED loads here (the streaming kernels use non-temporal ones): a split bucket
@@ -1073,7 +1073,21 @@ struct SplitView {
 // the fold of step i, the gathers of step i right after its keys arrive) -- for slices of several
 // steps (medium matrices of a fused split launch, where each wave streams tens of rows); the one-phase
 // form issues a step's loads, gathers and fold back to back.
-template <typename T, int W_, bool KC, int RUN, int P, int DIAG = 0, bool PIPE = false>
+// MODE 2 (batched): NB runs of the slice at a time -- all their keys, then all their values, then all
+// their gathers (each gather waits for its key only: the loads are counted in issue order), then the
+// folds in stored order -- so a batch costs two memory round trips (keys, gathers) with the value
+// stream under them, instead of two per step; NB keeps ~24 (fp64) / 48 (fp32) values per lane in flight.
+#ifndef VBC_SPLIT_BATCH_VALS
+#define VBC_SPLIT_BATCH_VALS (sizeof(T) == 8 ? 24 : 48)
+#endif
+template <typename T, int W_, int RUN>
+__host__ __device__ constexpr int split_batch_runs()
+{
+    constexpr int nb = (int)(VBC_SPLIT_BATCH_VALS) / (W_ * RUN);
+    return nb < 2 ? 2 : (nb > 16 ? 16 : nb);
+}
+
+template <typename T, int W_, bool KC, int RUN, int P, int DIAG = 0, int MODE = 0>
 __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, int lane, const T *__restrict__ x,
                                             T *__restrict__ y, T alpha, T beta, int rd_i, T *part)
 {
@@ -1091,6 +1105,7 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
     T acc[W_];
 #pragma unroll
     for (int k = 0; k < W_; k++) acc[k] = T(0);
+    const uint32_t imask = b.holes ? kHoleIdx : kSlotIdx;  // runs with holes: the row mask sits above the index
     // NS steps at a time go through three phases -- all keys and values, then all gathers, then the
     // folds in stored order.  NS = 1 measured fastest (ct20stif stand-in P = 2: NS 1 / 2 / 3 / 4 =
     // 8.7 / 8.8 / 9.5 / 11.1 us; ldoor 1/8 shard 11.4 / 13.1 / 13.7 / 16.3 us,
@@ -1099,7 +1114,43 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
 #define VBC_SPLIT_NS 1
 #endif
     constexpr int NS = VBC_SPLIT_NS;
-    if constexpr (PIPE && !KC && DIAG == 0) {
+    if constexpr ((MODE == 2 || MODE == 3) && !KC && DIAG == 0) {
+        constexpr int NB = split_batch_runs<T, W_, RUN>();
+        constexpr bool NT = MODE == 3;  // a layout larger than the Infinity Cache streams non-temporally
+        // (a form that issues batch i+1's keys with batch i's values measured slower: 248 VGPRs, ct20stif
+        // strict 9.1 -> 11.5 us, 'min blocks' 14.7 -> 15.4 us, profiles/r04_ab3_*.log)
+        for (int R = a; R < e; R += NB * RUN) {
+            uint32_t kk[NB];
+            T v[NB][RUN][W_], xv[NB][RUN];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const size_t o = (size_t)min(R + j * RUN, e - RUN) * 64 + lane;
+                kk[j] = NT ? __builtin_nontemporal_load(key + o) : key[o];
+            }
+#pragma unroll
+            for (int j = 0; j < NB; j++)
+#pragma unroll
+                for (int d = 0; d < RUN; d++)
+                    ld_row<T, W_, 0, NT>(val + (size_t)min(R + j * RUN + d, e - 1) * 64 * W_, lane, v[j][d]);
+#pragma unroll
+            for (int j = 0; j < NB; j++) ld_run<T, RUN>(xg + (kk[j] & imask), xv[j]);
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const bool live = R + j * RUN < e;
+                const bool pad = (kk[j] & kPad) != 0;
+#pragma unroll
+                for (int d = 0; d < RUN; d++) {
+                    const bool hole = b.holes && !((kk[j] >> (kHoleShift + d)) & 1u);
+                    const T xe = (pad || hole) ? T(0) : xv[j][d];
+#pragma unroll
+                    for (int k = 0; k < W_; k++) {
+                        const T nv = fmadd(v[j][d][k], xe, acc[k]);
+                        acc[k] = live ? nv : acc[k];
+                    }
+                }
+            }
+        }
+    } else if constexpr (MODE == 1 && !KC && DIAG == 0) {
         uint32_t kA[NR], kB[NR];
         T vA[U][W_], vB[U][W_], xv[NR][RUN];
         // rows past the slice are clamped to its last run (loaded, folded as no-ops): no branch in the
@@ -1115,7 +1166,7 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
         };
         auto gather = [&](const uint32_t (&kk)[NR]) {
 #pragma unroll
-            for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & kSlotIdx), xv[j]);
+            for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & imask), xv[j]);
         };
         auto fold = [&](int R, const uint32_t (&kk)[NR], const T (&v)[U][W_]) {
 #pragma unroll
@@ -1124,7 +1175,8 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
                 const bool pad = (kk[j] & kPad) != 0;
 #pragma unroll
                 for (int d = 0; d < RUN; d++) {
-                    const T xe = pad ? T(0) : xv[j][d];
+                    const bool hole = b.holes && !((kk[j] >> (kHoleShift + d)) & 1u);
+                    const T xe = (pad || hole) ? T(0) : xv[j][d];
 #pragma unroll
                     for (int k = 0; k < W_; k++) {
                         const T nv = fmadd(v[j * RUN + d][k], xe, acc[k]);
@@ -1166,7 +1218,7 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
         for (int t = 0; t < NS; t++)
 #pragma unroll
             for (int j = 0; j < NR; j++) {
-                const uint32_t gi = KC ? (bs[t][j] & kSlotIdx) + (kk[t][j] == kPad16 ? 0u : kk[t][j]) : kk[t][j] & kSlotIdx;
+                const uint32_t gi = KC ? (bs[t][j] & kSlotIdx) + (kk[t][j] == kPad16 ? 0u : kk[t][j]) : kk[t][j] & imask;
                 if constexpr (DIAG == 1) {
 #pragma unroll
                     for (int d = 0; d < RUN; d++) xv[t][j][d] = T(1) + T(gi & 1);
@@ -1182,7 +1234,8 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
                 const bool pad = KC ? kk[t][j] == kPad16 : (kk[t][j] & kPad) != 0;
 #pragma unroll
                 for (int d = 0; d < RUN; d++) {
-                    const T xe = pad ? T(0) : xv[t][j][d];
+                    const bool hole = !KC && b.holes && !((kk[t][j] >> (kHoleShift + d)) & 1u);
+                    const T xe = (pad || hole) ? T(0) : xv[t][j][d];
 #pragma unroll
                     for (int k = 0; k < W_; k++) {
                         const T nv = fmadd(v[t][j * RUN + d][k], xe, acc[k]);
@@ -1223,9 +1276,14 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
     const int c = b.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     if (c >= b.nranges) return;
     __shared__ T part[(P > 1 ? P - 1 : 1) * 64 * W_];
-    const SplitView v{b.rrow, b.key, b.val, b.base, b.kdoff, b.out, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst};
-    if (!KC && DIAG == 0 && b.deep)  // SlotBin::deep on a split bin: the pipelined slice loop
-        split_chunk<T, W_, KC, RUN, P, DIAG, true>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
+    const SplitView v{b.rrow, b.key, b.val, b.base, b.kdoff, b.out, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst,
+                      b.holes};
+    if (!KC && DIAG == 0 && b.deep == 1)  // SlotBin::deep on a split bin: 1 pipelined, 2 batched slice loop
+        split_chunk<T, W_, KC, RUN, P, DIAG, 1>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
+    else if (!KC && DIAG == 0 && b.deep == 2)
+        split_chunk<T, W_, KC, RUN, P, DIAG, 2>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
+    else if (!KC && DIAG == 0 && b.deep == 3)
+        split_chunk<T, W_, KC, RUN, P, DIAG, 3>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
     else
         split_chunk<T, W_, KC, RUN, P, DIAG>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
 }
@@ -1236,7 +1294,7 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
 // the split body of its part's width and row run (a switch, every workgroup one case).  A matrix of
 // several width buckets then costs one launch instead of one per planar bucket plus the slotted and
 // merge launches (the ct20stif stand-in's strict stripes have widths 1..6).
-template <typename T, int P, bool PIPE>
+template <typename T, int P, int MODE>
 __global__ __launch_bounds__(64 * P) void spmv_split_multi(const SplitMulti M, const T *__restrict__ x,
                                                            T *__restrict__ y, T alpha, T beta, int rd_i)
 {
@@ -1253,7 +1311,7 @@ __global__ __launch_bounds__(64 * P) void spmv_split_multi(const SplitMulti M, c
     case K: {                                                                                                     \
         const SplitPart &q = M.p[K];                                                                              \
         w = q.w; run = q.run; chunk0 = q.chunk0;                                                                  \
-        v = SplitView{q.rrow, q.key, q.val, nullptr, nullptr, q.out, q.nseg, q.out_affine, q.out_base, q.out_stride, q.wst}; \
+        v = SplitView{q.rrow, q.key, q.val, nullptr, nullptr, q.out, q.nseg, q.out_affine, q.out_base, q.out_stride, q.wst, q.holes}; \
         break;                                                                                                    \
     }
     switch (i) { VBC_PART(0) VBC_PART(1) VBC_PART(2) VBC_PART(3) VBC_PART(4) VBC_PART(5) VBC_PART(6) VBC_PART(7) }
@@ -1261,7 +1319,7 @@ __global__ __launch_bounds__(64 * P) void spmv_split_multi(const SplitMulti M, c
     __shared__ T part[(P > 1 ? P - 1 : 1) * 64 * 8];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = c - chunk0;
 #define VBC_WR(W, R) \
-    case W * 4 + R: split_chunk<T, W, false, R, P, 0, PIPE>(v, cc, wv, lane, x, y, alpha, beta, rd_i, part); break;
+    case W * 4 + R: split_chunk<T, W, false, R, P, 0, MODE>(v, cc, wv, lane, x, y, alpha, beta, rd_i, part); break;
     switch (w * 4 + run) {
         VBC_WR(1, 1) VBC_WR(2, 1) VBC_WR(3, 1) VBC_WR(4, 1) VBC_WR(5, 1) VBC_WR(6, 1) VBC_WR(7, 1) VBC_WR(8, 1)
         VBC_WR(1, 2) VBC_WR(2, 2) VBC_WR(3, 2) VBC_WR(4, 2) VBC_WR(5, 2) VBC_WR(6, 2) VBC_WR(7, 2) VBC_WR(8, 2)

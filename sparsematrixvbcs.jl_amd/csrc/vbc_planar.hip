@@ -260,10 +260,12 @@ static int launch_split_multi_t(const SplitMulti &M, int P, const void *x, void 
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
     const dim3 grid(M.nchunks);
-    const bool pipe = M.pad0 != 0;  // SplitMulti::pad0: the pipelined slice loop (vbc_device.hip finalize_launch)
+    const int mode = M.pad0;  // SplitMulti::pad0: slice loop 0 plain, 1 pipelined, 2 batched, 3 batched non-temporal
 #define VBC_MULTI(PP)                                                                                                   \
-    if (pipe) hipLaunchKernelGGL((spmv_split_multi<T, PP, true>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd); \
-    else hipLaunchKernelGGL((spmv_split_multi<T, PP, false>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd);
+    if (mode == 3) hipLaunchKernelGGL((spmv_split_multi<T, PP, 3>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd); \
+    else if (mode == 2) hipLaunchKernelGGL((spmv_split_multi<T, PP, 2>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd); \
+    else if (mode == 1) hipLaunchKernelGGL((spmv_split_multi<T, PP, 1>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd); \
+    else hipLaunchKernelGGL((spmv_split_multi<T, PP, 0>), grid, dim3(64 * PP), 0, s, M, xs, ys, (T)alpha, (T)beta, (int)rd);
     switch (P) {
     case 2: VBC_MULTI(2) break;
     case 4: VBC_MULTI(4) break;

@@ -626,7 +626,7 @@ def test_forward_masked_order(monkeypatch, dtype, w, R):
     assert np.array_equal(outs["1i"].astype(np.float64), O.mul(Ri, xi.astype(np.float64), np.zeros(B.m)))
 
 
-def test_small_mixed_widths_fused_split(golden):
+def test_small_mixed_widths_fused_split(golden, monkeypatch):
     """A small matrix with several width buckets (the ct20stif stand-in's strict stripes are 1..6 wide,
     calibrated to src/ref.out) runs every bucket planar and split, in ONE launch (vbc_info planar_mask
     bit 5): the product matches the oracle (the P slices reorder a chunk's sum: normwise 1e-12),
@@ -668,7 +668,9 @@ def test_small_mixed_widths_fused_split(golden):
     V.mul_(y32, B32.T, dev(x32))
     R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B32.val.astype(np.float64))
     assert rel(y32.cpu().numpy(), O.mul(R64, x32.astype(np.float64), np.zeros(B.n), trans=True)) <= TOL32
-    # one-hot probes (runtests.jl:42-53, exact) on the corpus cut into mixed widths 1..8
+    # one-hot probes (runtests.jl:42-53, exact) on the corpus cut into mixed widths 1..8 (P forced: the
+    # corpus' chunks are too short for the automatic rule to split them)
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "4")
     seen = 0
     for key, g in golden.items():
         A = g["A"]
@@ -681,3 +683,49 @@ def test_small_mixed_widths_fused_split(golden):
         seen += bool(Bm.info(trans=True)["planar_mask"] & 32)
         one_hot_probes(Bm, A)
     assert seen > 0
+
+
+def test_fused_split_runs_with_holes_nonfinite(monkeypatch):
+    """Runs with holes (SlotBin::holes): rows that almost come in node runs of 3 are padded to whole
+    runs inside the fused small split; a padded row's x is taken as 0, so a NaN / Inf in x at a row a
+    stripe does NOT store never reaches that stripe's outputs (the reference only visits stored rows,
+    multiply_1DVBC.jl:101-104), and the stored rows fold in their order (bit-exact on integer data)."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "4")
+    rng = np.random.default_rng(44)
+    N, L = 400, 300
+    widths = np.where(np.arange(L) % 2 == 0, 1, 2)  # two width buckets: the fused path
+    rows, cnt = [], []
+    for l in range(L):
+        nodes = np.sort(rng.choice(N, 12, replace=False))
+        r = (nodes[:, None] * 3 + np.arange(3)[None, :]).reshape(-1)
+        if l % 5 == 0:  # every fifth stripe misses one row of one of its runs: a hole
+            r = np.delete(r, rng.integers(0, len(r)))
+        rows.append(r)
+        cnt.append(len(r))
+    cnt = np.array(cnt)
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)])
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * widths)])
+    spl = np.concatenate([[1], 1 + np.cumsum(widths)])
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + 8)
+    val[:nv] = rng.integers(-8, 9, nv)
+    B = V.SparseMatrix1DVBC(8, 3 * N, int(spl[-1] - 1), V.SplitPartition(spl), pos, np.concatenate(rows) + 1, ofs, val)
+    inf = B.info(trans=True)
+    assert inf["planar_mask"] & 32 and inf["planar_run"] == 3
+    R = ref_of(B)
+    x = rng.integers(-8, 9, B.m).astype(np.float64)
+    y = torch.full((B.n,), float("nan"), dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert np.array_equal(y.cpu().numpy(), O.mul(R, x, np.zeros(B.n), trans=True))  # integer data: exact
+    stored = set(np.concatenate(rows).tolist())
+    holes = [r for l in range(0, L, 5) for r in range(3 * (rows[l][0] // 3), 3 * (rows[l][-1] // 3) + 3)
+             if r not in set(rows[l].tolist()) and (r // 3) in set((rows[l] // 3).tolist())]
+    assert holes
+    x[holes[0]] = np.nan
+    x[holes[-1]] = np.inf
+    V.mul_(y, B.T, dev(x))
+    ref = O.mul(R, x, np.zeros(B.n), trans=True)
+    got = y.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    assert np.array_equal(got[fin], ref[fin])

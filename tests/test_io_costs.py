@@ -351,3 +351,33 @@ def test_mesh_vbc_generator_equals_strict_2d_packer():
     R = O.RefVBC(Bd.m, Bd.n, Bd.U, Bd.W, Bd.Pi.spl, Bd.Phi.spl, Bd.pos, Bd.idx, Bd.ofs, Bd.val)
     x = np.random.default_rng(1).uniform(-1, 1, n)
     assert np.allclose(O.mul(R, x, np.zeros(n), trans=True), A.T @ x, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_products_from_2d_model_partitions(golden):
+    """products built from the SparseMatrixVBC cost-model partitions -- the reference's
+    default 5-phase memory packer (constructors_VBC.jl:1-8) and the "dynamic blocks 2D" / "dynamic
+    memory 2D" rows of bin/test_table.jl:94-104 -- match the oracle on the GPU, both directions, on the
+    reference corpus and the ct20stif stand-in."""
+    import torch
+    lim = lambda mdl, W: V.ConstrainedCost(mdl, V.VertexCount(), W)
+    b2, m2 = V.model_SparseMatrixVBC_blocks(), V.model_SparseMatrixVBC_memory(np.float64, np.int64)
+    packers = [None,
+               V.AlternatingPacker(V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks(), 4)),
+                                   V.DynamicTotalChunker(lim(V.permutedims(b2), 4)), V.DynamicTotalChunker(lim(b2, 4))),
+               V.AlternatingPacker(V.EquiChunker(1), V.EquiChunker(1), V.DynamicTotalChunker(lim(m2, 4)),
+                                   V.DynamicTotalChunker(lim(V.permutedims(m2), 4)), V.DynamicTotalChunker(lim(m2, 4)))]
+    mats = [g["A"] for g in golden.values()] + [V.synthetic.standin("Boeing/ct20stif").T.tocsc()]
+    rng = np.random.default_rng(8)
+    for A in mats:
+        for pk in packers:
+            B = V.SparseMatrixVBC[4, 4](A) if pk is None else V.SparseMatrixVBC[4, 4](A, pk)
+            R = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
+            for trans in (True, False):
+                nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+                x = rng.uniform(-1, 1, nx)
+                y = torch.zeros(ny, dtype=torch.float64, device="cuda:0")
+                V.mul_(y, B.T if trans else B, torch.from_numpy(x).cuda())
+                ref = O.mul(R, x, np.zeros(ny), trans=trans)
+                assert np.linalg.norm(y.cpu().numpy() - ref) <= 1e-12 * max(np.linalg.norm(ref), 1e-300)
+            B.release()

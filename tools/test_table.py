@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--fit-time-model", action="store_true", help="add the 'min time' row (fits the GPU model)")
     ap.add_argument("--no-2d", action="store_true")
+    ap.add_argument("--localities", default="uniform,banded", help="generators of the 1D time-model fit")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     import torch
@@ -150,7 +151,7 @@ def main():
                ("min blocks", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks()))),
                ("min memory", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_memory(dtype, np.int64))))]
     if args.fit_time_model:  # the reference's generator (uniform rows) and the banded one (costs.py)
-        for loc in ("uniform", "banded"):
+        for loc in args.localities.split(","):
             mdl = V.model_SparseMatrix1DVBC_TrSpMV_time(W, dtype, np.int64, dtype, locality=loc)
             methods.append((f"min time (GPU, {loc})", V.DynamicTotalChunker(lim(mdl))))
         # the candidates above and the two model partitions, timed on the GPU: the fastest wins
