@@ -583,7 +583,7 @@ def run_abi_sharded(args, world):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                                              "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)  # the line must not wait on a hang
     except subprocess.TimeoutExpired:
         return {"error": "timed out", "pass": False}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
