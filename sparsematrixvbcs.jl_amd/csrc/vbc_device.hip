@@ -417,7 +417,7 @@ static int slot_runs(const vbc_handle *h, const std::vector<Entry> &ents, const 
 static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vector<Entry> &ents,
                        const std::vector<int64_t> &sbeg0, const std::vector<int32_t> &out0, int64_t total_entries,
                        const char *val, Arena &ar, int &range0, PendingSlot &ps,
-                       const std::vector<int64_t> &order = {}, bool mask = false)
+                       const std::vector<int64_t> &order = {}, bool mask = false, int ks = 1)
 {
     const int esz = h->esz;
     // segment q of the layout is input segment order[q] (natural order when `order` is empty)
@@ -430,6 +430,15 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         out[q] = out0[o];
     }
     const int64_t nseg = (int64_t)sbeg.size() - 1;
+    int64_t nstripes = nseg;
+    if (ks > 1) {  // stripes cut into ks parts (build_ksplit): out / nseg per stripe, lanes 0 .. 64/ks - 1
+        const int m = 64 / ks;
+        std::vector<int32_t> os;
+        for (int64_t q = 0; q < nseg; q++)
+            if (q % 64 < m && out[q] >= 0) os.push_back(out[q]);
+        nstripes = (int64_t)os.size();
+        out.swap(os);
+    }
     const int64_t real = sbeg[nseg] - sbeg[0];
     const bool planar = slot_planar(h, kind, w);
     const int run = planar ? slot_runs(h, ents, sbeg0) : 1;  // sbeg0: the input order ents is in
@@ -532,7 +541,8 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.rpi = RPI;
     b.range0 = range0;
     b.nranges = (int32_t)nr;
-    b.nseg = (int32_t)nseg;
+    b.nseg = (int32_t)nstripes;
+    b.ks = ks;
     b.u = h->slot_u;
     b.diag = h->diag;
     b.xcd = (planar && split == 1) ? h->xcd_p : 0;  // split grids are small (one chunk per workgroup)
@@ -1150,6 +1160,48 @@ static void hole_runs(const vbc_handle *h, const Stripes &s, const std::vector<i
     }
 }
 
+// Long stripes of the fused split cut into ks parts (SlotBin::ks): each stripe's rows split at run
+// boundaries into ks parts of equal run counts (the last may be shorter), the stripes by decreasing
+// length, 64 / ks of them per chunk, part p of the chunk's stripe i in lane p * (64 / ks) + i; lanes past
+// the last stripe hold empty segments.  ents[sbeg[q] ..] are stripe q's rows, out[q] its first column.
+static int build_ksplit(vbc_handle *h, int w, int ks, const std::vector<Entry> &ents, const std::vector<int64_t> &sbeg,
+                        const std::vector<int32_t> &out, int64_t total, const char *val, Arena &ar, int &range0,
+                        PendingSlot &ps)
+{
+    const int64_t n = (int64_t)sbeg.size() - 1, m = 64 / ks;
+    const int R = slot_runs(h, ents, sbeg);
+    std::vector<int64_t> sx{0};  // segment bounds in ents order: stripe q's part p is segment q * ks + p
+    std::vector<int32_t> ox;
+    for (int64_t q = 0; q < n; q++) {
+        const int64_t runs = (sbeg[q + 1] - sbeg[q]) / R, per = (runs + ks - 1) / ks;
+        for (int p = 0; p < ks; p++) {
+            sx.push_back(sbeg[q] + std::min<int64_t>(runs, (p + 1) * per) * R);
+            ox.push_back(out[q]);
+        }
+    }
+    const int64_t nchk = (n + m - 1) / m;
+    for (int64_t t = n; t < nchk * m; t++)  // empty segments: stripe slots t >= n of the last chunk
+        for (int p = 0; p < ks; p++) {
+            sx.push_back(sx.back());
+            ox.push_back(-1);
+        }
+    std::vector<int64_t> byl(n);
+    for (int64_t q = 0; q < n; q++) byl[q] = q;
+    std::stable_sort(byl.begin(), byl.end(),
+                     [&](int64_t a, int64_t b) { return sbeg[a + 1] - sbeg[a] > sbeg[b + 1] - sbeg[b]; });
+    std::vector<int64_t> order((size_t)(nchk * 64));
+    for (int64_t c = 0; c < nchk; c++)
+        for (int p = 0; p < ks; p++)
+            for (int64_t i = 0; i < m; i++) {
+                const int64_t t = c * m + i;
+                order[c * 64 + p * m + i] = (t < n ? byl[t] : t) * ks + p;
+            }
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] long stripes: w %d, %lld stripes cut into %d parts (runs of %d), %lld chunks\n", w,
+                (long long)n, ks, R, (long long)nchk);
+    return build_slots(h, 0, w, w, ents, sx, ox, total, val, ar, range0, ps, order, false, ks);
+}
+
 // Transposed layout: segments = stripes of each width, entries = their stored rows.  A bucket runs
 // slotted (vbc_slots.h, every stripe of the width a segment, empty ones included) when its row counts
 // are near-uniform, else merged (non-empty stripes; empty ones go to the fill list).
@@ -1169,13 +1221,47 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     // at most half the wave slots (the split rule of build_slots) and every chunk keeps >= split_rows
     // (fp64) rows per wave; P is common to the launch.  VBC_SMALL_FUSE=0 turns it off.
     h->small_split = 0;
+    // Long stripes (SlotBin::ks): a chunk runs on one CU and costs its longest stripe's rows, so a few
+    // chunks of long stripes (a 'min blocks' partition's widest, fullest stripes: 3.4x the mean chunk on
+    // the ct20stif stand-in) set the product's time.  A stripe whose work (rows x width, values per
+    // lane) exceeds ksplit x the mean chunk's is cut into 2 (4 above twice that) parts of whole runs,
+    // laid side by side in the lanes of one chunk and summed across them before the store.
+    std::vector<uint8_t> kst;  // per stripe: parts (empty: none cut)
     // (auto layouts only: a forced VBC_SLOTS / VBC_SLOT_PLANAR keeps the layout the tests ask for)
     if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar < 0 && h->slots_mode < 0 && buckets.size() >= 2 &&
         (int)buckets.size() <= kSplitParts && buckets.rbegin()->first <= 8 && !sweep_possible(h, 1, s.m)) {
+        if (h->ksplit > 0) {
+            double work = 0;
+            int64_t nw = 0;
+            for (auto &kv : buckets) {  // chunks of the length-sorted buckets
+                std::vector<int64_t> len;
+                for (int64_t l : kv.second) len.push_back(s.rbeg[l + 1] - s.rbeg[l]);
+                std::sort(len.begin(), len.end(), std::greater<int64_t>());
+                for (size_t i = 0; i < len.size(); i += 64, nw++) work += (double)len[i] * kv.first;
+            }
+            const double thr = h->ksplit * work / (double)std::max<int64_t>(nw, 1);
+            kst.assign(s.L, 1);
+            int parts = 0, cut = 0;
+            for (auto &kv : buckets) {
+                int cls = 0;
+                for (int64_t l : kv.second) {
+                    const double wk = (double)(s.rbeg[l + 1] - s.rbeg[l]) * kv.first;
+                    kst[l] = wk > 2 * thr ? 4 : wk > thr ? 2 : 1;
+                    cls |= kst[l];
+                }
+                parts += __builtin_popcount(cls);
+                cut += cls > 1;
+            }
+            if (parts > kSplitParts || cut == 0 || !(thr > 0)) kst.clear();
+        }
         int64_t nch = 0, rows = 0;
         for (auto &kv : buckets) {
-            nch += ((int64_t)kv.second.size() + 63) / 64;
-            for (int64_t l : kv.second) rows += s.rbeg[l + 1] - s.rbeg[l];
+            int64_t cnt[5] = {0, 0, 0, 0, 0};
+            for (int64_t l : kv.second) {
+                cnt[kst.empty() ? 1 : kst[l]]++;
+                rows += s.rbeg[l + 1] - s.rbeg[l];
+            }
+            for (int k = 1; k <= 4; k *= 2) nch += (cnt[k] * k + 63) / 64;
         }
         const double slots = (double)h->target_ranges_p;
         const double avg = (double)rows / (double)std::max<int64_t>(nch, 1) / 64.0 * 1.1;  // rows per chunk (sorted)
@@ -1188,11 +1274,32 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             if (h->planar_split > 1) P = h->planar_split;
             if (P > 1) h->small_split = P;
         }
+        if (h->small_split <= 1) kst.clear();
         if (getenv("VBC_VERBOSE"))
-            fprintf(stderr, "[vbc] small fused split: %d buckets, %lld chunks, %.1f rows per chunk -> P = %d\n",
-                    (int)buckets.size(), (long long)nch, avg, h->small_split);
+            fprintf(stderr, "[vbc] small fused split: %d buckets, %lld chunks, %.1f rows per chunk -> P = %d%s\n",
+                    (int)buckets.size(), (long long)nch, avg, h->small_split, kst.empty() ? "" : ", long stripes cut");
     }
+    // the bins: a width bucket, or (long stripes cut) its stripes of each part count ks
+    std::vector<std::pair<int, std::vector<int64_t>>> subs;
+    std::vector<int> subk;
     for (auto &kv : buckets) {
+        if (kst.empty()) {
+            subs.emplace_back(kv.first, std::move(kv.second));
+            subk.push_back(1);
+            continue;
+        }
+        for (int k = 1; k <= 4; k *= 2) {
+            std::vector<int64_t> v;
+            for (int64_t l : kv.second)
+                if (kst[l] == k) v.push_back(l);
+            if (v.empty()) continue;
+            subs.emplace_back(kv.first, std::move(v));
+            subk.push_back(k);
+        }
+    }
+    for (size_t si = 0; si < subs.size(); si++) {
+        const auto &kv = subs[si];
+        const int ks = subk[si];
         const int w = kv.first;
         if (sweep_possible(h, w, s.m)) {
             std::vector<int64_t> sb{0};
@@ -1226,6 +1333,23 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         std::vector<int64_t> hsbeg;
         if (h->small_split > 1 && slot_planar(h, 0, w)) hole_runs(h, s, kv.second, w, hents, hsbeg);
         const std::vector<int64_t> &sb = hsbeg.empty() ? sbeg : hsbeg;
+        if (ks > 1) {  // long stripes of the fused split, cut into ks lane parts
+            std::vector<Entry> ents;
+            std::vector<int32_t> out;
+            for (int64_t l : kv.second) out.push_back((int32_t)s.col0[l]);
+            if (!hsbeg.empty()) {
+                ents.swap(hents);
+                sbeg.swap(hsbeg);
+            } else {
+                for (int64_t l : kv.second)
+                    for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
+                        ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+            }
+            PendingSlot ps;
+            if (int st = build_ksplit(h, w, ks, ents, sbeg, out, total, val, ar, srange0, ps)) return st;
+            pss.push_back(std::move(ps));
+            continue;
+        }
         if (want_slots(h, 0, wps, sb, hsbeg.empty() ? total : total + (hsbeg.back() - sbeg.back()), s.m, order, &mask)) {
             std::vector<Entry> ents;
             std::vector<int32_t> out;
@@ -1957,7 +2081,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
             int c0 = 0;
             for (size_t i = 0; i < L.pbins.size(); i++) {
                 const SlotBin &b = L.pbins[i];
-                M.p[i] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst, b.holes, 0,
+                M.p[i] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst, b.holes, b.ks,
                                    b.rrow, b.key, b.val, b.out};
                 c0 += b.nranges;  // a split bin's ranges are its chunks
             }
@@ -2160,6 +2284,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
+    if (const char *e = getenv("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
     if (const char *e = getenv("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));
@@ -2501,6 +2626,9 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
             if (b.lanes) info->planar_mask |= 4;
         }
     if (h->has_t && h->lt.fuse_split) info->planar_mask |= 32;  // the B'x planar bins run as one fused split launch
+    if (h->has_t)
+        for (const SlotBin &b : h->lt.pbins)
+            if (b.ks > 1) info->planar_mask |= 64;  // long stripes cut into lane parts (SlotBin::ks)
     info->fwd_run = 1;
     if (h->has_f)
         for (const auto &l : h->lf)

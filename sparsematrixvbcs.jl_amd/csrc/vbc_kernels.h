@@ -97,6 +97,9 @@ struct SlotBin {
     int32_t xcd;         // planar: XCD-contiguous workgroup order (xcd_block)
     int32_t holes;       // planar split runs with holes: a run's first key holds, in bits 27..29, which of its
                          // RUN rows the stripe stores (the others: zero values, x taken as 0); index bits 0..26
+    int32_t ks;          // planar split: > 1 = every stripe cut into ks parts of whole runs, part h of the
+                         // chunk's stripe i in lane h * (64 / ks) + i (long stripes of the fused split; the
+                         // parts are summed across lanes before the store), out / nseg per stripe
     int32_t mask;        // planar: chunk-local length order (lanes of a chunk by decreasing length, the chunk's
                          // 64 stripes kept) and nlive[row] = live lanes of the chunk row; dead lanes read
                          // lane 0's key and values (no extra lines fetched) and fold nothing (vbc_planar.h)
@@ -125,10 +128,11 @@ constexpr uint32_t kHoleIdx = (1u << 27) - 1;
 constexpr int kHoleShift = 27;
 
 // The parts of a fused split launch (vbc_planar.h spmv_split_multi): up to kSplitParts planar split
-// bins of a small matrix, their chunks concatenated (part k owns chunks [chunk0, next chunk0)).
-constexpr int kSplitParts = 8;
+// bins of a small matrix, their chunks concatenated (part k owns chunks [chunk0, next chunk0)).  A width
+// bucket may give up to three parts (its stripes cut into ks = 1, 2 or 4 parts, SlotBin::ks).
+constexpr int kSplitParts = 16;
 struct SplitPart {
-    int32_t w, run, chunk0, nseg, out_affine, out_base, out_stride, wst, holes, pad;
+    int32_t w, run, chunk0, nseg, out_affine, out_base, out_stride, wst, holes, ks;
     const int32_t *rrow;
     const uint32_t *key;
     const void *val;

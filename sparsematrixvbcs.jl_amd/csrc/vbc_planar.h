@@ -1060,7 +1060,7 @@ struct SplitView {
     const uint32_t *base;
     const uint32_t *kdoff;
     const int32_t *out;
-    int32_t nseg, out_affine, out_base, out_stride, wst, holes;
+    int32_t nseg, out_affine, out_base, out_stride, wst, holes, ks;
 };
 
 // Keys and values are CACHED loads here (the streaming kernels use non-temporal ones): a split bucket
@@ -1254,7 +1254,14 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
     for (int q = 0; q < P - 1; q++)
 #pragma unroll
         for (int k = 0; k < W_; k++) acc[k] += part[(q * W_ + k) * 64 + lane];
-    const int seg = c * 64 + lane;
+    // stripes cut into ks parts (SlotBin::ks): part h of stripe i sits in lane h * m + i; a fixed tree
+    // over the lanes (m apart, then 2m, ...) sums them, the same order for every stripe and every call
+    const int m = b.ks > 1 ? 64 / b.ks : 64;
+    for (int d = m; d < 64; d *= 2)
+#pragma unroll
+        for (int k = 0; k < W_; k++) acc[k] += __shfl_xor(acc[k], d, 64);
+    if (lane >= m) return;
+    const int seg = c * m + lane;
     if (seg >= b.nseg) return;
     if (DIAG == 3 && acc[0] != T(-12345.678)) return;
     const int o = b.out_affine ? b.out_base + seg * b.out_stride : G(b.out)[seg];
@@ -1277,7 +1284,7 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_split(const SlotBin b, con
     if (c >= b.nranges) return;
     __shared__ T part[(P > 1 ? P - 1 : 1) * 64 * W_];
     const SplitView v{b.rrow, b.key, b.val, b.base, b.kdoff, b.out, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst,
-                      b.holes};
+                      b.holes, b.ks};
     if (!KC && DIAG == 0 && b.deep == 1)  // SlotBin::deep on a split bin: 1 pipelined, 2 batched slice loop
         split_chunk<T, W_, KC, RUN, P, DIAG, 1>(v, c, threadIdx.x >> 6, threadIdx.x & 63, x, y, alpha, beta, rd_i, part);
     else if (!KC && DIAG == 0 && b.deep == 2)
@@ -1311,10 +1318,13 @@ __global__ __launch_bounds__(64 * P) void spmv_split_multi(const SplitMulti M, c
     case K: {                                                                                                     \
         const SplitPart &q = M.p[K];                                                                              \
         w = q.w; run = q.run; chunk0 = q.chunk0;                                                                  \
-        v = SplitView{q.rrow, q.key, q.val, nullptr, nullptr, q.out, q.nseg, q.out_affine, q.out_base, q.out_stride, q.wst, q.holes}; \
+        v = SplitView{q.rrow, q.key, q.val, nullptr, nullptr, q.out, q.nseg, q.out_affine, q.out_base, q.out_stride, q.wst, q.holes, q.ks}; \
         break;                                                                                                    \
     }
-    switch (i) { VBC_PART(0) VBC_PART(1) VBC_PART(2) VBC_PART(3) VBC_PART(4) VBC_PART(5) VBC_PART(6) VBC_PART(7) }
+    switch (i) {
+        VBC_PART(0) VBC_PART(1) VBC_PART(2) VBC_PART(3) VBC_PART(4) VBC_PART(5) VBC_PART(6) VBC_PART(7)
+        VBC_PART(8) VBC_PART(9) VBC_PART(10) VBC_PART(11) VBC_PART(12) VBC_PART(13) VBC_PART(14) VBC_PART(15)
+    }
 #undef VBC_PART
     __shared__ T part[(P > 1 ? P - 1 : 1) * 64 * 8];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = c - chunk0;

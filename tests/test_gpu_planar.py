@@ -729,3 +729,96 @@ def test_fused_split_runs_with_holes_nonfinite(monkeypatch):
     assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
     fin = np.isfinite(ref)
     assert np.array_equal(got[fin], ref[fin])
+
+
+def _node_stripes(rng, N, L, widths, nodes_of, hole_every):
+    """Stripes of node runs (rows 3 k .. 3 k + 2 of each chosen node), every hole_every-th missing one row."""
+    rows = []
+    for l in range(L):
+        nodes = np.sort(rng.choice(N, nodes_of(l), replace=False))
+        r = (nodes[:, None] * 3 + np.arange(3)[None, :]).reshape(-1)
+        if l % hole_every == 0:
+            r = np.delete(r, rng.integers(0, len(r)))
+        rows.append(r)
+    cnt = np.array([len(r) for r in rows])
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)])
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * widths)])
+    spl = np.concatenate([[1], 1 + np.cumsum(widths)])
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + 8)
+    val[:nv] = rng.integers(-8, 9, nv)
+    B = V.SparseMatrix1DVBC(8, 3 * N, int(spl[-1] - 1), V.SplitPartition(spl), pos, np.concatenate(rows) + 1, ofs, val)
+    return B, rows
+
+
+def test_fused_split_long_stripes_cut(monkeypatch):
+    """Long stripes of the fused split (SlotBin::ks, vbc_info planar_mask bit 6): a stripe whose rows x
+    width exceed 1.5x the mean chunk's is cut into 2 / 4 parts of whole runs, laid in the lanes of one
+    chunk and summed across the lanes before the store.  Exact on integer data (runs with holes, a NaN /
+    Inf at rows a long stripe does not store), the same bits on every call, and VBC_KSPLIT=0 keeps every
+    stripe whole with the same exact result."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "4")
+    rng = np.random.default_rng(45)
+    N, L = 600, 400
+    widths = 1 + np.arange(L) % 3
+    B, rows = _node_stripes(rng, N, L, widths, lambda l: 80 if l % 29 == 0 else (30 if l % 13 == 0 else 8), 7)
+    inf = B.info(trans=True)
+    assert inf["planar_mask"] & 32 and inf["planar_mask"] & 64 and inf["planar_run"] == 3
+    R = ref_of(B)
+    x = rng.integers(-8, 9, B.m).astype(np.float64)
+    ref = O.mul(R, x, np.zeros(B.n), trans=True)
+    y = torch.full((B.n,), float("nan"), dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert np.array_equal(y.cpu().numpy(), ref)
+    y2 = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    xr = rng.uniform(-1, 1, B.m)
+    V.mul_(y, B.T, dev(xr))
+    V.mul_(y2, B.T, dev(xr))
+    assert np.array_equal(y.cpu().numpy(), y2.cpu().numpy())  # deterministic
+    assert rel(y.cpu().numpy(), O.mul(R, xr, np.zeros(B.n), trans=True)) <= TOL64
+    # a NaN / Inf in a hole of a long stripe's run reaches nothing that stripe writes
+    long_holes = [r for l in range(0, L, 7 * 29) for r in range(3 * (rows[l][0] // 3), 3 * (rows[l][-1] // 3) + 3)
+                  if r not in set(rows[l].tolist()) and (r // 3) in set((rows[l] // 3).tolist())]
+    assert long_holes
+    xn = x.copy()
+    xn[long_holes[0]] = np.nan
+    xn[long_holes[-1]] = np.inf
+    V.mul_(y, B.T, dev(xn))
+    refn = O.mul(R, xn, np.zeros(B.n), trans=True)
+    got = y.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(refn)) and np.array_equal(np.isinf(got), np.isinf(refn))
+    assert np.array_equal(got[np.isfinite(refn)], refn[np.isfinite(refn)])
+    # alpha / beta on the cut stripes
+    y0 = rng.integers(-8, 9, B.n).astype(np.float64)
+    yb = dev(y0.copy())
+    V.mul_(yb, B.T, dev(x), 2.0, -1.0)
+    assert np.array_equal(yb.cpu().numpy(), O.mul(R, x, y0.copy(), 2.0, -1.0, trans=True, ref_semantics=False))
+    monkeypatch.setenv("VBC_KSPLIT", "0")
+    Bw = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+    assert Bw.info(trans=True)["planar_mask"] & 32 and not Bw.info(trans=True)["planar_mask"] & 64
+    yw = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(yw, Bw.T, dev(x))
+    assert np.array_equal(yw.cpu().numpy(), ref)
+
+
+def test_fused_split_min_blocks_partition():
+    """The ct20stif stand-in under the reference's 'min blocks' partition (bin/test_table.jl:67-69: widths
+    1..8, its widest stripes the fullest) cuts its long stripes (planar_mask bit 6) and matches the oracle
+    in fp64 and fp32."""
+    A = V.synthetic.standin("Boeing/ct20stif", np.float64)
+    meth = V.DynamicTotalChunker(V.ConstrainedCost(V.model_SparseMatrix1DVBC_blocks(), V.VertexCount(), 8))
+    B = V.SparseMatrix1DVBC[8](A, meth)
+    inf = B.info(trans=True)
+    assert inf["planar_mask"] & 32 and inf["planar_mask"] & 64
+    rng = np.random.default_rng(46)
+    R = ref_of(B)
+    x = rng.uniform(-1, 1, B.m)
+    y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert rel(y.cpu().numpy(), O.mul(R, x, np.zeros(B.n), trans=True)) <= TOL64
+    B32 = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val.astype(np.float32))
+    x32 = x.astype(np.float32)
+    y32 = torch.zeros(B.n, dtype=torch.float32, device=DEV)
+    V.mul_(y32, B32.T, dev(x32))
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B32.val.astype(np.float64))
+    assert rel(y32.cpu().numpy(), O.mul(R64, x32.astype(np.float64), np.zeros(B.n), trans=True)) <= TOL32

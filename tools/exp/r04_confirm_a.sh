@@ -13,4 +13,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 G="TCC_EA0_RDREQ_sum,TCC_BUBBLE_sum,TCC_EA0_RDREQ_32B_sum,TCC_EA0_RDREQ_DRAM_sum;TCC_HIT_sum,TCC_MISS_sum"
 timeout -k 10 400 python -u tools/pmc_traffic.py --counters "$G" --workload c5-mesh --dtype f32 --kernel spmm_panel \
     --read-factor 1 > gpurun_out/${tag}_pmc_c5mesh.log 2>&1 || exit $?
+bash tools/exp/r04_pmc_lat_c5.sh || exit $?
 exit $rc
