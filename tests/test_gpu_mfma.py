@@ -177,3 +177,23 @@ def test_mfma_host_memory_and_info():
     assert rel(Y, ref_cols(R, X, np.zeros((B.n, 16)), 1.0, 0.0)) <= TOL64
     inf = B.info(multi=True)
     assert inf["bins_m"] == 1 and inf["bins_t"] == 0 and inf["bytes_m"] > 0
+
+
+@pytest.mark.parametrize("workload,scale", [("c5", 0.1), ("c5-mesh", 0.05)])
+def test_c5_panels_scaled_every_column(workload, scale):
+    """The bench's C5 inputs at reduced scale (the random 8x8-tile generator, costs.jl:200-220, 1e7 values;
+    the structured 3x3 node-tile mesh, 5e6), 16 row-major right-hand sides through the matrix-core panel
+    product, B'X and B X: every column against the oracle (fp32 vs the fp64 product, normwise 1e-5)."""
+    import bench
+    B = bench.build_matrix(workload, np.float32, scale)
+    rng = np.random.default_rng(47)
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        X = rng.uniform(-1, 1, (nx, 16)).astype(np.float32)
+        Y = torch.empty((ny, 16), dtype=torch.float32, device=DEV)
+        V.mul_(Y, B.T if trans else B, torch.from_numpy(X).to(DEV))
+        got = Y.cpu().numpy()
+        Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+        for j in range(16):
+            ref = O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64), np.zeros(ny), trans=trans)
+            assert rel(got[:, j], ref) <= TOL32, (trans, j)
