@@ -152,7 +152,7 @@ struct vbc_handle {
     int small_fuse = 1;               // VBC_SMALL_FUSE: 0 = never fuse the buckets of a small matrix
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split
-    double ksplit = 1.5;              // VBC_KSPLIT: fused split stripes above this x the mean chunk work are cut
+    double ksplit = 1.0;              // VBC_KSPLIT: fused split stripes above this x the mean chunk work are cut
                                       // into 2 / 4 lane parts (SlotBin::ks; 0: never)
     int split_pipe = -1;              // VBC_SPLIT_PIPE: split bins' pipelined slice loop (-1 auto, 0 off, 1 on)
     int split_rows = 12;              // VBC_SPLIT_ROWS: fewest chunk rows per wave of an automatic split

@@ -8,7 +8,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERN = {"probe": "probe", "ns": "spmv_sweep", "fe": "spmv_slots"}
+KERN = {"probe": "probe", "ns": "spmv_sweep", "fe": "spmv_slots", "c5": "spmm_panel", "c5mesh": "spmm_panel"}
 out = {}
 for d in sorted(glob.glob(sys.argv[1] + "/r04_lat_*")):
     if d.endswith(".log"):
