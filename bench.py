@@ -105,8 +105,11 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
     return V.synthetic.north_star(dtype=dtype, scale=scale, seed=seed, mixed=(workload == "ns-mixed"))
 
 
-def kernel_name(B, local, k):
+def kernel_name(B, local, k, trans=True):
     if k > 1:
+        if B.info(local, trans, multi=True)["planar_mask"] & 128:
+            return ("vbc::spmm_quads<T, W, VEC> (VALU stripe quads: 16 stripes x 4 right-hand-side quads per wave, "
+                    "csrc/vbc_panel.h)")
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     inf = B.info(local, True)
     if inf["planar_bins"] > 0:
@@ -318,7 +321,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
         "gflops": round(2.0 * nnz * k * steps / elapsed / 1e9, 2),
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel_name(B, local, k),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel_name(B, local, k, trans),
             "bytes_per_launch": bytes_roof, "avg_launch_ms": round(kernel_ms, 5), "traffic_source": traffic_src,
         },
         "config": {

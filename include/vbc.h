@@ -299,7 +299,9 @@ typedef struct vbc_info {
                                the forward planar bucket runs the split product (P waves per chunk);
                                bit 4: the forward bucket in lane streams (node blocks transposed);
                                bit 5: a small matrix's B'x buckets of every width (1..8) laid out planar
-                               and split, run by ONE fused launch (planar_split = its P) */
+                               and split, run by ONE fused launch (planar_split = its P); bit 6: some of
+                               those stripes cut into 2 / 4 lane parts (long stripes); bit 7: the multi-RHS
+                               layout has VALU stripe-quad buckets (widths <= 8, spmm_quads) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

@@ -1763,8 +1763,78 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
 
 struct PendingPanel {
     PanelBin b;
+    QuadBin qb;  // quad: a stripe-quad bucket (o_rgrp = its chunk rows)
+    bool quad;
     size_t o_key, o_val, o_out, o_rgrp, o_rseg;
 };
+
+// Stripe-quad bucket (vbc_panel.h spmm_quads): chunks of 16 stripes of width w <= 8, chunk rows = its
+// longest stripe's, rows x 16 keys (x row or kPanelSentinel) and rows x 16 x w values.  Natural stripe
+// order when the chunks pad <= slots_pad, else by decreasing length inside windows of 32 chunks.
+static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<int64_t> &stripes, int w, const char *val,
+                        Arena &ar, PendingPanel &pp)
+{
+    const int esz = h->esz;
+    const int64_t n = (int64_t)stripes.size();
+    std::vector<int64_t> sbeg{0};
+    for (int64_t l : stripes) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
+    std::vector<int64_t> order;
+    auto padded = [&](const std::vector<int64_t> &sb) {
+        int64_t rows = 0;
+        for (int32_t c : chunk_rows(sb, 16)) rows += c;
+        return rows * 16;
+    };
+    if ((double)padded(sbeg) > h->slots_pad * (double)std::max<int64_t>(sbeg[n], 1)) order = sorted_order(sbeg, 16);
+    std::vector<int64_t> ord(n);
+    for (int64_t i = 0; i < n; i++) ord[i] = order.empty() ? i : order[i];
+    const int64_t nch = (n + 15) / 16;
+    std::vector<int32_t> crow{0}, out(n);
+    for (int64_t c = 0; c < nch; c++) {
+        int64_t len = 0;
+        for (int64_t i = c * 16; i < std::min(n, c * 16 + 16); i++) {
+            const int64_t l = stripes[ord[i]];
+            len = std::max<int64_t>(len, s.rbeg[l + 1] - s.rbeg[l]);
+        }
+        crow.push_back((int32_t)(crow.back() + len));
+    }
+    for (int64_t i = 0; i < n; i++) out[i] = (int32_t)s.col0[stripes[ord[i]]];
+    const int64_t rows = crow.back();
+    pp = PendingPanel{};
+    pp.quad = true;
+    QuadBin &b = pp.qb;
+    b.w = w;
+    b.nchunks = (int32_t)nch;
+    b.nseg = (int32_t)n;
+    b.out_affine = 1;
+    b.out_base = n > 0 ? out[0] : 0;
+    b.out_stride = n > 1 ? out[1] - out[0] : 0;
+    for (int64_t i = 1; i < n && b.out_affine; i++) b.out_affine = (int64_t)out[i] == (int64_t)out[0] + i * b.out_stride;
+    pp.o_key = ar.reserve(std::max<int64_t>(rows, 1) * 16 * 4);
+    pp.o_val = ar.reserve(std::max<int64_t>(rows, 1) * 16 * w * esz);
+    pp.o_out = ar.reserve(std::max<int64_t>(n, 1) * 4);
+    pp.o_rgrp = ar.reserve(crow.size() * 4);
+    std::memcpy(ar.at<int32_t>(pp.o_out), out.data(), out.size() * 4);
+    std::memcpy(ar.at<int32_t>(pp.o_rgrp), crow.data(), crow.size() * 4);
+    uint32_t *key = ar.at<uint32_t>(pp.o_key);
+    char *vv = ar.at<char>(pp.o_val);
+    for (int64_t c = 0; c < nch; c++)
+        for (int64_t r = crow[c]; r < crow[c + 1]; r++)
+            for (int sl = 0; sl < 16; sl++) {
+                const int64_t i = c * 16 + sl, e = r * 16 + sl, k = r - crow[c];
+                const int64_t l = i < n ? stripes[ord[i]] : -1;
+                if (l >= 0 && s.rbeg[l] + k < s.rbeg[l + 1]) {
+                    key[e] = (uint32_t)s.rows[s.rbeg[l] + k];
+                    std::memcpy(vv + e * w * esz, val + (s.voff[l] + k * s.w[l]) * esz, (size_t)w * esz);
+                } else {
+                    key[e] = kPanelSentinel;
+                    std::memset(vv + e * w * esz, 0, (size_t)w * esz);
+                }
+            }
+    h->bytes_m += rows * 16 * (4 + (int64_t)w * esz) + n * 4;
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] stripe quads: w %d, %lld stripes, %lld chunks, %lld rows (%s order, %lld real)\n", w,
+                (long long)n, (long long)nch, (long long)rows, order.empty() ? "natural" : "sorted", (long long)sbeg[n]);
+}
 
 // Panel layout (vbc_panel.h) of the transposed product: per width bucket (stripes wider than 16 are
 // cut into 16-column pieces that share the stripe's rows), S = 16/w consecutive stripes per panel,
@@ -1786,7 +1856,9 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     // groups of every bucket first: ranges are spread over the launch in proportion to them
     std::map<int, std::vector<int64_t>> pgroups;  // w -> groups per panel
     int64_t total_groups = 0;
+    auto quads = [&](int w) { return w <= h->panel_quads && w <= 8; };  // VALU stripe quads (spmm_quads)
     for (auto &kv : buckets) {
+        if (quads(kv.first)) continue;
         const int S = 16 / kv.first;
         auto &pg = pgroups[kv.first];
         for (size_t p0 = 0; p0 < kv.second.size(); p0 += S) {
@@ -1800,6 +1872,14 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     if (total_groups >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "matrix too large for the panel layout");
     int range0 = 0;
     for (auto &kv : buckets) {
+        if (quads(kv.first)) {  // w <= 8: every piece is a whole stripe
+            std::vector<int64_t> st;
+            for (const Piece &pc : kv.second) st.push_back(pc.l);
+            PendingPanel pp;
+            build_quads(h, s, st, kv.first, val, ar, pp);
+            pps.push_back(pp);
+            continue;
+        }
         const int w = kv.first, S = 16 / w;
         const std::vector<Piece> &pcs = kv.second;
         const std::vector<int64_t> &pg = pgroups[w];
@@ -1999,8 +2079,18 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
 static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, PanelLaunch &L)
 {
     L.bins.clear();
+    L.qbins.clear();
     char *base = static_cast<char *>(h->d_arena);
     for (const PendingPanel &pp : pps) {
+        if (pp.quad) {
+            QuadBin q = pp.qb;
+            q.key = reinterpret_cast<const uint32_t *>(base + pp.o_key);
+            q.val = base + pp.o_val;
+            q.out = reinterpret_cast<const int32_t *>(base + pp.o_out);
+            q.crow = reinterpret_cast<const int32_t *>(base + pp.o_rgrp);
+            L.qbins.push_back(q);
+            continue;
+        }
         PanelBin b = pp.b;
         b.key = reinterpret_cast<const uint32_t *>(base + pp.o_key);
         b.val = base + pp.o_val;
@@ -2302,6 +2392,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
         if (const char *e = getenv("VBC_PANEL_DIAG")) h->panel_valu |= atoi(e) & ~1;
         if (const char *e = getenv("VBC_PANEL_NOBUF")) h->panel_nobuf = atoi(e) != 0;
+        if (const char *e = getenv("VBC_PANEL_QUADS")) h->panel_quads = atoi(e);
     }
 
     Arena ar;
@@ -2606,7 +2697,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->device_bytes = (int64_t)h->arena_bytes;
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
-    info->bins_m = h->has_m ? (int32_t)h->lm.bins.size() : h->has_mf ? (int32_t)h->lmf.bins.size() : 0;
+    info->bins_m = h->has_m ? (int32_t)(h->lm.bins.size() + h->lm.qbins.size())
+                 : h->has_mf ? (int32_t)(h->lmf.bins.size() + h->lmf.qbins.size()) : 0;
+    if ((h->has_m && !h->lm.qbins.empty()) || (h->has_mf && !h->lmf.qbins.empty()))
+        info->planar_mask |= 128;  // multi-RHS buckets in the VALU stripe-quad layout (spmm_quads)
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)(l.sbins.size() + l.pbins.size()) : 0;  // + planar forward
     info->slot_bins = sl;

@@ -56,6 +56,7 @@ struct Launch {
 struct PanelLaunch {
     std::vector<PanelBin> bins;
     PanelBin *d_bins = nullptr;
+    std::vector<QuadBin> qbins;  // stripe-quad buckets (VALU, w <= 8): one launch each
     int total_ranges = 0;
     int nfill = 0;
     size_t o_fill = 0;
@@ -102,6 +103,7 @@ struct vbc_handle {
     int target_ranges_m = 4096;
     int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
+    int panel_quads = 8;          // VBC_PANEL_QUADS: widest stripe of the VALU stripe-quad layout (0: MFMA panels only)
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch

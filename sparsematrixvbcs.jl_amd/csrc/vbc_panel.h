@@ -343,6 +343,166 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
     flush_general(segc - ((segc - 1) / S) * S);  // the last panel (the bin's last may hold < S stripes)
 }
 
+// Stripe-quad layout (round 4; VALU multi-RHS product for stripes of width w <= 8).  An f32 MFMA has no
+// throughput edge over the f32 VALU on gfx950 (both 64 flop / clk / SIMD), and the panel's 16 x 16 x 4
+// MFMA puts only w of its 16 M rows to use (w = 3 node tiles: 19 %), so narrow stripes run on the VALU:
+// a wave owns a chunk of 16 stripes, lane 4 s + q holds stripe s's output columns for right-hand sides
+// 4 q .. 4 q + 3 (w x 4 accumulators), and steps through the chunk's rows in stored order -- per row one
+// key (its x row), the w values (lane q loads component q (and q + 4); a DPP quad broadcast hands each
+// component to the stripe's 4 lanes) and one 16-B gather of the quad's 4 right-hand sides, folded by
+// w x 4 fmas.  Rows of a chunk: its longest stripe's; shorter stripes pad with the sentinel key (x read
+// as 0 past the buffer, zero values).  Each column is one fma chain over the stripe's rows in stored
+// order (the reference's multiply_VBC.jl:93-147 order per column), deterministic, and a non-finite x
+// reaches only the stripes that store its row.
+struct QuadBin {
+    int32_t w;            // stripe width (1..8)
+    int32_t nchunks;      // chunks of 16 stripes
+    int32_t nseg;         // stripes
+    int32_t out_affine;   // out[s] == out_base + s * out_stride
+    int32_t out_base;
+    int32_t out_stride;
+    const int32_t *crow;  // nchunks + 1: first row of each chunk
+    const uint32_t *key;  // rows x 16: x row, or kPanelSentinel
+    const void *val;      // rows x 16 x w values
+    const int32_t *out;   // per stripe: first y column
+};
+
+// v from lane (lane & ~3) | C of its quad (DPP quad_perm [C, C, C, C])
+template <int C, typename T>
+__device__ __forceinline__ T quad_bcast(T v)
+{
+    constexpr int ctrl = C | (C << 2) | (C << 4) | (C << 6);
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false));
+    } else {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, ctrl, 0xF, 0xF, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), ctrl, 0xF, 0xF, false);
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T quad_bcast_rt(T v, int c)
+{
+    switch (c & 3) {
+    case 0: return quad_bcast<0>(v);
+    case 1: return quad_bcast<1>(v);
+    case 2: return quad_bcast<2>(v);
+    default: return quad_bcast<3>(v);
+    }
+}
+
+#ifndef VBC_QUAD_BATCH
+#define VBC_QUAD_BATCH 8
+#endif
+
+// VEC: X and Y row-major with contiguous right-hand sides (column stride 1), 16-B aligned rows, nrhs a
+// multiple of 4, X below 2 GiB: 16-B buffer gathers (past X for padding rows: zeros) and 16-B stores;
+// otherwise one element at a time through 64-bit addresses.
+template <typename T, int W, bool VEC>
+__global__ __launch_bounds__(kBlockThreads) void spmm_quads(const QuadBin b, const T *__restrict__ X, int64_t sxr,
+                                                            int64_t sxc, uint32_t xbytes, T *__restrict__ Y, int64_t syr,
+                                                            int64_t syc, int nrhs, T alpha, T beta, int rd_i)
+{
+    const int c = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    if (c >= b.nchunks) return;
+    const int lane = threadIdx.x & 63, s = lane >> 2, q = lane & 3;
+    const int r0 = __builtin_amdgcn_readfirstlane(G(b.crow)[c]), r1 = __builtin_amdgcn_readfirstlane(G(b.crow)[c + 1]);
+    constexpr int esz = (int)sizeof(T);
+    constexpr int NV = (W + 3) / 4;  // value components per lane per row
+    constexpr int NB = sizeof(T) == 4 ? VBC_QUAD_BATCH : (VBC_QUAD_BATCH + 1) / 2;
+    const bool qlive = 4 * q < nrhs;
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const gptr<const T> xg = G(X);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(X), 0, (int)xbytes, 0x00020000);
+    const uint32_t sxr_b = (uint32_t)(sxr * esz), qoff = (uint32_t)(4 * q * esz);
+    T acc[W][4];
+#pragma unroll
+    for (int k = 0; k < W; k++)
+#pragma unroll
+        for (int t = 0; t < 4; t++) acc[k][t] = T(0);
+    for (int r = r0; r < r1; r += NB) {
+        uint32_t kk[NB];
+        T v[NB][NV], xv[NB][4];
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const size_t rr = (size_t)min(r + j, r1 - 1) * 16 + s;
+            kk[j] = key[rr];
+#pragma unroll
+            for (int u = 0; u < NV; u++) v[j][u] = val[rr * W + min(4 * u + q, W - 1)];
+        }
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const bool ok = r + j < r1 && kk[j] != kPanelSentinel && qlive;
+            if constexpr (VEC) {
+                const uint32_t xo = ok ? kk[j] * sxr_b + qoff : xbytes;  // past X: zeros
+                if constexpr (sizeof(T) == 4) {
+                    typedef float f4 __attribute__((ext_vector_type(4)));
+                    const f4 t4 = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
+#pragma unroll
+                    for (int t = 0; t < 4; t++) xv[j][t] = t4[t];
+                } else {
+                    typedef double d2 __attribute__((ext_vector_type(2)));
+                    const d2 a = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
+                    const d2 bb = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xo + 16 : xbytes, 0, 0));
+                    xv[j][0] = a[0];
+                    xv[j][1] = a[1];
+                    xv[j][2] = bb[0];
+                    xv[j][3] = bb[1];
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int col = 4 * q + t;
+                    xv[j][t] = (ok && col < nrhs) ? xg[(int64_t)kk[j] * sxr + (int64_t)col * sxc] : T(0);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const bool live = r + j < r1;  // rows past the chunk (the batch's clamped tail): no-ops
+#pragma unroll
+            for (int k = 0; k < W; k++) {
+                const T vk = quad_bcast_rt(v[j][k >> 2], k);
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const T nv = fmadd(vk, xv[j][t], acc[k][t]);
+                    acc[k][t] = live ? nv : acc[k][t];
+                }
+            }
+        }
+    }
+    const int seg = c * 16 + s;
+    if (seg >= b.nseg || !qlive) return;
+    const int64_t o = b.out_affine ? (int64_t)b.out_base + (int64_t)seg * b.out_stride : (int64_t)G(b.out)[seg];
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+        gptr<T> yo = G(Y) + (o + k) * syr;
+        if constexpr (VEC) {
+            T o4[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) o4[t] = alpha * acc[k][t];
+            if (rd_i) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) o4[t] = fmadd(beta, yo[4 * q + t], o4[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) yo[4 * q + t] = o4[t];
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int col = 4 * q + t;
+                if (col < nrhs) {
+                    T ov = alpha * acc[k][t];
+                    if (rd_i) ov = fmadd(beta, yo[(int64_t)col * syc], ov);
+                    yo[(int64_t)col * syc] = ov;
+                }
+            }
+        }
+    }
+}
+
 // Y rows of the stripes that store no row (and belong to no panel): beta * Y or 0.
 template <typename T>
 __global__ __launch_bounds__(kBlockThreads) void fill_rows_mm(const int32_t *__restrict__ fill, int nfill, T *__restrict__ Y,

@@ -18,6 +18,14 @@ DEV = "cuda:0"
 TOL64, TOL32 = 1e-12, 1e-5
 
 
+@pytest.fixture(autouse=True, params=["8", "0"], ids=["quads", "panels"])
+def multi_layout(request, monkeypatch):
+    """Every test on both multi-RHS layouts: stripes of width <= 8 in the VALU stripe-quad layout
+    (spmm_quads, the default) and, with VBC_PANEL_QUADS=0, every width on the MFMA panels."""
+    monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
+    return request.param
+
+
 def rel(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
@@ -197,3 +205,18 @@ def test_c5_panels_scaled_every_column(workload, scale):
         for j in range(16):
             ref = O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64), np.zeros(ny), trans=trans)
             assert rel(got[:, j], ref) <= TOL32, (trans, j)
+
+
+def test_quads_layout_flag_and_mixed_widths(multi_layout):
+    """vbc_info planar_mask bit 7 reports the VALU stripe-quad buckets (widths <= 8) unless
+    VBC_PANEL_QUADS=0; a matrix with widths 3 and 12 runs both kernels in one product (quads for the
+    3-wide stripes, MFMA panels for the 12-wide ones) and matches the oracle on every column."""
+    B = V.synthetic.vbr_1dvbc(700, 80, 900, np.where(np.arange(80) % 2 == 0, 3, 12), W=16, dtype=np.float32, seed=12)
+    inf = B.info(multi=True)
+    assert bool(inf["planar_mask"] & 128) == (multi_layout == "8")
+    assert inf["bins_m"] == 2
+    R = ref_1d(B)
+    X = np.random.default_rng(2).uniform(-1, 1, (B.m, 16)).astype(np.float32)
+    Yd = as_dev(np.zeros((B.n, 16), np.float32), "R")
+    V.mul_(Yd, B.T, as_dev(X, "R"), engine="mfma")
+    assert rel(Yd.cpu().numpy(), ref_cols(R, X, np.zeros((B.n, 16)), 1.0, 0.0)) <= TOL32

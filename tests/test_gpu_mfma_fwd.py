@@ -17,6 +17,14 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
+@pytest.fixture(autouse=True, params=["8", "0"], ids=["quads", "panels"])
+def multi_layout(request, monkeypatch):
+    """Every test on both multi-RHS layouts: stripes of width <= 8 in the VALU stripe-quad layout
+    (spmm_quads, the default) and, with VBC_PANEL_QUADS=0, every width on the MFMA panels."""
+    monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
+    return request.param
+
+
 def ref_cols_fwd(R, X, Y0, alpha, beta):
     Rd = R
     if R.val.dtype != np.float64:
