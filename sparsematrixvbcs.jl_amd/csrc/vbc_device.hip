@@ -1239,7 +1239,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                 std::sort(len.begin(), len.end(), std::greater<int64_t>());
                 for (size_t i = 0; i < len.size(); i += 64, nw++) work += (double)len[i] * kv.first;
             }
-            const double thr = h->ksplit * work / (double)std::max<int64_t>(nw, 1);
+            // never below a CU's share of the whole: with many chunks per CU (the ldoor stand-in's 'min
+            // blocks', 2550 chunks) a long chunk is averaged out, and cutting only adds chunks (70 -> 107 us)
+            const double thr = std::max(h->ksplit * work / (double)std::max<int64_t>(nw, 1), work / (double)h->cus);
             kst.assign(s.L, 1);
             int parts = 0, cut = 0;
             for (auto &kv : buckets) {
@@ -1771,9 +1773,12 @@ struct PendingPanel {
 // Stripe-quad bucket (vbc_panel.h spmm_quads): chunks of 16 stripes of width w <= 8, chunk rows = its
 // longest stripe's, rows x 16 keys (x row or kPanelSentinel) and rows x 16 x w values.  Natural stripe
 // order when the chunks pad <= slots_pad, else by decreasing length inside windows of 32 chunks.
-static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<int64_t> &stripes, int w, const char *val,
-                        Arena &ar, PendingPanel &pp)
+// pcs: the bucket's pieces (stripe, first column of the piece inside it).
+static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<std::pair<int64_t, int>> &pcs, int w,
+                        const char *val, Arena &ar, PendingPanel &pp)
 {
+    std::vector<int64_t> stripes;
+    for (const auto &pc : pcs) stripes.push_back(pc.first);
     const int esz = h->esz;
     const int64_t n = (int64_t)stripes.size();
     std::vector<int64_t> sbeg{0};
@@ -1797,7 +1802,7 @@ static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<int64
         }
         crow.push_back((int32_t)(crow.back() + len));
     }
-    for (int64_t i = 0; i < n; i++) out[i] = (int32_t)s.col0[stripes[ord[i]]];
+    for (int64_t i = 0; i < n; i++) out[i] = (int32_t)(s.col0[stripes[ord[i]]] + pcs[ord[i]].second);
     const int64_t rows = crow.back();
     pp = PendingPanel{};
     pp.quad = true;
@@ -1824,7 +1829,8 @@ static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<int64
                 const int64_t l = i < n ? stripes[ord[i]] : -1;
                 if (l >= 0 && s.rbeg[l] + k < s.rbeg[l + 1]) {
                     key[e] = (uint32_t)s.rows[s.rbeg[l] + k];
-                    std::memcpy(vv + e * w * esz, val + (s.voff[l] + k * s.w[l]) * esz, (size_t)w * esz);
+                    std::memcpy(vv + e * w * esz, val + (s.voff[l] + k * s.w[l] + pcs[ord[i]].second) * esz,
+                                (size_t)w * esz);
                 } else {
                     key[e] = kPanelSentinel;
                     std::memset(vv + e * w * esz, 0, (size_t)w * esz);
@@ -1872,9 +1878,9 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     if (total_groups >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "matrix too large for the panel layout");
     int range0 = 0;
     for (auto &kv : buckets) {
-        if (quads(kv.first)) {  // w <= 8: every piece is a whole stripe
-            std::vector<int64_t> st;
-            for (const Piece &pc : kv.second) st.push_back(pc.l);
+        if (quads(kv.first)) {  // w <= 8: whole stripes, or the last piece of a stripe wider than 16
+            std::vector<std::pair<int64_t, int>> st;
+            for (const Piece &pc : kv.second) st.emplace_back(pc.l, pc.c0);
             PendingPanel pp;
             build_quads(h, s, st, kv.first, val, ar, pp);
             pps.push_back(pp);
@@ -2380,6 +2386,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
+    h->cus = std::max(1, prop.multiProcessorCount);
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));
         h->occ_p = 1;

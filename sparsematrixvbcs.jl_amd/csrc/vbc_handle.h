@@ -103,7 +103,7 @@ struct vbc_handle {
     int target_ranges_m = 4096;
     int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
-    int panel_quads = 8;          // VBC_PANEL_QUADS: widest stripe of the VALU stripe-quad layout (0: MFMA panels only)
+    int panel_quads = 0;          // VBC_PANEL_QUADS: widest stripe of the VALU stripe-quad layout (0: MFMA panels only)
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch
@@ -154,6 +154,7 @@ struct vbc_handle {
     int small_fuse = 1;               // VBC_SMALL_FUSE: 0 = never fuse the buckets of a small matrix
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split
+    int cus = 256;                    // compute units of the device
     double ksplit = 1.0;              // VBC_KSPLIT: fused split stripes above this x the mean chunk work are cut
                                       // into 2 / 4 lane parts (SlotBin::ks; 0: never)
     int split_pipe = -1;              // VBC_SPLIT_PIPE: split bins' pipelined slice loop (-1 auto, 0 off, 1 on)

@@ -402,7 +402,7 @@ __device__ __forceinline__ T quad_bcast_rt(T v, int c)
 template <typename T, int W, bool VEC>
 __global__ __launch_bounds__(kBlockThreads) void spmm_quads(const QuadBin b, const T *__restrict__ X, int64_t sxr,
                                                             int64_t sxc, uint32_t xbytes, T *__restrict__ Y, int64_t syr,
-                                                            int64_t syc, int nrhs, T alpha, T beta, int rd_i)
+                                                            int64_t syc, int nrhs, T alpha, T beta, int rd_i, int diag)
 {
     const int c = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
     if (c >= b.nchunks) return;
@@ -417,87 +417,84 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_quads(const QuadBin b, con
     const gptr<const T> xg = G(X);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(X), 0, (int)xbytes, 0x00020000);
     const uint32_t sxr_b = (uint32_t)(sxr * esz), qoff = (uint32_t)(4 * q * esz);
-    T acc[W][4];
+    // accumulators of stripe column k, right-hand sides 4 q + 2 h, 4 q + 2 h + 1 (fp32: packed fmas)
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    t2 acc[W][2];
 #pragma unroll
-    for (int k = 0; k < W; k++)
+    for (int k = 0; k < W; k++) acc[k][0] = acc[k][1] = t2{T(0), T(0)};
+    // the keys of batch i + 1 are loaded with batch i's values and gathers: one round trip per batch
+    uint32_t kn[NB];
 #pragma unroll
-        for (int t = 0; t < 4; t++) acc[k][t] = T(0);
+    for (int j = 0; j < NB; j++) kn[j] = r0 < r1 ? key[(size_t)min(r0 + j, r1 - 1) * 16 + s] : kPanelSentinel;
     for (int r = r0; r < r1; r += NB) {
         uint32_t kk[NB];
-        T v[NB][NV], xv[NB][4];
+        T v[NB][NV];
+        t2 xv[NB][2];
 #pragma unroll
         for (int j = 0; j < NB; j++) {
+            kk[j] = kn[j];
             const size_t rr = (size_t)min(r + j, r1 - 1) * 16 + s;
-            kk[j] = key[rr];
 #pragma unroll
             for (int u = 0; u < NV; u++) v[j][u] = val[rr * W + min(4 * u + q, W - 1)];
         }
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const bool ok = r + j < r1 && kk[j] != kPanelSentinel && qlive;
+            const uint32_t xr = (diag & 16) ? (kk[j] & 3u) : kk[j];  // ablation: gathers confined to 4 rows
             if constexpr (VEC) {
-                const uint32_t xo = ok ? kk[j] * sxr_b + qoff : xbytes;  // past X: zeros
+                const uint32_t xo = ok ? xr * sxr_b + qoff : xbytes;  // past X: zeros
                 if constexpr (sizeof(T) == 4) {
                     typedef float f4 __attribute__((ext_vector_type(4)));
                     const f4 t4 = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
-#pragma unroll
-                    for (int t = 0; t < 4; t++) xv[j][t] = t4[t];
+                    xv[j][0] = t2{t4[0], t4[1]};
+                    xv[j][1] = t2{t4[2], t4[3]};
                 } else {
-                    typedef double d2 __attribute__((ext_vector_type(2)));
-                    const d2 a = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
-                    const d2 bb = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xo + 16 : xbytes, 0, 0));
-                    xv[j][0] = a[0];
-                    xv[j][1] = a[1];
-                    xv[j][2] = bb[0];
-                    xv[j][3] = bb[1];
+                    xv[j][0] = __builtin_bit_cast(t2, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
+                    xv[j][1] = __builtin_bit_cast(t2, __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xo + 16 : xbytes, 0, 0));
                 }
             } else {
+                T e[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
                     const int col = 4 * q + t;
-                    xv[j][t] = (ok && col < nrhs) ? xg[(int64_t)kk[j] * sxr + (int64_t)col * sxc] : T(0);
+                    e[t] = (ok && col < nrhs) ? xg[(int64_t)xr * sxr + (int64_t)col * sxc] : T(0);
                 }
+                xv[j][0] = t2{e[0], e[1]};
+                xv[j][1] = t2{e[2], e[3]};
             }
         }
 #pragma unroll
+        for (int j = 0; j < NB; j++) kn[j] = key[(size_t)min(r + NB + j, r1 - 1) * 16 + s];
+#pragma unroll
         for (int j = 0; j < NB; j++) {
-            const bool live = r + j < r1;  // rows past the chunk (the batch's clamped tail): no-ops
+            // rows past the chunk (the batch's clamped tail): zero values times zero x, no-ops
+            const bool live = r + j < r1;
+#pragma unroll
+            for (int u = 0; u < NV; u++) v[j][u] = live ? v[j][u] : T(0);
 #pragma unroll
             for (int k = 0; k < W; k++) {
                 const T vk = quad_bcast_rt(v[j][k >> 2], k);
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const T nv = fmadd(vk, xv[j][t], acc[k][t]);
-                    acc[k][t] = live ? nv : acc[k][t];
-                }
+                const t2 vv = t2{vk, vk};
+                acc[k][0] = __builtin_elementwise_fma(vv, xv[j][0], acc[k][0]);
+                acc[k][1] = __builtin_elementwise_fma(vv, xv[j][1], acc[k][1]);
             }
         }
     }
     const int seg = c * 16 + s;
-    if (seg >= b.nseg || !qlive) return;
+    if (seg >= b.nseg || !qlive || (diag & 2)) return;
     const int64_t o = b.out_affine ? (int64_t)b.out_base + (int64_t)seg * b.out_stride : (int64_t)G(b.out)[seg];
 #pragma unroll
     for (int k = 0; k < W; k++) {
         gptr<T> yo = G(Y) + (o + k) * syr;
-        if constexpr (VEC) {
-            T o4[4];
+        const T a4[4] = {acc[k][0][0], acc[k][0][1], acc[k][1][0], acc[k][1][1]};
 #pragma unroll
-            for (int t = 0; t < 4; t++) o4[t] = alpha * acc[k][t];
-            if (rd_i) {
-#pragma unroll
-                for (int t = 0; t < 4; t++) o4[t] = fmadd(beta, yo[4 * q + t], o4[t]);
-            }
-#pragma unroll
-            for (int t = 0; t < 4; t++) yo[4 * q + t] = o4[t];
-        } else {
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const int col = 4 * q + t;
-                if (col < nrhs) {
-                    T ov = alpha * acc[k][t];
-                    if (rd_i) ov = fmadd(beta, yo[(int64_t)col * syc], ov);
-                    yo[(int64_t)col * syc] = ov;
-                }
+        for (int t = 0; t < 4; t++) {
+            const int col = 4 * q + t;
+            if (VEC || col < nrhs) {
+                const int64_t yi = VEC ? (int64_t)col : (int64_t)col * syc;
+                T ov = alpha * a4[t];
+                if (rd_i) ov = fmadd(beta, yo[yi], ov);
+                yo[yi] = ov;
             }
         }
     }

@@ -36,10 +36,10 @@ static int mulmat_panel(const vbc_handle *h, int trans, int64_t nrhs, const char
     do {                                                                                                      \
         if (vec)                                                                                              \
             hipLaunchKernelGGL((spmm_quads<T, W, true>), dim3(grid), dim3(kBlockThreads), 0, s, qb, xs, sxr, sxc, xb, \
-                               ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd);                                 \
+                               ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu);               \
         else                                                                                                  \
             hipLaunchKernelGGL((spmm_quads<T, W, false>), dim3(grid), dim3(kBlockThreads), 0, s, qb, xs, sxr, sxc, xb, \
-                               ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd);                                 \
+                               ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu);               \
     } while (0)
             switch (qb.w) {
             case 1: VBC_QUADS(1); break;

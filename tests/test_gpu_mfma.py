@@ -20,8 +20,9 @@ TOL64, TOL32 = 1e-12, 1e-5
 
 @pytest.fixture(autouse=True, params=["8", "0"], ids=["quads", "panels"])
 def multi_layout(request, monkeypatch):
-    """Every test on both multi-RHS layouts: stripes of width <= 8 in the VALU stripe-quad layout
-    (spmm_quads, the default) and, with VBC_PANEL_QUADS=0, every width on the MFMA panels."""
+    """Every test on both multi-RHS layouts: every width on the MFMA panels (the default,
+    VBC_PANEL_QUADS=0) and, with VBC_PANEL_QUADS=8, stripes of width <= 8 in the VALU stripe-quad layout
+    (spmm_quads; measured slower on both C5 inputs, kept as the A/B alternative)."""
     monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
     return request.param
 
