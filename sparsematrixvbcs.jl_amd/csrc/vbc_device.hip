@@ -1273,6 +1273,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         if ((double)nch * 2 <= slots) {
             int P = 1;
             while (P < 8 && (double)nch * P * 2 <= 2 * slots && avg / (P * 2) >= minrows) P *= 2;
+            // fusing pays even when the chunks are too short to split: one launch instead of one per
+            // bucket (the thermal1 stand-in's 'min blocks', 8 buckets of 16-row chunks: 41 us unfused)
+            P = std::max(P, 2);
             if (h->planar_split > 1) P = h->planar_split;
             if (P > 1) h->small_split = P;
         }

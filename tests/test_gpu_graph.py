@@ -50,7 +50,9 @@ def test_forked_groups_bitwise_eager_graph_and_two_streams(monkeypatch):
     the groups after the first on side streams joined back into the caller's (Launch::fork_*).  It
     must equal the sequential launch (VBC_FORK=0) bit for bit: eagerly, replayed from a HIP graph,
     and with the same handle used from two caller streams at once, each product ordered after the
-    writes of x that precede it on its own stream."""
+    writes of x that precede it on its own stream.  (VBC_SMALL_FUSE=0: the matrix is small enough for the
+    fused split, which would run all its buckets as one launch.)"""
+    monkeypatch.setenv("VBC_SMALL_FUSE", "0")
     rng = np.random.default_rng(5)
     L = 20000
     G = V.synthetic.vbr_1dvbc(40000, L, 200000, np.arange(L) % 8 + 1, W=8, seed=9)
