@@ -1276,6 +1276,18 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             // fusing pays even when the chunks are too short to split: one launch instead of one per
             // bucket (the thermal1 stand-in's 'min blocks', 8 buckets of 16-row chunks: 41 us unfused)
             P = std::max(P, 2);
+            // many chunks (more waves than one round of the chip): P that fills whole rounds of resident
+            // waves -- the ldoor stand-in's 'min blocks', 2550 chunks: P = 2 / 4 / 8 give 1.25 / 2.5 / 5.0
+            // rounds of 4096 fp32 waves (70.9 / 70.1 / 66.0 us, profiles/r04_ab7_ldoor32_blocks.log)
+            auto rounds = [&](int p) {
+                const double cap = (double)h->cus * std::max(1, h->occ_multi[p == 2 ? 1 : p == 4 ? 2 : 3]);
+                return (double)nch * p / cap;
+            };
+            if (rounds(P) > 1.0) {
+                auto eff = [&](int p) { const double r = rounds(p); return r / std::ceil(r); };
+                for (int p = 2; p <= 8; p *= 2)
+                    if (eff(p) > eff(P) + 0.05) P = p;
+            }
             if (h->planar_split > 1) P = h->planar_split;
             if (P > 1) h->small_split = P;
         }
@@ -2390,6 +2402,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     h->cus = std::max(1, prop.multiProcessorCount);
+    for (int lp = 1; lp <= 3; lp++) h->occ_multi[lp] = occupancy_split_multi(h->esz, 1 << lp);
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));
         h->occ_p = 1;

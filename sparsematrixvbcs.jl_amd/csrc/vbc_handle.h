@@ -155,6 +155,7 @@ struct vbc_handle {
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split
     int cus = 256;                    // compute units of the device
+    int occ_multi[4] = {0, 0, 0, 0};  // resident waves per CU of the fused split launch, P = 2 / 4 / 8 (index log2 P)
     double ksplit = 1.0;              // VBC_KSPLIT: fused split stripes above this x the mean chunk work are cut
                                       // into 2 / 4 lane parts (SlotBin::ks; 0: never)
     int split_pipe = -1;              // VBC_SPLIT_PIPE: split bins' pipelined slice loop (-1 auto, 0 off, 1 on)

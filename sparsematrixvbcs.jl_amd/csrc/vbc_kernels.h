@@ -202,6 +202,7 @@ int occupancy_slots(int esz, int kind);
 int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                   double alpha, double beta, bool rd, hipStream_t s);
 int occupancy_planar(int esz);
+int occupancy_split_multi(int esz, int P);
 int launch_split_multi(int esz, const SplitMulti &M, int P, const void *x, void *y, double alpha, double beta, bool rd,
                        hipStream_t s);
 int occupancy_lanes(int esz);

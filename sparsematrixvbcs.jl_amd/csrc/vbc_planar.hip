@@ -284,6 +284,20 @@ int launch_split_multi(int esz, const SplitMulti &M, int P, const void *x, void 
                     : launch_split_multi_t<float>(M, P, x, y, alpha, beta, rd, s);
 }
 
+// Resident waves per CU of the fused split launch (batched slice loop) with P waves per workgroup.
+int occupancy_split_multi(int esz, int P)
+{
+    int nb = 0;
+#define VBC_OCC_MULTI(TT, PP) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, spmv_split_multi<TT, PP, 2>, 64 * PP, 0)
+    if (esz == 8) {
+        if (P == 2) VBC_OCC_MULTI(double, 2); else if (P == 4) VBC_OCC_MULTI(double, 4); else VBC_OCC_MULTI(double, 8);
+    } else {
+        if (P == 2) VBC_OCC_MULTI(float, 2); else if (P == 4) VBC_OCC_MULTI(float, 4); else VBC_OCC_MULTI(float, 8);
+    }
+#undef VBC_OCC_MULTI
+    return nb * P;
+}
+
 int occupancy_planar(int esz)
 {
     int occ = 0;
