@@ -562,7 +562,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         const double rows_per_wave = (double)rows / (double)std::max<int64_t>(nch, 1) / split;
         const int u0 = (9 / w) / run * run;  // planar_split_step (vbc_planar.h, VBC_SPLIT_VALS = 9)
         const double step_rows = (double)std::min(8 * run, std::max(run, u0));
-        b.deep = h->split_pipe >= 0 ? h->split_pipe : (rows_per_wave > 2.0 * step_rows ? 2 : 0);
+        b.deep = h->split_pipe >= 0 ? h->split_pipe : (rows_per_wave > h->split_deep * step_rows ? 2 : 0);
         // VBC_SPLIT_NT_MB: above that many value bytes the batched loop reads keys and values non-temporally
         // (mode 3).  Off by default: slower on every table partition, the 300 MB ldoor 'min blocks' too
         // (68.3 -> 77.7 us; ct20stif strict 8.9 -> 12.3 us; profiles/r04_ab4_*.log)
@@ -2396,6 +2396,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
+    if (const char *e = getenv("VBC_SPLIT_DEEP")) h->split_deep = std::max(0.0, atof(e));
     if (const char *e = getenv("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));

@@ -159,6 +159,7 @@ struct vbc_handle {
     double ksplit = 1.0;              // VBC_KSPLIT: fused split stripes above this x the mean chunk work are cut
                                       // into 2 / 4 lane parts (SlotBin::ks; 0: never)
     int split_pipe = -1;              // VBC_SPLIT_PIPE: split bins' pipelined slice loop (-1 auto, 0 off, 1 on)
+    double split_deep = 2.0;          // VBC_SPLIT_DEEP: auto slice loop batched above this many steps per wave
     int split_rows = 12;              // VBC_SPLIT_ROWS: fewest chunk rows per wave of an automatic split
     int fwd_min_rows = 16;            // VBC_FWD_MIN_ROWS: fewest chunk rows per range of the forward run layout
     int planar_wps = 2;               // VBC_PLANAR_WPS: most resident waves per SIMD of a plain planar bin (0: occupancy)
