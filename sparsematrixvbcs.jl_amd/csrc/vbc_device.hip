@@ -245,7 +245,7 @@ static int slot_spl(const vbc_handle *h, int kind, int w)
 // fp32 w = 3 (12-B rows, no padding to 4).
 static bool slot_planar(const vbc_handle *h, int kind, int w)
 {
-    if (kind == 0 && h->small_split > 1 && w >= 1 && w <= 8) return true;  // fused small-matrix split (below)
+    if (kind == 0 && h->small_split > 1 && w >= 1 && w <= 8 && ((h->fuse_w >> w) & 1)) return true;  // fused split (below)
     if (kind != 0 || h->slot_planar == 0 || w < 3 || w > 8) return false;
     return h->esz == 8 || w != 4;
 }
@@ -324,8 +324,9 @@ constexpr double kSmallPad = 4.0;
 
 static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<int64_t> &sbeg,
                       int64_t total_entries, int64_t gather_limit, std::vector<int64_t> &order,
-                      bool *mask = nullptr)
+                      bool *mask = nullptr, int wsrc = -1)
 {
+    const bool fused = kind == 0 && h->small_split > 1 && wsrc >= 1 && wsrc <= 8 && ((h->fuse_w >> wsrc) & 1);
     if (mask) *mask = false;
     const int64_t nseg = (int64_t)sbeg.size() - 1;
     const int64_t real = nseg > 0 ? sbeg[nseg] - sbeg[0] : 0;
@@ -352,7 +353,7 @@ static int want_slots(const vbc_handle *h, int kind, int w, const std::vector<in
         // per range ran 193 us against the merge kernel's 171 us, profiles/r03_fork_ab2.log)
         return ratio <= (pad_limit > 0 ? pad_limit : h->slots_pad) && (double)longest <= std::max(64.0, 0.5 * rows_per_range);
     };
-    if (kind == 0 && h->small_split > 1 && h->slots_mode != 0) {
+    if (fused && h->slots_mode != 0) {
         // fused small-matrix split (build_transposed): P waves fold every chunk, so a chunk longer than
         // the rows of a range does not unbalance anything; padding rows cost instructions and a few
         // cached lines of a matrix that stays in L2, so a sorted order may pad up to kSmallPad
@@ -468,7 +469,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         for (int32_t c : cr) rows += c;
         // planar buckets with fewer chunks than wave slots: one chunk per workgroup of `split` waves
         split = 1;
-        if (planar && kind == 0 && h->small_split > 1) {
+        if (planar && kind == 0 && h->small_split > 1 && wsrc <= 8 && ((h->fuse_w >> wsrc) & 1)) {
             split = h->small_split;  // fused small-matrix split: one P for every bucket of the launch
         } else if (planar && h->planar_split != 0) {
             if (h->planar_split > 1) split = h->planar_split;
@@ -543,6 +544,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.nranges = (int32_t)nr;
     b.nseg = (int32_t)nstripes;
     b.ks = ks;
+    b.fused = (planar && kind == 0 && split > 1 && h->small_split > 1 && wsrc <= 8 && ((h->fuse_w >> wsrc) & 1)) ? 1 : 0;
     b.u = h->slot_u;
     b.diag = h->diag;
     b.xcd = (planar && split == 1) ? h->xcd_p : 0;  // split grids are small (one chunk per workgroup)
@@ -1221,6 +1223,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     // at most half the wave slots (the split rule of build_slots) and every chunk keeps >= split_rows
     // (fp64) rows per wave; P is common to the launch.  VBC_SMALL_FUSE=0 turns it off.
     h->small_split = 0;
+    h->fuse_w = 0;
     // Long stripes (SlotBin::ks): a chunk runs on one CU and costs its longest stripe's rows, so a few
     // chunks of long stripes (a 'min blocks' partition's widest, fullest stripes: 3.4x the mean chunk on
     // the ct20stif stand-in) set the product's time.  A stripe whose work (rows x width, values per
@@ -1230,10 +1233,27 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     // (auto layouts only: a forced VBC_SLOTS / VBC_SLOT_PLANAR keeps the layout the tests ask for)
     if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar < 0 && h->slots_mode < 0 && buckets.size() >= 2 &&
         (int)buckets.size() <= kSplitParts && buckets.rbegin()->first <= 8 && !sweep_possible(h, 1, s.m)) {
+        // the fused buckets: all of them; or, when their chunks would overflow the launch and one bucket
+        // holds most of them, every bucket but that one (a large operator's dominant width keeps its
+        // streaming layout, and its small side buckets -- a time-model partition's few 1-, 4- and 5-wide
+        // stripes beside 305,000 3-wide ones -- run as one fused launch instead of one launch each)
+        const double slots0 = (double)h->target_ranges_p;
+        int64_t nall = 0, nmax = 0;
+        int wmax = 0;
+        for (auto &kv : buckets) {
+            const int64_t c = ((int64_t)kv.second.size() + 63) / 64;
+            nall += c;
+            if (c > nmax) { nmax = c; wmax = kv.first; }
+        }
+        for (auto &kv : buckets) h->fuse_w |= 1u << kv.first;
+        if ((double)nall * 2 > slots0 && buckets.size() >= 3 && (double)nmax >= 0.8 * (double)nall)
+            h->fuse_w &= ~(1u << wmax);
+        auto fused_w = [&](int w) { return ((h->fuse_w >> w) & 1) != 0; };
         if (h->ksplit > 0) {
             double work = 0;
             int64_t nw = 0;
             for (auto &kv : buckets) {  // chunks of the length-sorted buckets
+                if (!fused_w(kv.first)) continue;
                 std::vector<int64_t> len;
                 for (int64_t l : kv.second) len.push_back(s.rbeg[l + 1] - s.rbeg[l]);
                 std::sort(len.begin(), len.end(), std::greater<int64_t>());
@@ -1245,6 +1265,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             kst.assign(s.L, 1);
             int parts = 0, cut = 0;
             for (auto &kv : buckets) {
+                if (!fused_w(kv.first)) continue;
                 int cls = 0;
                 for (int64_t l : kv.second) {
                     const double wk = (double)(s.rbeg[l + 1] - s.rbeg[l]) * kv.first;
@@ -1257,7 +1278,10 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             if (parts > kSplitParts || cut == 0 || !(thr > 0)) kst.clear();
         }
         int64_t nch = 0, rows = 0;
+        int nf = 0;
         for (auto &kv : buckets) {
+            if (!fused_w(kv.first)) continue;
+            nf++;
             int64_t cnt[5] = {0, 0, 0, 0, 0};
             for (int64_t l : kv.second) {
                 cnt[kst.empty() ? 1 : kst[l]]++;
@@ -1270,7 +1294,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         // (the batched slice loop costs a round trip per batch, not per step: thinner slices than the
         // single-bucket rule's split_rows pay off -- ct20stif 'min blocks' P = 4 / 8: 15.7 / 14.7 us)
         const double minrows = (double)h->small_rows * h->esz / 8.0;
-        if ((double)nch * 2 <= slots) {
+        if ((double)nch * 2 <= slots && nf >= 2) {
             int P = 1;
             while (P < 8 && (double)nch * P * 2 <= 2 * slots && avg / (P * 2) >= minrows) P *= 2;
             // fusing pays even when the chunks are too short to split: one launch instead of one per
@@ -1291,10 +1315,14 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             if (h->planar_split > 1) P = h->planar_split;
             if (P > 1) h->small_split = P;
         }
-        if (h->small_split <= 1) kst.clear();
+        if (h->small_split <= 1) {
+            kst.clear();
+            h->fuse_w = 0;
+        }
         if (getenv("VBC_VERBOSE"))
-            fprintf(stderr, "[vbc] small fused split: %d buckets, %lld chunks, %.1f rows per chunk -> P = %d%s\n",
-                    (int)buckets.size(), (long long)nch, avg, h->small_split, kst.empty() ? "" : ", long stripes cut");
+            fprintf(stderr, "[vbc] small fused split: %d of %d buckets (width mask 0x%x), %lld chunks, %.1f rows per "
+                    "chunk -> P = %d%s\n", nf, (int)buckets.size(), h->fuse_w, (long long)nch, avg, h->small_split,
+                    kst.empty() ? "" : ", long stripes cut");
     }
     // the bins: a width bucket, or (long stripes cut) its stripes of each part count ks
     std::vector<std::pair<int, std::vector<int64_t>>> subs;
@@ -1367,7 +1395,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             pss.push_back(std::move(ps));
             continue;
         }
-        if (want_slots(h, 0, wps, sb, hsbeg.empty() ? total : total + (hsbeg.back() - sbeg.back()), s.m, order, &mask)) {
+        if (want_slots(h, 0, wps, sb, hsbeg.empty() ? total : total + (hsbeg.back() - sbeg.back()), s.m, order, &mask, w)) {
             std::vector<Entry> ents;
             std::vector<int32_t> out;
             for (int64_t l : kv.second) out.push_back((int32_t)s.col0[l]);
@@ -2182,25 +2210,31 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
     // the fused small-matrix split (build_transposed): every planar bin a split bin of the common P, all
     // of them one launch of spmv_split_multi (their chunks concatenated)
     L.fuse_split = 0;
-    if (h->small_split > 1 && !L.pbins.empty() && (int)L.pbins.size() <= kSplitParts) {
+    if (h->small_split > 1) {
+        int nfb = 0;
         bool all = true;
-        for (const SlotBin &b : L.pbins)
+        for (const SlotBin &b : L.pbins) {
+            if (!b.fused) continue;
+            nfb++;
             all = all && b.kind == 0 && b.split == h->small_split && !b.kc && !b.lanes && !b.pair && !b.mask &&
                   b.diag == 0 && b.wkey >= 1 && b.wkey <= 8 && b.w == b.wkey && b.run >= 1 && b.run <= 3;
-        if (all) {
+        }
+        if (nfb > 0 && nfb <= kSplitParts && all) {
             SplitMulti M{};
-            int c0 = 0;
-            for (size_t i = 0; i < L.pbins.size(); i++) {
-                const SlotBin &b = L.pbins[i];
-                M.p[i] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst, b.holes, b.ks,
-                                   b.rrow, b.key, b.val, b.out};
+            int c0 = 0, i = 0;
+            for (const SlotBin &b : L.pbins) {
+                if (!b.fused) continue;
+                M.p[i++] = SplitPart{b.wkey, b.run, c0, b.nseg, b.out_affine, b.out_base, b.out_stride, b.wst, b.holes, b.ks,
+                                     b.rrow, b.key, b.val, b.out};
                 c0 += b.nranges;  // a split bin's ranges are its chunks
+                M.pad0 = std::max<int32_t>(M.pad0, b.deep);  // slice loop (build_slots)
             }
-            M.nparts = (int)L.pbins.size();
+            M.nparts = nfb;
             M.nchunks = c0;
-            for (const SlotBin &b : L.pbins) M.pad0 = std::max<int32_t>(M.pad0, b.deep);  // slice loop (build_slots)
             L.multi = M;
             L.fuse_split = h->small_split;
+        } else {
+            for (SlotBin &b : L.pbins) b.fused = 0;  // each split bin on its own launch
         }
     }
     L.d_fill = reinterpret_cast<const int32_t *>(base + L.o_fill);

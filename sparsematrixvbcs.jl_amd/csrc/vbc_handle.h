@@ -151,6 +151,7 @@ struct vbc_handle {
     int slot_wonly = 1;               // VBC_SLOT_WONLY=0: the all-width slotted kernel even for one-width launches
     int split_kc = 0;                 // VBC_SPLIT_KC=1: compressed keys for split planar bins too
     int small_split = 0;              // > 1: this B'x layout is the fused small-matrix split with P waves per chunk
+    uint32_t fuse_w = 0;              // bit w: the width-w bucket belongs to the fused split (all, or the side buckets)
     int small_fuse = 1;               // VBC_SMALL_FUSE: 0 = never fuse the buckets of a small matrix
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split

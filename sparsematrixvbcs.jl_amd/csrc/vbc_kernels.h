@@ -97,6 +97,7 @@ struct SlotBin {
     int32_t xcd;         // planar: XCD-contiguous workgroup order (xcd_block)
     int32_t holes;       // planar split runs with holes: a run's first key holds, in bits 27..29, which of its
                          // RUN rows the stripe stores (the others: zero values, x taken as 0); index bits 0..26
+    int32_t fused;       // planar split bin run inside the fused split launch (Launch::multi), not on its own
     int32_t ks;          // planar split: > 1 = every stripe cut into ks parts of whole runs, part h of the
                          // chunk's stripe i in lane h * (64 / ks) + i (long stripes of the fused split; the
                          // parts are summed across lanes before the store), out / nseg per stripe

@@ -14,7 +14,8 @@ namespace vbc {
 // slotted bins, each planar bin, and the merge kernel with its fix-up (+ the fill list).
 int launch_groups(const Launch &L)
 {
-    const int planar = L.fuse_split ? (int)!L.pbins.empty() : (int)L.pbins.size();  // fused: one launch
+    int planar = L.fuse_split ? 1 : 0;  // the fused split bins: one launch
+    for (const SlotBin &b : L.pbins) planar += L.fuse_split && b.fused ? 0 : 1;
     return (L.sweep_tiles > 0) + (L.slot_ranges > 0) + planar + (L.total_ranges > 0 || L.nfill > 0);
 }
 
@@ -68,7 +69,7 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
             return VBC_HIP_ERROR;
         }
     }
-    if (L.fuse_split && !L.pbins.empty()) {  // the small-matrix split bins: one launch for all of them
+    if (L.fuse_split) {  // the fused split bins: one launch for all of them
         if (mine(true)) {
             const hipError_t e = (hipError_t)launch_split_multi((int)sizeof(T), L.multi, L.fuse_split, x, y, alpha, beta,
                                                                 rd, stream);
@@ -78,9 +79,10 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
             }
         }
     }
-    for (size_t i = 0; i < (L.fuse_split ? 0 : L.pbins.size()); i++) {  // planar buckets (vbc_planar.h): one launch each
-        if (!mine(true)) continue;
+    for (size_t i = 0; i < L.pbins.size(); i++) {  // the other planar buckets (vbc_planar.h): one launch each
         const SlotBin &pb = L.pbins[i];
+        if (L.fuse_split && pb.fused) continue;
+        if (!mine(true)) continue;
         const bool faste = !rd && pb.out_affine && !getenv("VBC_NO_FASTE");
         const bool staged = faste && pb.contig && slot_stage != 0;
         const hipError_t e = (hipError_t)launch_planar((int)sizeof(T), pb, L.d_pbins + i, faste, staged, x, y, alpha,

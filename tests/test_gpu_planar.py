@@ -822,3 +822,24 @@ def test_fused_split_min_blocks_partition():
     V.mul_(y32, B32.T, dev(x32))
     R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B32.val.astype(np.float64))
     assert rel(y32.cpu().numpy(), O.mul(R64, x32.astype(np.float64), np.zeros(B.n), trans=True)) <= TOL32
+
+
+def test_fused_side_buckets_beside_a_dominant_width():
+    """A large matrix whose chunks overflow one fused launch, with one dominant width (300,000 3-wide
+    stripes) and small side buckets (1-, 4- and 5-wide stripes, as a time-model partition leaves them):
+    the dominant bucket keeps its own planar layout and the side buckets run as one fused split launch
+    (planar_mask bit 5 with planar_bins >= 2); the product matches the oracle, fp64 and fp32."""
+    L = 301500
+    widths = np.full(L, 3)
+    widths[100::601] = 4
+    widths[200::601] = 5
+    widths[300::601] = 1
+    for dtype, tol in ((np.float64, TOL64), (np.float32, TOL32)):
+        B = V.synthetic.vbr_1dvbc(200000, L, 6 * L, widths, W=8, dtype=dtype, seed=48)
+        inf = B.info(trans=True)
+        assert inf["planar_mask"] & 32 and inf["planar_bins"] >= 2, inf
+        R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+        x = np.random.default_rng(49).uniform(-1, 1, B.m).astype(dtype)
+        y = torch.zeros(B.n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+        V.mul_(y, B.T, dev(x))
+        assert rel(y.cpu().numpy(), O.mul(R, x.astype(np.float64), np.zeros(B.n), trans=True)) <= tol
