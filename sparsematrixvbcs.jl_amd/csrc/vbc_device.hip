@@ -61,6 +61,7 @@ struct Arena {
 struct PendingBin {
     Bin b;
     size_t o_key, o_val, o_rseg, o_out, o_carry, o_cseg;
+    double work = 0;  // matrix bytes the bin streams (launch-group ordering)
 };
 
 static int check_limits(const Stripes &s)
@@ -921,6 +922,7 @@ static void commit_launch_keys(const vbc_handle *h, std::vector<PendingSlot> &ps
 struct PendingSweep {
     SweepBin b;
     size_t o_tstep, o_key, o_loc, o_val, o_out, o_sbase;
+    double work = 0;  // matrix bytes the bin streams (launch-group ordering)
 };
 
 // Whether a bucket lacks x locality: the gathers of windows of 64 consecutive segments (the segments
@@ -1360,6 +1362,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             if (want_sweep(h, w, s.m, sb, ents)) {
                 PendingSweep pw;
                 if (int st = build_sweep(h, 0, w, sb, ents, out, val, ar, tile0, pw)) return st;
+                pw.work = (double)ents.size() * (4.0 + (double)w * h->esz);
                 pws.push_back(pw);
                 continue;
             }
@@ -1433,6 +1436,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         PendingBin pb;
         if (int st = build_bucket(h, 0, wp, ents, out, total, val, ar, range0, pb, w)) return st;
         h->bytes_t += (int64_t)ents.size() * (4 + (int64_t)wp * h->esz) + (int64_t)out.size() * 4;
+        pb.work = (double)ents.size() * (4.0 + (double)wp * h->esz);
         pbs.push_back(pb);
     }
     commit_launch_keys(h, pss, ar);
@@ -2245,6 +2249,26 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
     if (!L.sbins.empty()) {
         VBC_HIP(hipMalloc(&L.d_sbins, L.sbins.size() * sizeof(SlotBin)));
         VBC_HIP(hipMemcpy(L.d_sbins, L.sbins.data(), L.sbins.size() * sizeof(SlotBin), hipMemcpyHostToDevice));
+    }
+    // bytes per launch group, in launch_group's order (sweep, slots, fused split, planar bins, merge)
+    L.gwork.clear();
+    {
+        std::vector<double> pw_planar;
+        double slots = 0, fused = 0, sweep = 0, merge = 0;
+        size_t pi = 0;
+        for (const PendingSlot &ps : pss) {
+            const double wk = (double)ps.rows * ps.b.rpi * ps.b.w * h->esz + (double)ps.key_bytes;
+            if (!ps.b.planar) slots += wk;
+            else if (L.fuse_split && L.pbins[pi++].fused) fused += wk;
+            else pw_planar.push_back(wk);
+        }
+        for (const PendingSweep &pw : pws) sweep += pw.work;
+        for (const PendingBin &pb : pbs) merge += pb.work;
+        if (L.sweep_tiles > 0) L.gwork.push_back(sweep);
+        if (L.slot_ranges > 0) L.gwork.push_back(slots);
+        if (L.fuse_split) L.gwork.push_back(fused);
+        for (double wk : pw_planar) L.gwork.push_back(wk);
+        if (L.total_ranges > 0 || L.nfill > 0) L.gwork.push_back(merge + 1.0);
     }
     return VBC_OK;
 }

@@ -48,6 +48,8 @@ struct Launch {
     // spmv_split_multi with fuse_split waves per chunk (0: one launch per planar bin)
     int fuse_split = 0;
     SplitMulti multi{};
+    std::vector<double> gwork;  // matrix bytes of each launch group (launch_groups order): the heaviest is
+                                // submitted last, so the small groups are already dispatched when it fills the chip
     std::vector<hipStream_t> fork_streams;
     std::vector<hipEvent_t> fork_events;  // [0]: the fork, [1 + i]: side stream i done
 };

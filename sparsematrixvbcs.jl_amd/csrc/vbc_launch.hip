@@ -184,10 +184,18 @@ static int launch(const vbc_handle *h, const Launch &L, int kind, const void *x,
     }
     VBC_HIP(hipEventRecord(L.fork_events[0], stream));
     for (int i = 0; i < used; i++) VBC_HIP(hipStreamWaitEvent(L.fork_streams[i], L.fork_events[0], 0));
-    int st = VBC_OK;
+    // the heaviest group goes last, on the caller's stream: submitted first, it would fill every CU and
+    // the small groups would wait for its tail (the ldoor stand-in's 'min memory': 3-wide bucket + one
+    // 32-stripe chunk of 6-wide stripes)
+    int gh = 0;
+    if ((int)L.gwork.size() == G)
+        for (int g = 1; g < G; g++)
+            if (L.gwork[g] > L.gwork[gh]) gh = g;
+    int st = VBC_OK, si = 0;
     for (int g = 0; g < G && st == VBC_OK; g++)
-        st = launch_group<T>(L, kind, x, y, alpha, beta, rd, g == 0 ? stream : L.fork_streams[(g - 1) % nside],
-                             h->xcd, h->slot_stage, g);
+        if (g != gh)
+            st = launch_group<T>(L, kind, x, y, alpha, beta, rd, L.fork_streams[si++ % nside], h->xcd, h->slot_stage, g);
+    if (st == VBC_OK) st = launch_group<T>(L, kind, x, y, alpha, beta, rd, stream, h->xcd, h->slot_stage, gh);
     for (int i = 0; i < used; i++) {  // joined even after a failed launch: no side stream is left dangling
         if (hipEventRecord(L.fork_events[1 + i], L.fork_streams[i]) != hipSuccess ||
             hipStreamWaitEvent(stream, L.fork_events[1 + i], 0) != hipSuccess) {
