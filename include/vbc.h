@@ -301,7 +301,9 @@ typedef struct vbc_info {
                                bit 5: a small matrix's B'x buckets of every width (1..8) laid out planar
                                and split, run by ONE fused launch (planar_split = its P); bit 6: some of
                                those stripes cut into 2 / 4 lane parts (long stripes); bit 7: the multi-RHS
-                               layout has VALU stripe-quad buckets (widths <= 8, spmm_quads) */
+                               layout has VALU stripe-quad buckets (widths <= 8, spmm_quads); bit 8: the
+                               forward product runs on the transposed layout of C = Bᵀ (stripes of several
+                               widths: one fused launch instead of one per width) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

@@ -1453,6 +1453,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     L.total_ranges = range0;
     L.slot_ranges = srange0;
     L.sweep_tiles = tile0;
+    L.fuse_p = h->small_split;  // (the handle's field is rebuilt by the next build_transposed call)
     L.sweep_tile_bytes = h->sweep_tile;
     if (const char *e = getenv("VBC_SWEEP_DIAG")) L.sweep_diag = atoi(e);
     h->bytes_t += (s.m + s.n) * h->esz;  // x read once, y written once
@@ -1687,6 +1688,24 @@ static int build_fwd_lanes(vbc_handle *h, int w, int R, const std::vector<Entry>
 // Forward layout: per width bucket, segments = output rows with entries of that width (ascending),
 // entries = (row, stripe) blocks ordered by stripe within the row.  With a single bucket, a slotted
 // layout takes every row as a segment (affine, no fill list).
+// Whether the forward product is built as the transposed product of C = Bᵀ (transpose_stripes): stripes
+// of two or more widths (the forward layouts would need a scale pass plus one launch per width, each
+// adding into y), at most 2^23 stored rows, float eltypes, not VBC_CREATE_SERIAL (C sums each output over
+// B's columns in ascending order, not stripe by stripe), VBC_FWD_T != 0.
+static bool fwd_via_t_wanted(const vbc_handle *h, const Stripes &s, unsigned flags)
+{
+    if (h->fwd_t == 0 || (flags & VBC_CREATE_SERIAL) || h->dtype == VBC_I64) return false;
+    if ((int64_t)s.rows.size() > (int64_t(1) << 23)) return false;
+    int w0 = -1;
+    bool mixed = false;
+    for (int64_t l = 0; l < s.L && !mixed; l++) {
+        if (s.rbeg[l + 1] == s.rbeg[l]) continue;
+        if (w0 < 0) w0 = s.w[l];
+        mixed = s.w[l] != w0;
+    }
+    return mixed || h->fwd_t == 2;
+}
+
 static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
                          std::vector<std::vector<PendingBin>> &pbs, std::vector<std::vector<PendingSlot>> &pss,
                          std::vector<std::vector<PendingSweep>> &pws, std::vector<Launch> &Ls,
@@ -2011,16 +2030,16 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     return VBC_OK;
 }
 
-// Forward panel layout (VBC_CREATE_MULTI_FORWARD): Y = B·X is the transposed product of C = Bᵀ, so
-// the transposed panel layout of C serves it.  C's stripes are B's output row groups g (rows
-// [a_g, a_g + u_g), u_g <= 16): Π's block rows for a SparseMatrixVBC, else runs of consecutive rows
-// whose stripe lists are identical (a node's dof rows), else single rows.  Every stripe l of B that
-// stores rows of group g contributes w_l stored rows of C (its columns c, ascending), each holding the
-// u_g values B[a_g .. a_g+u_g-1, col0_l + c] (0 for a row of the group the stripe does not store) and
-// gathering X row col0_l + c.  Groups in row order, their stripes in stripe order (the reference's
-// forward loop, multiply_VBC.jl:68-77).
-static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                               std::vector<PendingPanel> &pps, PanelLaunch &L)
+// C = Bᵀ as stripes (the layouts of B's forward product built as transposed products of C): C's stripes
+// are B's output row groups g (rows [a_g, a_g + u_g), u_g <= maxu): Π's block rows for a SparseMatrixVBC,
+// else runs of consecutive rows whose stripe lists are identical (a node's dof rows), else single rows.
+// Every stripe l of B that stores rows of group g contributes w_l stored rows of C (its columns c,
+// ascending), each holding the u_g values B[a_g .. a_g+u_g-1, col0_l + c] and gathering x row col0_l + c.
+// Groups in row order, their stripes in stripe order (the reference's forward loop,
+// multiply_VBC.jl:68-77).  Every row of a group is stored by the same stripes, so C holds exactly the
+// values (fill zeros included) the reference multiplies.
+static int transpose_stripes(const vbc_handle *h, const Stripes &s, const char *val, int maxu, Stripes &c,
+                             std::vector<char> &cv)
 {
     const int esz = h->esz;
     const int64_t m = s.m;
@@ -2028,7 +2047,7 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
     std::vector<int64_t> a;
     if (!s.grp.empty()) {
         for (size_t k = 0; k + 1 < s.grp.size(); k++)
-            for (int64_t i = s.grp[k]; i < s.grp[k + 1]; i += 16) a.push_back(i);  // blocks taller than 16: pieces
+            for (int64_t i = s.grp[k]; i < s.grp[k + 1]; i += maxu) a.push_back(i);  // taller blocks: pieces
     } else {
         // the stripes storing each row (rows ascend inside a stripe, so each list comes out sorted)
         std::vector<int64_t> cnt(m + 1, 0);
@@ -2043,7 +2062,7 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
         };
         for (int64_t i = 0; i < m;) {
             int64_t e = i + 1;
-            while (e < m && e - i < 16 && cnt[i + 1] > cnt[i] && same(i, e)) e++;
+            while (e < m && e - i < maxu && cnt[i + 1] > cnt[i] && same(i, e)) e++;
             a.push_back(i);
             i = e;
         }
@@ -2067,7 +2086,7 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
         }
     }
     std::stable_sort(blks.begin(), blks.end(), [](const Blk &x, const Blk &y) { return x.g < y.g; });
-    Stripes c;
+    c = Stripes{};
     c.m = s.n;  // C = Bᵀ: its x is B's x (length n), its y is B's y (length m)
     c.n = m;
     c.L = ng;
@@ -2089,7 +2108,7 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
         c.voff[g] = nv;
         nv += (c.rbeg[g + 1] - c.rbeg[g]) * c.w[g];
     }
-    std::vector<char> cv((size_t)std::max<int64_t>(nv, 1) * esz, 0);
+    cv.assign((size_t)std::max<int64_t>(nv, 1) * esz, 0);
     std::vector<int64_t> at(c.rbeg.begin(), c.rbeg.end() - 1);  // next stored row of each group
     for (const Blk &b : blks) {
         const int64_t l = b.l, wl = s.w[l], u = c.w[b.g];
@@ -2118,6 +2137,18 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
             }
         }
     }
+    return VBC_OK;
+}
+
+// Forward panel layout (VBC_CREATE_MULTI_FORWARD): Y = B·X is the transposed product of C = Bᵀ, so the
+// transposed panel layout of C (transpose_stripes, groups up to 16 rows) serves it.
+static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
+                               std::vector<PendingPanel> &pps, PanelLaunch &L)
+{
+    Stripes c;
+    std::vector<char> cv;
+    if (int st = transpose_stripes(h, s, val, 16, c, cv)) return st;
+    const int64_t ng = c.L;
     int32_t widest = 0;
     for (int64_t g = 0; g < ng; g++) widest = std::max(widest, c.w[g]);
     h->mf_group = widest;
@@ -2214,13 +2245,13 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
     // the fused small-matrix split (build_transposed): every planar bin a split bin of the common P, all
     // of them one launch of spmv_split_multi (their chunks concatenated)
     L.fuse_split = 0;
-    if (h->small_split > 1) {
+    if (L.fuse_p > 1) {
         int nfb = 0;
         bool all = true;
         for (const SlotBin &b : L.pbins) {
             if (!b.fused) continue;
             nfb++;
-            all = all && b.kind == 0 && b.split == h->small_split && !b.kc && !b.lanes && !b.pair && !b.mask &&
+            all = all && b.kind == 0 && b.split == L.fuse_p && !b.kc && !b.lanes && !b.pair && !b.mask &&
                   b.diag == 0 && b.wkey >= 1 && b.wkey <= 8 && b.w == b.wkey && b.run >= 1 && b.run <= 3;
         }
         if (nfb > 0 && nfb <= kSplitParts && all) {
@@ -2236,7 +2267,7 @@ static int finalize_launch(vbc_handle *h, const std::vector<PendingBin> &pbs, co
             M.nparts = nfb;
             M.nchunks = c0;
             L.multi = M;
-            L.fuse_split = h->small_split;
+            L.fuse_split = L.fuse_p;
         } else {
             for (SlotBin &b : L.pbins) b.fused = 0;  // each split bin on its own launch
         }
@@ -2281,6 +2312,12 @@ static void release(vbc_handle *h)
     if (h->lt.d_sbins) (void)hipFree(h->lt.d_sbins);
     if (h->lt.d_wbins) (void)hipFree(h->lt.d_wbins);
     if (h->lt.d_pbins) (void)hipFree(h->lt.d_pbins);
+    if (h->lft.d_bins) (void)hipFree(h->lft.d_bins);
+    if (h->lft.d_sbins) (void)hipFree(h->lft.d_sbins);
+    if (h->lft.d_wbins) (void)hipFree(h->lft.d_wbins);
+    if (h->lft.d_pbins) (void)hipFree(h->lft.d_pbins);
+    for (hipStream_t q : h->lft.fork_streams) (void)hipStreamDestroy(q);
+    for (hipEvent_t e : h->lft.fork_events) (void)hipEventDestroy(e);
     if (h->lm.d_bins) (void)hipFree(h->lm.d_bins);
     if (h->lmf.d_bins) (void)hipFree(h->lmf.d_bins);
     for (auto &l : h->lf) {
@@ -2454,6 +2491,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
+    if (const char *e = getenv("VBC_FWD_T")) h->fwd_t = atoi(e);
     if (const char *e = getenv("VBC_SPLIT_DEEP")) h->split_deep = std::max(0.0, atof(e));
     if (const char *e = getenv("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
@@ -2511,7 +2549,29 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
             std::memcpy(ar.at<int32_t>(h->lt.o_fill), fill_t.data(), fill_t.size() * 4);
         }
     }
-    if (st == VBC_OK && (flags & VBC_CREATE_FORWARD)) {
+    std::vector<PendingBin> ptf;
+    std::vector<PendingSlot> stf;
+    std::vector<PendingSweep> swf;
+    std::vector<int32_t> fill_tf;
+    if (st == VBC_OK && (flags & VBC_CREATE_FORWARD) && fwd_via_t_wanted(h, s, flags)) {
+        // small mixed-width forward product as the transposed product of C = Bᵀ (one fused launch instead
+        // of a scale pass and one forward launch per width bucket, each adding into y)
+        Stripes c;
+        std::vector<char> cv;
+        st = transpose_stripes(h, s, v, 8, c, cv);
+        if (st == VBC_OK) {
+            const int64_t bt = h->bytes_t;
+            st = build_transposed(h, c, cv.data(), ar, ptf, stf, swf, h->lft, fill_tf);
+            h->bytes_f = h->bytes_t - bt;
+            h->bytes_t = bt;
+        }
+        if (st == VBC_OK) {
+            h->has_f = h->has_ft = true;
+            h->lft.nfill = (int)fill_tf.size();
+            h->lft.o_fill = ar.reserve(fill_tf.size() * 4);
+            std::memcpy(ar.at<int32_t>(h->lft.o_fill), fill_tf.data(), fill_tf.size() * 4);
+        }
+    } else if (st == VBC_OK && (flags & VBC_CREATE_FORWARD)) {
         st = build_forward(h, s, v, ar, pf, sf, wf, h->lf, fill_f);
         h->has_f = st == VBC_OK;
         if (st == VBC_OK) {
@@ -2533,25 +2593,28 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         return fail(VBC_HIP_ERROR, "hipMemcpy of the matrix arena failed");
     }
     if (h->has_t && (st = finalize_launch(h, pt, st_t, h->lt, sw_t))) { release(h); return st; }
-    if (h->has_t && h->fork && launch_groups(h->lt) >= 2) {  // side streams for the independent B'x groups
-        const int ns = std::min(launch_groups(h->lt) - 1, 3);
+    if (h->has_ft && (st = finalize_launch(h, ptf, stf, h->lft, swf))) { release(h); return st; }
+    for (Launch *lp : {&h->lt, &h->lft}) {  // side streams for the independent groups of a transposed launch
+        Launch &Lx = *lp;
+        if (!(lp == &h->lt ? h->has_t : h->has_ft) || !h->fork || launch_groups(Lx) < 2) continue;
+        const int ns = std::min(launch_groups(Lx) - 1, 3);
         for (int i = 0; i < ns; i++) {
             hipStream_t q = nullptr;
             if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipStreamCreate failed"); }
-            h->lt.fork_streams.push_back(q);
+            Lx.fork_streams.push_back(q);
         }
         for (int i = 0; i <= ns; i++) {
             hipEvent_t e = nullptr;
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipEventCreate failed"); }
-            h->lt.fork_events.push_back(e);
+            Lx.fork_events.push_back(e);
         }
     }
     if (h->has_m && (st = finalize_panel(h, pm, h->lm))) { release(h); return st; }
     if (h->has_mf && (st = finalize_panel(h, pmf, h->lmf))) { release(h); return st; }
     for (size_t b = 0; b < pf.size(); b++)
         if ((st = finalize_launch(h, pf[b], sf[b], h->lf[b], wf[b]))) { release(h); return st; }
-    if (h->has_f && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
-    h->has_scratch = h->has_t && !h->lt.bins.empty();
+    if (h->has_f && !h->has_ft && pf.empty() && (st = finalize_launch(h, {}, {}, h->lf[0]))) { release(h); return st; }
+    h->has_scratch = (h->has_t && !h->lt.bins.empty()) || (h->has_ft && !h->lft.bins.empty());
     for (const Launch &l : h->lf) h->has_scratch = h->has_scratch || (h->has_f && !l.bins.empty());
     *out = h;
     return VBC_OK;
@@ -2775,7 +2838,9 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->bins_t = h->has_t ? (int32_t)h->lt.bins.size() : 0;
     int32_t bf = 0;
     for (auto &l : h->lf) bf += (int32_t)l.bins.size();
+    if (h->has_ft) bf += (int32_t)(h->lft.bins.size() + h->lft.sbins.size() + h->lft.pbins.size() + h->lft.wbins.size());
     info->bins_f = h->has_f ? bf : 0;
+    if (h->has_ft) info->planar_mask |= 256;  // the forward product runs on the transposed layout of C = Bᵀ
     info->device_bytes = (int64_t)h->arena_bytes;
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;

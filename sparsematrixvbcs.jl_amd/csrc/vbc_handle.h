@@ -47,6 +47,7 @@ struct Launch {
     // small mixed-width B'x (vbc_device.hip build_transposed): every planar split bin in ONE launch of
     // spmv_split_multi with fuse_split waves per chunk (0: one launch per planar bin)
     int fuse_split = 0;
+    int fuse_p = 0;  // the fused split's P as build_transposed chose it (finalize_launch builds `multi`)
     SplitMulti multi{};
     std::vector<double> gwork;  // matrix bytes of each launch group (launch_groups order): the heaviest is
                                 // submitted last, so the small groups are already dispatched when it fills the chip
@@ -109,6 +110,9 @@ struct vbc_handle {
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch
+    vbc::Launch lft;              // forward product as the transposed product of C = Bᵀ (small mixed widths)
+    bool has_ft = false;
+    int fwd_t = 1;                // VBC_FWD_T: 0 never build the forward product on C = Bᵀ, 2 always
     std::vector<vbc::Launch> lf;  // forward product: one launch per width bucket
     bool f_scale = false;         // forward with several buckets: scale y by beta first
     int64_t bytes_t = 0, bytes_f = 0;

@@ -214,6 +214,7 @@ static int mul_device(const vbc_handle *h, int trans, const void *x, void *y, do
         return launch<T>(h, h->lt, 0, x, y, alpha, beta, beta != 0.0, stream);
     }
     if (h->m == 0) return VBC_OK;
+    if (h->has_ft) return launch<T>(h, h->lft, 0, x, y, alpha, beta, beta != 0.0, stream);  // on C = Bᵀ
     if (h->f_scale) {
         hipLaunchKernelGGL((scale<T>), dim3(std::min<int64_t>((h->m + kBlockThreads - 1) / kBlockThreads, 4096)),
                            dim3(kBlockThreads), 0, stream, static_cast<T *>(y), h->m, (T)beta, (int)(beta != 0.0));

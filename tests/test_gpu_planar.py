@@ -843,3 +843,45 @@ def test_fused_side_buckets_beside_a_dominant_width():
         y = torch.zeros(B.n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
         V.mul_(y, B.T, dev(x))
         assert rel(y.cpu().numpy(), O.mul(R, x.astype(np.float64), np.zeros(B.n), trans=True)) <= tol
+
+
+def test_forward_mixed_widths_on_transposed_layout(monkeypatch):
+    """B·x of a matrix whose stripes have several widths (the ct20stif stand-in's strict stripes, 1..6
+    wide) runs as the transposed product of C = Bᵀ (vbc_info planar_mask bit 8: C's stripes are B's row
+    groups, one fused launch): it matches the oracle's forward product (normwise 1e-12) with alpha /
+    beta, a NaN / Inf in x reaches exactly the rows the reference's stripes touch, fp32 agrees at 1e-5,
+    and VBC_FWD_T=0 (the per-width forward launches) and serial=True give the same result."""
+    import bench
+    B = bench.build_matrix("ct20stif", np.float64)
+    assert B.info(trans=False)["planar_mask"] & 256
+    R = ref_of(B)
+    rng = np.random.default_rng(50)
+    x = rng.uniform(-1, 1, B.n)
+    y0 = rng.uniform(-1, 1, B.m)
+    for alpha, beta in ((1.0, 0.0), (0.5, -1.5)):
+        y = dev(y0.copy())
+        V.mul_(y, B, dev(x), alpha, beta)
+        ref = O.mul(R, x, y0.copy(), alpha, beta, trans=False, ref_semantics=False)
+        assert rel(y.cpu().numpy(), ref) <= TOL64, (alpha, beta)
+    xn = x.copy()
+    xn[[7, 4001]] = [np.nan, np.inf]
+    y = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(y, B, dev(xn))
+    ref = O.mul(R, xn, np.zeros(B.m), trans=False)
+    got = y.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
+    assert rel(got[np.isfinite(ref)], ref[np.isfinite(ref)]) <= TOL64
+    yt = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(yt, B, dev(x))
+    monkeypatch.setenv("VBC_FWD_T", "0")
+    Bw = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+    assert not Bw.info(trans=False)["planar_mask"] & 256
+    yw = torch.zeros(B.m, dtype=torch.float64, device=DEV)
+    V.mul_(yw, Bw, dev(x))
+    assert rel(yw.cpu().numpy(), yt.cpu().numpy()) <= TOL64
+    monkeypatch.delenv("VBC_FWD_T")
+    B32 = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val.astype(np.float32))
+    y32 = torch.zeros(B.m, dtype=torch.float32, device=DEV)
+    V.mul_(y32, B32, dev(x.astype(np.float32)))
+    R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B32.val.astype(np.float64))
+    assert rel(y32.cpu().numpy(), O.mul(R64, x.astype(np.float32).astype(np.float64), np.zeros(B.m), trans=False)) <= TOL32
