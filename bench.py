@@ -50,6 +50,7 @@ WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
                         "AlternatingPacker(StrictChunker(8), StrictChunker(8)) tiles)",
              "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
              "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)",
+             "ct20stif-fwd": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8), forward y = B*x",
              "ldoor-csc": "C4 TrSpMV!(y, A, x) on the GHS_psdef/ldoor stand-in (CSC, 952203^2, 42.5M nnz)"}
 
 
@@ -90,8 +91,9 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
         return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
     if workload == "c5-mesh":
         return V.synthetic.c5_mesh(dtype=dtype, scale=scale, seed=seed)
-    if workload in ("ldoor", "ct20stif", "ldoor-csc"):
-        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ldoor-csc": "GHS_psdef/ldoor"}[workload]
+    if workload in ("ldoor", "ct20stif", "ct20stif-fwd", "ldoor-csc"):
+        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ct20stif-fwd": "Boeing/ct20stif",
+                "ldoor-csc": "GHS_psdef/ldoor"}[workload]
         try:
             A = V.io.mdopen(name, dtype=dtype).A
         except FileNotFoundError:
@@ -111,6 +113,12 @@ def kernel_name(B, local, k, trans=True):
             return ("vbc::spmm_quads<T, W, VEC> (VALU stripe quads: 16 stripes x 4 right-hand-side quads per wave, "
                     "csrc/vbc_panel.h)")
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
+    if not trans:
+        inf = B.info(local, False)
+        if inf["planar_mask"] & 256:
+            return ("the transposed kernels on C = B^T (forward of a mixed-width matrix: vbc::spmv_split_multi "
+                    "fused split over C's row groups, csrc/vbc_planar.h)")
+        return "forward kernels (vbc::spmv_planar_fwd / spmv_slots<T, 1, ...>, csrc/vbc_planar.h, vbc_slots.h)"
     inf = B.info(local, True)
     if inf["planar_bins"] > 0:
         if inf["planar_mask"] & 4:
@@ -282,7 +290,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     csc = not hasattr(B, "ofs")
     rng = np.random.default_rng(0xC0FFEE)
     k = args.nrhs if workload in ("c5", "c5-fwd", "c5-mesh") else 1
-    trans = workload != "c5-fwd"
+    trans = workload not in ("c5-fwd", "ct20stif-fwd")
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
     x_host = rng.uniform(-1, 1, (nx, k) if k > 1 else nx).astype(dtype)
     x = torch.from_numpy(x_host).to(device)  # k > 1: row-major X (right-hand sides interleaved)
@@ -327,7 +335,8 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
         "config": {
             "workload": WORKLOADS[workload] + (f"-scale{args.scale}" if args.scale != 1.0 else ""),
             "op": ("TrSpMV!(y, A, x) -- CSC transposed product (TrSpMV.jl:1-20)" if csc else
-                   "mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if k == 1 else
+                   ("mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if trans else
+                    "mul!(y, B, x) -- forward 1DVBC (multiply_1DVBC.jl:9-83)") if k == 1 else
                    f"Y = B'X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:89-192 per column), "
                    "matrix-core panel kernel" if trans else
                    f"Y = B*X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:3-87 per column), "
@@ -690,7 +699,7 @@ def main():
         if not args.no_secondary:
             sec = {}
             for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("c5-fwd", np.float32),
-                           ("c5-mesh", np.float32), ("ct20stif", np.float64), ("ldoor", np.float64),
+                           ("c5-mesh", np.float32), ("ct20stif", np.float64), ("ct20stif-fwd", np.float64), ("ldoor", np.float64),
                            ("ldoor-csc", np.float32)):
                 if wl == args.workload:
                     continue
