@@ -1148,7 +1148,7 @@ static void hole_runs(const vbc_handle *h, const Stripes &s, const std::vector<i
                 for (int d = 0; d < R; d++) {
                     const int64_t row = k * R + d;
                     if (r < s.rbeg[l + 1] && s.rows[r] == row) {
-                        hents.push_back({(uint32_t)row, s.voff[l] + (r - s.rbeg[l]) * w});
+                        hents.push_back({(uint32_t)row, s.voff[l] + (r - s.rbeg[l]) * s.vstride(l)});
                         r++;
                     } else {
                         hents.push_back({(uint32_t)row, -1});  // a hole of the run
@@ -1206,13 +1206,60 @@ static int build_ksplit(vbc_handle *h, int w, int ks, const std::vector<Entry> &
     return build_slots(h, 0, w, w, ents, sx, ox, total, val, ar, range0, ps, order, false, ks);
 }
 
+// Column pieces (B'x layouts only): when one width wd holds >= 80 % of the stripes, a side stripe whose
+// width is a multiple k·wd runs as k wd-wide stripes over the same stored rows (values addressed in
+// place through Stripes::vst).  The ldoor stand-in's 'min memory' partition is 317,337 3-wide stripes
+// and 32 6-wide ones: as two buckets, the 6-wide one is a single chunk whose wave walks 51 rows of
+// dependent loads at the loaded-memory latency of the streaming bucket beside it (42.6 us against the
+// strict partition's 33.8 us, profiles/r04_ab11_ldoor32_*.log).  Every output column keeps its
+// stripe's rows in stored order, so each column is summed exactly as before (multiply_1DVBC.jl:101-104).
+static bool column_pieces(const vbc_handle *h, const Stripes &s, Stripes &c)
+{
+    if (h->colsplit == 0 || s.L < 2) return false;
+    std::map<int, int64_t> cnt;
+    for (int64_t l = 0; l < s.L; l++) cnt[s.w[l]]++;
+    if (cnt.size() < 2) return false;
+    int wd = 0;
+    int64_t nd = 0;
+    for (auto &kv : cnt)
+        if (kv.second > nd) { nd = kv.second; wd = kv.first; }
+    if ((double)nd < 0.8 * (double)s.L) return false;
+    bool any = false;
+    for (auto &kv : cnt) any = any || (kv.first > wd && kv.first % wd == 0);
+    if (!any) return false;
+    c.m = s.m;
+    c.n = s.n;
+    c.grp = s.grp;
+    c.rbeg.assign(1, 0);
+    for (int64_t l = 0; l < s.L; l++) {
+        const int wl = s.w[l];
+        const int k = (wl > wd && wl % wd == 0) ? wl / wd : 1;
+        const int wp = k > 1 ? wd : wl;
+        for (int j = 0; j < k; j++) {
+            c.col0.push_back(s.col0[l] + (int64_t)j * wp);
+            c.w.push_back(wp);
+            c.voff.push_back(s.voff[l] + (int64_t)j * wp);
+            c.vst.push_back((int32_t)s.vstride(l));
+            c.rows.insert(c.rows.end(), s.rows.begin() + s.rbeg[l], s.rows.begin() + s.rbeg[l + 1]);
+            c.rbeg.push_back((int64_t)c.rows.size());
+        }
+    }
+    c.L = (int64_t)c.w.size();
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] column pieces: %lld stripes -> %lld (dominant width %d)\n", (long long)s.L,
+                (long long)c.L, wd);
+    return true;
+}
+
 // Transposed layout: segments = stripes of each width, entries = their stored rows.  A bucket runs
 // slotted (vbc_slots.h, every stripe of the width a segment, empty ones included) when its row counts
 // are near-uniform, else merged (non-empty stripes; empty ones go to the fill list).
-static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
+static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, Arena &ar,
                             std::vector<PendingBin> &pbs, std::vector<PendingSlot> &pss,
                             std::vector<PendingSweep> &pws, Launch &L, std::vector<int32_t> &fill)
 {
+    Stripes sp;
+    const Stripes &s = column_pieces(h, s0, sp) ? sp : s0;
     std::map<int, std::vector<int64_t>> buckets;  // w -> stripes
     for (int64_t l = 0; l < s.L; l++) buckets[s.w[l]].push_back(l);
     const int64_t total = (int64_t)s.rows.size();
@@ -1226,6 +1273,8 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     // (fp64) rows per wave; P is common to the launch.  VBC_SMALL_FUSE=0 turns it off.
     h->small_split = 0;
     h->fuse_w = 0;
+    // VBC_SMALL_FUSE=2: a single-width small matrix runs the fused split too (A/B)
+    const int fuse_min = h->small_fuse >= 2 ? 1 : 2;
     // Long stripes (SlotBin::ks): a chunk runs on one CU and costs its longest stripe's rows, so a few
     // chunks of long stripes (a 'min blocks' partition's widest, fullest stripes: 3.4x the mean chunk on
     // the ct20stif stand-in) set the product's time.  A stripe whose work (rows x width, values per
@@ -1233,7 +1282,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
     // laid side by side in the lanes of one chunk and summed across them before the store.
     std::vector<uint8_t> kst;  // per stripe: parts (empty: none cut)
     // (auto layouts only: a forced VBC_SLOTS / VBC_SLOT_PLANAR keeps the layout the tests ask for)
-    if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar < 0 && h->slots_mode < 0 && buckets.size() >= 2 &&
+    if (h->planar_split != 0 && h->small_fuse != 0 && h->slot_planar < 0 && h->slots_mode < 0 && (int)buckets.size() >= fuse_min &&
         (int)buckets.size() <= kSplitParts && buckets.rbegin()->first <= 8 && !sweep_possible(h, 1, s.m)) {
         // the fused buckets: all of them; or, when their chunks would overflow the launch and one bucket
         // holds most of them, every bucket but that one (a large operator's dominant width keeps its
@@ -1248,8 +1297,9 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             if (c > nmax) { nmax = c; wmax = kv.first; }
         }
         for (auto &kv : buckets) h->fuse_w |= 1u << kv.first;
-        if ((double)nall * 2 > slots0 && buckets.size() >= 3 && (double)nmax >= 0.8 * (double)nall)
-            h->fuse_w &= ~(1u << wmax);
+        const bool side = h->side_fuse < 0 ? (double)nall * 2 > slots0 && buckets.size() >= 3 && (double)nmax >= 0.8 * (double)nall
+                                           : h->side_fuse == 1 && (double)nmax >= 0.8 * (double)nall;
+        if (side) h->fuse_w &= ~(1u << wmax);
         auto fused_w = [&](int w) { return ((h->fuse_w >> w) & 1) != 0; };
         if (h->ksplit > 0) {
             double work = 0;
@@ -1296,7 +1346,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
         // (the batched slice loop costs a round trip per batch, not per step: thinner slices than the
         // single-bucket rule's split_rows pay off -- ct20stif 'min blocks' P = 4 / 8: 15.7 / 14.7 us)
         const double minrows = (double)h->small_rows * h->esz / 8.0;
-        if ((double)nch * 2 <= slots && nf >= 2) {
+        if ((double)nch * 2 <= slots && nf >= fuse_min) {
             int P = 1;
             while (P < 8 && (double)nch * P * 2 <= 2 * slots && avg / (P * 2) >= minrows) P *= 2;
             // fusing pays even when the chunks are too short to split: one launch instead of one per
@@ -1357,7 +1407,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                 sb.push_back(sb.back() + s.rbeg[l + 1] - s.rbeg[l]);
                 out.push_back((int32_t)s.col0[l]);
                 for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
-                    ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+                    ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * s.vstride(l)});
             }
             if (want_sweep(h, w, s.m, sb, ents)) {
                 PendingSweep pw;
@@ -1391,7 +1441,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             } else {
                 for (int64_t l : kv.second)
                     for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
-                        ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+                        ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * s.vstride(l)});
             }
             PendingSlot ps;
             if (int st = build_ksplit(h, w, ks, ents, sbeg, out, total, val, ar, srange0, ps)) return st;
@@ -1409,7 +1459,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
                 ents.reserve(sbeg.back());
                 for (int64_t l : kv.second)
                     for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
-                        ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * w});
+                        ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * s.vstride(l)});
             }
             PendingSlot ps;
             if (want_lanes(h, wps, w, sbeg, out, total, mask)) {
@@ -1430,7 +1480,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s, const char *val, Ar
             out.push_back((int32_t)s.col0[l]);
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++)
                 ents.push_back({(uint32_t)s.rows[r] | (r == s.rbeg[l] ? kHead : 0u),
-                                s.voff[l] + (r - s.rbeg[l]) * w});
+                                s.voff[l] + (r - s.rbeg[l]) * s.vstride(l)});
         }
         if (ents.empty()) continue;
         PendingBin pb;
@@ -2488,6 +2538,8 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
+    if (const char *e = getenv("VBC_SIDE_FUSE")) h->side_fuse = atoi(e) < 0 ? -1 : atoi(e) != 0;
+    if (const char *e = getenv("VBC_COLSPLIT")) h->colsplit = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
@@ -2850,6 +2902,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
         info->planar_mask |= 128;  // multi-RHS buckets in the VALU stripe-quad layout (spmm_quads)
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)(l.sbins.size() + l.pbins.size()) : 0;  // + planar forward
+    if (h->has_ft) sl += (int32_t)(h->lft.sbins.size() + h->lft.pbins.size());  // forward on C = Bᵀ's layout
     info->slot_bins = sl;
     int32_t sw = h->has_t ? (int32_t)h->lt.wbins.size() : 0;
     for (auto &l : h->lf) sw += h->has_f ? (int32_t)l.wbins.size() : 0;

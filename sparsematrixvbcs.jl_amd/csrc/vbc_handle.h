@@ -85,6 +85,9 @@ struct Stripes {
     std::vector<int64_t> rbeg;  // L+1 prefix into rows
     std::vector<int32_t> rows;  // 0-based x row of each stored w-wide row
     std::vector<int64_t> voff;  // element offset of the stripe's first value in the input val
+    std::vector<int32_t> vst;   // per stripe: elements between its stored rows' values (empty: the width;
+                                // a column piece keeps its source stripe's stride)
+    int64_t vstride(int64_t l) const { return vst.empty() ? w[l] : vst[l]; }
     std::vector<int64_t> grp;   // 2D input: Π's block-row starts (K + 1, 0-based); empty for 1D / CSC
 };
 
@@ -159,6 +162,10 @@ struct vbc_handle {
     int small_split = 0;              // > 1: this B'x layout is the fused small-matrix split with P waves per chunk
     uint32_t fuse_w = 0;              // bit w: the width-w bucket belongs to the fused split (all, or the side buckets)
     int small_fuse = 1;               // VBC_SMALL_FUSE: 0 = never fuse the buckets of a small matrix
+    int side_fuse = -1;               // VBC_SIDE_FUSE: the dominant bucket outside the fused split (-1 auto, 0 never,
+                                      // 1 whenever one width holds >= 80 % of the chunks)
+    int colsplit = 1;                 // VBC_COLSPLIT=0: no column pieces (side stripes of a multiple of the
+                                      // dominant width run as that many dominant-width stripes)
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split
     int cus = 256;                    // compute units of the device

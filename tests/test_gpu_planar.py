@@ -885,3 +885,30 @@ def test_forward_mixed_widths_on_transposed_layout(monkeypatch):
     V.mul_(y32, B32, dev(x.astype(np.float32)))
     R64 = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B32.val.astype(np.float64))
     assert rel(y32.cpu().numpy(), O.mul(R64, x.astype(np.float32).astype(np.float64), np.zeros(B.m), trans=False)) <= TOL32
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_column_pieces_side_stripes(dtype, monkeypatch):
+    """One dominant width (3) with a few 6-wide side stripes (the ldoor stand-in's 'min memory' shape):
+    the side stripes run as pairs of 3-wide column pieces in the dominant bucket (one planar bin
+    instead of two), bitwise equal to VBC_COLSPLIT=0 and to the oracle in the reference's serial order."""
+    L = 60000
+    widths = np.full(L, 3)
+    widths[7::997] = 6
+    widths[11::1999] = 9
+    B = V.synthetic.vbr_1dvbc(120000, L, 8 * L, widths, W=9, dtype=dtype, seed=71)
+    R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    x = np.random.default_rng(72).uniform(-1, 1, B.m).astype(dtype)
+    want = O.mul(R, x.astype(np.float64), np.zeros(B.n), trans=True)
+    ys, bins = [], []
+    for cs in ("1", "0"):
+        monkeypatch.setenv("VBC_COLSPLIT", cs)
+        Bc = V.SparseMatrix1DVBC(B.W, B.m, B.n, B.Phi, B.pos, B.idx, B.ofs, B.val)
+        Bc.serial = True
+        bins.append(Bc.info(trans=True)["planar_bins"])
+        y = torch.zeros(B.n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=DEV)
+        V.mul_(y, Bc.T, dev(x))
+        ys.append(y.cpu().numpy())
+        assert rel(ys[-1], want) <= (TOL64 if dtype == np.float64 else TOL32)
+    assert bins[0] < bins[1], bins
+    assert np.array_equal(ys[0], ys[1])
