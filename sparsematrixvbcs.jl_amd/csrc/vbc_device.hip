@@ -1215,17 +1215,23 @@ static int build_ksplit(vbc_handle *h, int w, int ks, const std::vector<Entry> &
 // stripe's rows in stored order, so each column is summed exactly as before (multiply_1DVBC.jl:101-104).
 static bool column_pieces(const vbc_handle *h, const Stripes &s, Stripes &c)
 {
-    if (h->colsplit == 0 || s.L < 2) return false;
+    if (h->colsplit == 0 || s.L < 1) return false;
     std::map<int, int64_t> cnt;
     for (int64_t l = 0; l < s.L; l++) cnt[s.w[l]]++;
-    if (cnt.size() < 2) return false;
     int wd = 0;
     int64_t nd = 0;
     for (auto &kv : cnt)
         if (kv.second > nd) { nd = kv.second; wd = kv.first; }
-    if ((double)nd < 0.8 * (double)s.L) return false;
+    // VBC_COLSPLIT_W=c (A/B): every stripe wider than c as pieces of c columns (+ the remainder)
+    const int cw = h->colsplit_w;
     bool any = false;
-    for (auto &kv : cnt) any = any || (kv.first > wd && kv.first % wd == 0);
+    if (cw > 0) {
+        wd = cw;
+        for (auto &kv : cnt) any = any || kv.first > cw;
+    } else {
+        if (cnt.size() < 2 || (double)nd < 0.8 * (double)s.L) return false;
+        for (auto &kv : cnt) any = any || (kv.first > wd && kv.first % wd == 0);
+    }
     if (!any) return false;
     c.m = s.m;
     c.n = s.n;
@@ -1233,12 +1239,12 @@ static bool column_pieces(const vbc_handle *h, const Stripes &s, Stripes &c)
     c.rbeg.assign(1, 0);
     for (int64_t l = 0; l < s.L; l++) {
         const int wl = s.w[l];
-        const int k = (wl > wd && wl % wd == 0) ? wl / wd : 1;
-        const int wp = k > 1 ? wd : wl;
-        for (int j = 0; j < k; j++) {
-            c.col0.push_back(s.col0[l] + (int64_t)j * wp);
+        const bool cut = wl > wd && (cw > 0 || wl % wd == 0);
+        for (int c0 = 0; c0 < wl; c0 += cut ? wd : wl) {
+            const int wp = cut ? std::min(wd, wl - c0) : wl;
+            c.col0.push_back(s.col0[l] + c0);
             c.w.push_back(wp);
-            c.voff.push_back(s.voff[l] + (int64_t)j * wp);
+            c.voff.push_back(s.voff[l] + c0);
             c.vst.push_back((int32_t)s.vstride(l));
             c.rows.insert(c.rows.end(), s.rows.begin() + s.rbeg[l], s.rows.begin() + s.rbeg[l + 1]);
             c.rbeg.push_back((int64_t)c.rows.size());
@@ -1273,8 +1279,20 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
     // (fp64) rows per wave; P is common to the launch.  VBC_SMALL_FUSE=0 turns it off.
     h->small_split = 0;
     h->fuse_w = 0;
-    // VBC_SMALL_FUSE=2: a single-width small matrix runs the fused split too (A/B)
-    const int fuse_min = h->small_fuse >= 2 ? 1 : 2;
+    // A single-width small matrix runs the fused split when its bucket would otherwise take the merge
+    // layout (chunks too long to balance one wave each: the 3dtube stand-in's 'overlap' partition, 15,110
+    // 3-wide stripes of ~71 rows, fp64 16.4 -> 7.8 us, fp32 14.2 -> 6.8 us); a bucket the planar layouts
+    // take keeps them (ldoor's 1/8 stripe shard: masked planar 12.4 us, fused 14.3 us,
+    // profiles/r04_ab13_*.log, r04_ab15_*.log).  VBC_SMALL_FUSE=2 fuses every single-width one.
+    int fuse_min = h->small_fuse >= 2 ? 1 : 2;
+    if (fuse_min == 2 && h->small_fuse == 1 && buckets.size() == 1 && buckets.begin()->first <= 8) {
+        const int w = buckets.begin()->first;
+        const int wps = slot_planar(h, 0, w) ? w : (h->esz == 8 && w == 3) ? 3 : padded_width(h, w);
+        std::vector<int64_t> sb{0}, order;
+        for (int64_t l : buckets.begin()->second) sb.push_back(sb.back() + s.rbeg[l + 1] - s.rbeg[l]);
+        bool mask = false;
+        if (!(sweep_possible(h, w, s.m)) && want_slots(h, 0, wps, sb, total, s.m, order, &mask, w) == 0) fuse_min = 1;
+    }
     // Long stripes (SlotBin::ks): a chunk runs on one CU and costs its longest stripe's rows, so a few
     // chunks of long stripes (a 'min blocks' partition's widest, fullest stripes: 3.4x the mean chunk on
     // the ct20stif stand-in) set the product's time.  A stripe whose work (rows x width, values per
@@ -1745,6 +1763,8 @@ static int build_fwd_lanes(vbc_handle *h, int w, int R, const std::vector<Entry>
 static bool fwd_via_t_wanted(const vbc_handle *h, const Stripes &s, unsigned flags)
 {
     if (h->fwd_t == 0 || (flags & VBC_CREATE_SERIAL) || h->dtype == VBC_I64) return false;
+    // a forced layout family (VBC_SLOTS / VBC_SWEEP / VBC_SLOT_PLANAR) keeps the forward layouts the tests ask for
+    if (h->fwd_t != 2 && (h->slots_mode >= 0 || h->sweep_mode >= 0 || h->slot_planar >= 0)) return false;
     if ((int64_t)s.rows.size() > (int64_t(1) << 23)) return false;
     int w0 = -1;
     bool mixed = false;
@@ -2540,6 +2560,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
     if (const char *e = getenv("VBC_SIDE_FUSE")) h->side_fuse = atoi(e) < 0 ? -1 : atoi(e) != 0;
     if (const char *e = getenv("VBC_COLSPLIT")) h->colsplit = atoi(e) != 0;
+    if (const char *e = getenv("VBC_COLSPLIT_W")) h->colsplit_w = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
