@@ -2532,6 +2532,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     // fp64 only (profiles/r03_sweeppack_*.log)
     h->sweep_pack = h->esz == 8;
     if (const char *e = getenv("VBC_FORK")) h->fork = atoi(e) != 0;
+    if (const char *e = getenv("VBC_FORK_SIDE_KB")) h->fork_side_bytes = atof(e) * 1024.0;
     if (const char *e = getenv("VBC_SWEEP_PACK")) h->sweep_pack = atoi(e) != 0;
     if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
     if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
@@ -2670,6 +2671,17 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     for (Launch *lp : {&h->lt, &h->lft}) {  // side streams for the independent groups of a transposed launch
         Launch &Lx = *lp;
         if (!(lp == &h->lt ? h->has_t : h->has_ft) || !h->fork || launch_groups(Lx) < 2) continue;
+        // no fork beside one dominant group when the others are more than a few waves of work: they are
+        // latency-bound, and beside a launch that saturates HBM their dependent loads wait on a loaded
+        // memory system while holding its wave slots (the ldoor stand-in's fp64 'min blocks': merge
+        // kernel 131.5 us + fused side launch 11.5 us one after another, 160.3 / 88.7 us side by side;
+        // 154 against 188 us per product, profiles/r04_bprof_*).  A side group of a few chunks still
+        // forks (its one wave hides under the big launch).
+        if ((int)Lx.gwork.size() == launch_groups(Lx)) {
+            double tot = 0, big = 0;
+            for (double wk : Lx.gwork) { tot += wk; big = std::max(big, wk); }
+            if (big >= 0.9 * tot && tot - big > h->fork_side_bytes) continue;
+        }
         const int ns = std::min(launch_groups(Lx) - 1, 3);
         for (int i = 0; i < ns; i++) {
             hipStream_t q = nullptr;

@@ -166,6 +166,8 @@ struct vbc_handle {
                                       // 1 whenever one width holds >= 80 % of the chunks)
     int colsplit = 1;                 // VBC_COLSPLIT=0: no column pieces (side stripes of a multiple of the
                                       // dominant width run as that many dominant-width stripes)
+    double fork_side_bytes = 1 << 20; // VBC_FORK_SIDE_KB: beside a group with >= 90 % of the bytes, the others fork only
+                                      // while they hold at most this many bytes
     int colsplit_w = 0;               // VBC_COLSPLIT_W=c: every stripe wider than c as c-wide pieces (A/B)
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split
