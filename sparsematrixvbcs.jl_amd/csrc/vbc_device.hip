@@ -1284,15 +1284,18 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
     // 3-wide stripes of ~71 rows, fp64 16.4 -> 7.8 us, fp32 14.2 -> 6.8 us); a bucket the planar layouts
     // take keeps them (ldoor's 1/8 stripe shard: masked planar 12.4 us, fused 14.3 us,
     // profiles/r04_ab13_*.log, r04_ab15_*.log).  VBC_SMALL_FUSE=2 fuses every single-width one.
-    int fuse_min = h->small_fuse >= 2 ? 1 : 2;
-    if (fuse_min == 2 && h->small_fuse == 1 && buckets.size() == 1 && buckets.begin()->first <= 8) {
-        const int w = buckets.begin()->first;
+    // (a bucket headed for the merge layout: no slotted / planar layout balances its chunks)
+    auto merge_bound = [&](int w, const std::vector<int64_t> &stripes) {
+        if (w > 8 || sweep_possible(h, w, s.m)) return false;
         const int wps = slot_planar(h, 0, w) ? w : (h->esz == 8 && w == 3) ? 3 : padded_width(h, w);
         std::vector<int64_t> sb{0}, order;
-        for (int64_t l : buckets.begin()->second) sb.push_back(sb.back() + s.rbeg[l + 1] - s.rbeg[l]);
+        for (int64_t l : stripes) sb.push_back(sb.back() + s.rbeg[l + 1] - s.rbeg[l]);
         bool mask = false;
-        if (!(sweep_possible(h, w, s.m)) && want_slots(h, 0, wps, sb, total, s.m, order, &mask, w) == 0) fuse_min = 1;
-    }
+        return want_slots(h, 0, wps, sb, total, s.m, order, &mask, w) == 0;
+    };
+    int fuse_min = h->small_fuse >= 2 ? 1 : 2;
+    if (fuse_min == 2 && h->small_fuse == 1 && buckets.size() == 1 && merge_bound(buckets.begin()->first, buckets.begin()->second))
+        fuse_min = 1;
     // Long stripes (SlotBin::ks): a chunk runs on one CU and costs its longest stripe's rows, so a few
     // chunks of long stripes (a 'min blocks' partition's widest, fullest stripes: 3.4x the mean chunk on
     // the ct20stif stand-in) set the product's time.  A stripe whose work (rows x width, values per
@@ -1315,7 +1318,12 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
             if (c > nmax) { nmax = c; wmax = kv.first; }
         }
         for (auto &kv : buckets) h->fuse_w |= 1u << kv.first;
-        const bool side = h->side_fuse < 0 ? (double)nall * 2 > slots0 && buckets.size() >= 3 && (double)nmax >= 0.8 * (double)nall
+        // a dominant bucket headed for the merge layout is better fused too, up to one chunk per wave slot
+        // (the ldoor stand-in's fp64 'min blocks', 2,358 chunks of 6-wide stripes of 69 rows: merge kernel
+        // 131.5 us + the fused side launch 11.5 us; all fused 131.5 us, profiles/r04_ab17_ldoor64_blocks.log)
+        const bool dom_merge = h->side_fuse < 0 && (double)nmax >= 0.8 * (double)nall && (double)nall <= slots0 &&
+                               merge_bound(wmax, buckets[wmax]);
+        const bool side = h->side_fuse < 0 ? (double)nall * 2 > slots0 && buckets.size() >= 3 && (double)nmax >= 0.8 * (double)nall && !dom_merge
                                            : h->side_fuse == 1 && (double)nmax >= 0.8 * (double)nall;
         if (side) h->fuse_w &= ~(1u << wmax);
         auto fused_w = [&](int w) { return ((h->fuse_w >> w) & 1) != 0; };
@@ -1364,7 +1372,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
         // (the batched slice loop costs a round trip per batch, not per step: thinner slices than the
         // single-bucket rule's split_rows pay off -- ct20stif 'min blocks' P = 4 / 8: 15.7 / 14.7 us)
         const double minrows = (double)h->small_rows * h->esz / 8.0;
-        if ((double)nch * 2 <= slots && nf >= fuse_min) {
+        if ((double)nch * (dom_merge ? 1 : 2) <= slots && nf >= fuse_min) {
             int P = 1;
             while (P < 8 && (double)nch * P * 2 <= 2 * slots && avg / (P * 2) >= minrows) P *= 2;
             // fusing pays even when the chunks are too short to split: one launch instead of one per
