@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--nrhs", type=int, default=0, help=">0: time the multi-RHS product (row-major X / Y)")
     ap.add_argument("--shard", default="", help="R/N: time stripe shard R of the N-way split (distributed.stripe_split)")
     ap.add_argument("--method", default="", help="ct20stif / ldoor / 3dtube / thermal1: build the stand-in with this "
-                    "bin/test_table.jl method instead of StrictChunker(8): overlap | blocks | memory | overlap2d07")
+                    "bin/test_table.jl method instead of StrictChunker(8): overlap | blocks | memory | overlap2d07 | blocks2d")
     ap.add_argument("--graph", action="store_true",
                     help="time each variant as one HIP-graph replay of --reps products (span / reps), as bench.py "
                          "does: per-launch event brackets inflate small kernels")
@@ -53,7 +53,12 @@ def main():
         meth = {"": V.StrictChunker(8), "strict": V.StrictChunker(8), "overlap": V.OverlapChunker(0.9, 8),
                 "blocks": V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks())),
                 "memory": V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_memory(dtype, np.int64)))}
-        if args.method == "overlap2d07":
+        if args.method == "blocks2d":  # bin/test_table.jl 'dynamic blocks 2D'
+            b2 = V.model_SparseMatrixVBC_blocks()
+            B = V.SparseMatrixVBC[8, 8](A, V.AlternatingPacker(V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks())),
+                                                               V.DynamicTotalChunker(lim(V.permutedims(b2))),
+                                                               V.DynamicTotalChunker(lim(b2))))
+        elif args.method == "overlap2d07":
             B = V.SparseMatrixVBC[8, 8](A, V.AlternatingPacker(V.OverlapChunker(0.7, 8), V.OverlapChunker(0.7, 8)))
         else:
             B = V.SparseMatrix1DVBC[8](A, meth[args.method])
