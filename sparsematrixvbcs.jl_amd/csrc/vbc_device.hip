@@ -1382,7 +1382,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
             // waves -- the ldoor stand-in's 'min blocks', 2550 chunks: P = 2 / 4 / 8 give 1.25 / 2.5 / 5.0
             // rounds of 4096 fp32 waves (70.9 / 70.1 / 66.0 us, profiles/r04_ab7_ldoor32_blocks.log)
             auto rounds = [&](int p) {
-                const double cap = (double)h->cus * std::max(1, h->occ_multi[p == 2 ? 1 : p == 4 ? 2 : p == 8 ? 3 : 4]);
+                const double cap = (double)h->cus * std::max(1, h->occ_multi[p == 2 ? 1 : p == 4 ? 2 : 3]);
                 return (double)nch * p / cap;
             };
             if (rounds(P) > 1.0) {
@@ -2569,7 +2569,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
     if (const char *e = getenv("VBC_SIDE_FUSE")) h->side_fuse = atoi(e) < 0 ? -1 : atoi(e) != 0;
     if (const char *e = getenv("VBC_COLSPLIT")) h->colsplit = atoi(e) != 0;
-    if (const char *e = getenv("VBC_FUSE_PMAX")) h->fuse_pmax = atoi(e) >= 16 ? 16 : atoi(e) >= 8 ? 8 : atoi(e) >= 4 ? 4 : 2;
+    if (const char *e = getenv("VBC_FUSE_PMAX")) h->fuse_pmax = atoi(e) >= 8 ? 8 : atoi(e) >= 4 ? 4 : 2;
     if (const char *e = getenv("VBC_COLSPLIT_W")) h->colsplit_w = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
     if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
@@ -2582,7 +2582,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     h->cus = std::max(1, prop.multiProcessorCount);
-    for (int lp = 1; lp <= 4; lp++) h->occ_multi[lp] = occupancy_split_multi(h->esz, 1 << lp);
+    for (int lp = 1; lp <= 3; lp++) h->occ_multi[lp] = occupancy_split_multi(h->esz, 1 << lp);
     if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));
         h->occ_p = 1;

@@ -168,12 +168,13 @@ struct vbc_handle {
                                       // dominant width run as that many dominant-width stripes)
     double fork_side_bytes = 1 << 20; // VBC_FORK_SIDE_KB: beside a group with >= 90 % of the bytes, the others fork only
                                       // while they hold at most this many bytes
-    int fuse_pmax = 8;                // VBC_FUSE_PMAX: most waves per chunk of the fused split launch (2 / 4 / 8 / 16)
+    int fuse_pmax = 8;                // VBC_FUSE_PMAX: most waves per chunk of the fused split launch (2 / 4 / 8; P = 16,
+                                      // 1024-thread workgroups, measured 1.4-1.9x slower: profiles/r04_ab20_*.log)
     int colsplit_w = 0;               // VBC_COLSPLIT_W=c: every stripe wider than c as c-wide pieces (A/B)
     int64_t split_nt_bytes = 0;       // VBC_SPLIT_NT_MB: value bytes above which split bins stream nt (0: never)
     int small_rows = 8;               // VBC_SMALL_ROWS: fewest chunk rows per wave (fp64) of the fused small split
     int cus = 256;                    // compute units of the device
-    int occ_multi[5] = {0, 0, 0, 0, 0};  // resident waves per CU of the fused split launch, P = 2 / 4 / 8 / 16 (index log2 P)
+    int occ_multi[4] = {0, 0, 0, 0};  // resident waves per CU of the fused split launch, P = 2 / 4 / 8 (index log2 P)
     double ksplit = 1.0;              // VBC_KSPLIT: fused split stripes above this x the mean chunk work are cut
                                       // into 2 / 4 lane parts (SlotBin::ks; 0: never)
     int split_pipe = -1;              // VBC_SPLIT_PIPE: split bins' pipelined slice loop (-1 auto, 0 off, 1 on)

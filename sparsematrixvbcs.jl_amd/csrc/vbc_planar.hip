@@ -270,7 +270,6 @@ static int launch_split_multi_t(const SplitMulti &M, int P, const void *x, void 
     case 2: VBC_MULTI(2) break;
     case 4: VBC_MULTI(4) break;
     case 8: VBC_MULTI(8) break;
-    case 16: VBC_MULTI(16) break;
     default: return (int)hipErrorInvalidValue;
     }
 #undef VBC_MULTI
@@ -291,11 +290,9 @@ int occupancy_split_multi(int esz, int P)
     int nb = 0;
 #define VBC_OCC_MULTI(TT, PP) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, spmv_split_multi<TT, PP, 2>, 64 * PP, 0)
     if (esz == 8) {
-        if (P == 2) VBC_OCC_MULTI(double, 2); else if (P == 4) VBC_OCC_MULTI(double, 4);
-        else if (P == 8) VBC_OCC_MULTI(double, 8); else VBC_OCC_MULTI(double, 16);
+        if (P == 2) VBC_OCC_MULTI(double, 2); else if (P == 4) VBC_OCC_MULTI(double, 4); else VBC_OCC_MULTI(double, 8);
     } else {
-        if (P == 2) VBC_OCC_MULTI(float, 2); else if (P == 4) VBC_OCC_MULTI(float, 4);
-        else if (P == 8) VBC_OCC_MULTI(float, 8); else VBC_OCC_MULTI(float, 16);
+        if (P == 2) VBC_OCC_MULTI(float, 2); else if (P == 4) VBC_OCC_MULTI(float, 4); else VBC_OCC_MULTI(float, 8);
     }
 #undef VBC_OCC_MULTI
     return nb * P;
