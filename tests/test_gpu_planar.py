@@ -912,3 +912,25 @@ def test_column_pieces_side_stripes(dtype, monkeypatch):
         assert rel(ys[-1], want) <= (TOL64 if dtype == np.float64 else TOL32)
     assert bins[0] < bins[1], bins
     assert np.array_equal(ys[0], ys[1])
+
+
+def test_ldoor_min_blocks_and_min_memory_partitions():
+    """The ldoor stand-in under the reference's 'min blocks' partition (150,920 6-wide stripes beside 3-, 7-
+    and 8-wide ones; fp64 its dominant bucket is merge-bound, so it is fused with the side buckets: one
+    fused split launch, planar_mask bit 5) and 'min memory' (32 6-wide stripes beside 317,337 3-wide ones,
+    run as 3-wide column pieces: one planar bin): both match the oracle (bin/test_table.jl:67-69)."""
+    A = V.synthetic.standin("GHS_psdef/ldoor", np.float64).T.tocsc()
+    lim = lambda mdl: V.ConstrainedCost(mdl, V.VertexCount(), 8)
+    rng = np.random.default_rng(81)
+    for name, meth in (("blocks", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_blocks()))),
+                       ("memory", V.DynamicTotalChunker(lim(V.model_SparseMatrix1DVBC_memory(np.float64, np.int64))))):
+        B = V.SparseMatrix1DVBC[8](A, meth)
+        inf = B.info(trans=True)
+        if name == "blocks":
+            assert inf["planar_mask"] & 32, inf
+        else:
+            assert inf["planar_bins"] == 1, inf
+        x = rng.uniform(-1, 1, B.m)
+        y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+        V.mul_(y, B.T, dev(x))
+        assert rel(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(B.n), trans=True)) <= TOL64, name
