@@ -565,7 +565,9 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         const double rows_per_wave = (double)rows / (double)std::max<int64_t>(nch, 1) / split;
         const int u0 = (9 / w) / run * run;  // planar_split_step (vbc_planar.h, VBC_SPLIT_VALS = 9)
         const double step_rows = (double)std::min(8 * run, std::max(run, u0));
-        b.deep = h->split_pipe >= 0 ? h->split_pipe : (rows_per_wave > h->split_deep * step_rows ? 2 : 0);
+        // (fused bins only: a single-bucket split bin keeps the plain loop -- ldoor's 1/8 stripe shard 12.4 us
+        // batched, 11.1 us plain, profiles/r04_ab22_*.log)
+        b.deep = h->split_pipe >= 0 ? h->split_pipe : (b.fused && rows_per_wave > h->split_deep * step_rows ? 2 : 0);
         // VBC_SPLIT_NT_MB: above that many value bytes the batched loop reads keys and values non-temporally
         // (mode 3).  Off by default: slower on every table partition, the 300 MB ldoor 'min blocks' too
         // (68.3 -> 77.7 us; ct20stif strict 8.9 -> 12.3 us; profiles/r04_ab4_*.log)
