@@ -48,7 +48,10 @@ WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
              "c5-fwd": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS forward Y = B*X (costs.jl:200-220 generator)",
              "c5-mesh": "C5-VBC2D-3x3-node-tiles-2Mx2M-1e8nnz-16RHS (structured: 3D stiffness stand-in, "
                         "AlternatingPacker(StrictChunker(8), StrictChunker(8)) tiles)",
+             "fe-fwd": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2 (SuiteSparse-like mesh operator), forward y = B*x",
+             "fe3d-fwd": "FE-3D-stiffness-dof3-1e7x1e7-1e8nnz-w3 (irregular: random 18-neighbour subsets), forward y = B*x",
              "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
+             "ldoor-fwd": "C3 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3, forward y = B*x",
              "ct20stif": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8)",
              "ct20stif-fwd": "C2 Boeing/ct20stif stand-in 52329^2 2.6M nnz, StrictChunker(8), forward y = B*x",
              "ldoor-csc": "C4 TrSpMV!(y, A, x) on the GHS_psdef/ldoor stand-in (CSC, 952203^2, 42.5M nnz)"}
@@ -82,6 +85,8 @@ def load_traffic(workload, dtype):
 
 def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
     import sparsematrixvbcs_amd as V
+    if workload in ("fe-fwd", "fe3d-fwd", "ldoor-fwd", "ct20stif-fwd"):  # the same matrix, forward product
+        workload = workload[:-4]
     if workload == "fe":
         return V.synthetic.fe_grid_2d(int(round(2236 * scale ** 0.5)), dof=2, dtype=dtype, seed=seed)
     if workload == "fe3d":
@@ -91,9 +96,8 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
         return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
     if workload == "c5-mesh":
         return V.synthetic.c5_mesh(dtype=dtype, scale=scale, seed=seed)
-    if workload in ("ldoor", "ct20stif", "ct20stif-fwd", "ldoor-csc"):
-        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ct20stif-fwd": "Boeing/ct20stif",
-                "ldoor-csc": "GHS_psdef/ldoor"}[workload]
+    if workload in ("ldoor", "ct20stif", "ldoor-csc"):
+        name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ldoor-csc": "GHS_psdef/ldoor"}[workload]
         try:
             A = V.io.mdopen(name, dtype=dtype).A
         except FileNotFoundError:
@@ -115,11 +119,28 @@ def kernel_name(B, local, k, trans=True):
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     if not trans:
         inf = B.info(local, False)
-        if inf["planar_mask"] & 256:
+        pm, R = inf["planar_mask"], inf["fwd_run"]
+        if pm & 256:
             return ("the transposed kernels on C = B^T (forward of a mixed-width matrix: vbc::spmv_split_multi "
                     "fused split over C's row groups, csrc/vbc_planar.h)")
-        return "forward kernels (vbc::spmv_planar_fwd / spmv_slots<T, 1, ...>, csrc/vbc_planar.h, vbc_slots.h)"
+        if pm & 16:
+            return (f"vbc::spmv_planar_lanes<T, W={R}, RUN, DEEP, RD> (forward lane streams: node blocks of "
+                    f"{R} output rows transposed into the B'x lane-stream layout, csrc/vbc_planar.h)")
+        if pm & 8:
+            return f"vbc::spmv_planar_fwd_split<T, W, R={R}, P> (split forward chunks, csrc/vbc_planar.h)"
+        if R > 1:
+            return (f"vbc::spmv_planar_fwd<T, W, R={R}, FASTE, NB, KC> (forward row runs: one x-slice gather per "
+                    f"block serves {R} output rows" + (", masked chunk-local order" if pm & 2 else "") +
+                    ", csrc/vbc_planar.h)")
+        if inf["sweep_bins"] > 0:
+            return "vbc::spmv_sweep<T, TB> kind 1 (row-swept tiles, one accumulator per output row, csrc/vbc_sweep.hip)"
+        if inf["slot_bins"] > 0:
+            return "vbc::spmv_slots<T, 1, U, FASTE> (slotted output rows, csrc/vbc_slots.h)"
+        return "vbc::spmv_ranges<T, 1, K, P> (merge layout, csrc/vbc_kernels.h)"
     inf = B.info(local, True)
+    if inf["planar_mask"] & 32:
+        return (f"vbc::spmv_split_multi<T, P={inf['planar_split']}, MODE> (fused small-matrix split: every width "
+                "bucket in one launch, P waves per 64-stripe chunk, csrc/vbc_planar.h)")
     if inf["planar_bins"] > 0:
         if inf["planar_mask"] & 4:
             return (f"vbc::spmv_planar_lanes<T, W, RUN={inf['planar_run']}, DEEP, RD> (per-lane compacted streams: "
@@ -290,7 +311,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     csc = not hasattr(B, "ofs")
     rng = np.random.default_rng(0xC0FFEE)
     k = args.nrhs if workload in ("c5", "c5-fwd", "c5-mesh") else 1
-    trans = workload not in ("c5-fwd", "ct20stif-fwd")
+    trans = not workload.endswith("-fwd")
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
     x_host = rng.uniform(-1, 1, (nx, k) if k > 1 else nx).astype(dtype)
     x = torch.from_numpy(x_host).to(device)  # k > 1: row-major X (right-hand sides interleaved)
@@ -698,8 +719,9 @@ def main():
         out["device"] = box_info(device)
         if not args.no_secondary:
             sec = {}
-            for wl, dt in (("fe3d", dtype), ("ns", dtype), ("c5", np.float32), ("c5-fwd", np.float32),
-                           ("c5-mesh", np.float32), ("ct20stif", np.float64), ("ct20stif-fwd", np.float64), ("ldoor", np.float64),
+            for wl, dt in (("fe-fwd", dtype), ("fe3d", dtype), ("fe3d-fwd", dtype), ("ns", dtype), ("c5", np.float32),
+                           ("c5-fwd", np.float32), ("c5-mesh", np.float32), ("ct20stif", np.float64),
+                           ("ct20stif-fwd", np.float64), ("ldoor", np.float64), ("ldoor-fwd", np.float64),
                            ("ldoor-csc", np.float32)):
                 if wl == args.workload:
                     continue

@@ -296,7 +296,8 @@ typedef struct vbc_info {
     int32_t planar_mask;    /* bit 0: a B'x planar bucket, bit 1: the forward planar bucket, in masked chunk-local
                                length order (padding lanes fetch nothing); bit 2: a B'x planar bucket in
                                per-lane compacted streams (tiles of stripes dealt to the lanes); bit 3:
-                               the forward planar bucket runs the split product (P waves per chunk);
+                               the forward product sums some chunk's blocks in P slices (a split forward
+                               planar bucket, or -- with bit 8 -- a split bin of C = Bᵀ's layout);
                                bit 4: the forward bucket in lane streams (node blocks transposed);
                                bit 5: a small matrix's B'x buckets of every width (1..8) laid out planar
                                and split, run by ONE fused launch (planar_split = its P); bit 6: some of

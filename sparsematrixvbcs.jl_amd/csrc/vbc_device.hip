@@ -1130,18 +1130,21 @@ static void hole_runs(const vbc_handle *h, const Stripes &s, const std::vector<i
     if (real == 0) return;
     for (int R = 3; R >= 2; R--) {
         int64_t expanded = 0;
-        bool exact = true;
+        bool exact = true, past = false;
         for (int64_t l : stripes) {
             int64_t prev = -1, groups = 0;
             for (int64_t r = s.rbeg[l]; r < s.rbeg[l + 1]; r++) {
                 const int64_t k = s.rows[r] / R;
                 if (k != prev) { groups++; prev = k; }
+                // the kernels gather a run's R x values with one unconditional R-wide load: a run whose
+                // last row lies past the operand (m % R != 0) would read beyond x's allocation
+                past = past || k * R + R > s.m;
             }
             expanded += groups * R;
             exact = exact && groups * R == s.rbeg[l + 1] - s.rbeg[l];
         }
         if (exact) return;  // whole runs already: slot_runs finds them
-        if ((double)(expanded - real) > kHoleFill * (double)real) continue;
+        if (past || (double)(expanded - real) > kHoleFill * (double)real) continue;
         hsbeg.assign(1, 0);
         hents.reserve(expanded);
         for (int64_t l : stripes) {
@@ -1455,9 +1458,23 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
         // fused small split: rows that ALMOST come in aligned runs (a stiffness operator's dof rows, some
         // stripes missing one of a node's rows -- the structural zeros of ct20stif-like matrices) are
         // padded to whole runs, the absent rows marked in the run's key (hole_runs)
+        // Only a bucket of the fused launch takes them: its bins run the split product (build_slots gives a
+        // fused bucket split = small_split), the one kernel family that folds absent rows (voff < 0); a
+        // side bucket, a lane-stream or an unfused slotted / pair layout keeps the plain rows.
         std::vector<Entry> hents;
         std::vector<int64_t> hsbeg;
-        if (h->small_split > 1 && slot_planar(h, 0, w)) hole_runs(h, s, kv.second, w, hents, hsbeg);
+        const bool fused_bucket = h->small_split > 1 && w <= 8 && ((h->fuse_w >> w) & 1) != 0;
+        if (fused_bucket && slot_planar(h, 0, w)) hole_runs(h, s, kv.second, w, hents, hsbeg);
+        if (!hsbeg.empty()) {
+            std::vector<int32_t> out0;
+            for (int64_t l : kv.second) out0.push_back((int32_t)s.col0[l]);
+            std::vector<int64_t> order0;
+            bool mask0 = false;
+            if (want_slots(h, 0, wps, sbeg, total, s.m, order0, &mask0, w) && want_lanes(h, wps, w, sbeg, out0, total, mask0)) {
+                hents.clear();
+                hsbeg.clear();
+            }
+        }
         const std::vector<int64_t> &sb = hsbeg.empty() ? sbeg : hsbeg;
         if (ks > 1) {  // long stripes of the fused split, cut into ks lane parts
             std::vector<Entry> ents;
@@ -1480,7 +1497,8 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
             std::vector<Entry> ents;
             std::vector<int32_t> out;
             for (int64_t l : kv.second) out.push_back((int32_t)s.col0[l]);
-            if (!hsbeg.empty()) {
+            const bool holes = !hsbeg.empty();
+            if (holes) {
                 ents.swap(hents);
                 sbeg.swap(hsbeg);
             } else {
@@ -1490,7 +1508,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
                         ents.push_back({(uint32_t)s.rows[r], s.voff[l] + (r - s.rbeg[l]) * s.vstride(l)});
             }
             PendingSlot ps;
-            if (want_lanes(h, wps, w, sbeg, out, total, mask)) {
+            if (!holes && want_lanes(h, wps, w, sbeg, out, total, mask)) {
                 if (int st = build_lanes(h, w, ents, sbeg, out, slot_runs(h, ents, sbeg), total, val, ar, ps)) return st;
             } else if (int st = build_slots(h, 0, wps, w, ents, sbeg, out, total, val, ar, srange0, ps, order, mask)) {
                 return st;
@@ -2976,6 +2994,9 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
                 if (b.split > 1) info->planar_mask |= 8;
                 if (b.lanes) info->planar_mask |= 16;
             }
+    if (h->has_ft)  // the forward product on C = Bᵀ: its split bins sum P slices too (bit 3, as a split forward)
+        for (const SlotBin &b : h->lft.pbins)
+            if (b.split > 1) info->planar_mask |= 8;
     info->bytes_m = h->has_m ? h->bytes_m : h->bytes_mf;  // a forward-only multi handle: its Bᵀ panel layout
     return VBC_OK;
 }

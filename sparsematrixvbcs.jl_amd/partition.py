@@ -303,7 +303,9 @@ class AlternatingPacker:
         self.methods = tuple(methods)
 
     @property
-    def row_method(self):  # (round-3 attribute names)
+    def row_method(self):  # (round-3 attribute names); None: a one-phase packer has no row phase
+        if len(self.methods) < 2:
+            return None
         return self.methods[-1] if len(self.methods) % 2 == 0 else self.methods[-2]
 
     @property

@@ -731,6 +731,77 @@ def test_fused_split_runs_with_holes_nonfinite(monkeypatch):
     assert np.array_equal(got[fin], ref[fin])
 
 
+def _holey_matrix(rng, N, L, widths, m=None, last_row_every=0):
+    """Stripes of 12 node runs of 3 rows each, every fifth missing one row (a hole); m rows (default 3 N).
+    last_row_every > 0: every such stripe also stores row m - 1 (m % 3 != 0: a run past the operand)."""
+    m = 3 * N if m is None else m
+    rows = []
+    for l in range(L):
+        nodes = np.sort(rng.choice(N, 12, replace=False))
+        r = (nodes[:, None] * 3 + np.arange(3)[None, :]).reshape(-1)
+        if l % 5 == 0:
+            r = np.delete(r, rng.integers(0, len(r)))
+        if last_row_every and l % last_row_every == 0:
+            r = np.append(r, m - 1)
+        rows.append(r)
+    cnt = np.array([len(r) for r in rows])
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)])
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * widths)])
+    spl = np.concatenate([[1], 1 + np.cumsum(widths)])
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + 8)
+    val[:nv] = rng.integers(-8, 9, nv)
+    return V.SparseMatrix1DVBC(8, m, int(spl[-1] - 1), V.SplitPartition(spl), pos, np.concatenate(rows) + 1, ofs, val)
+
+
+@pytest.mark.parametrize("env", [{"VBC_PLANAR_LANES": "1"}, {"VBC_SIDE_FUSE": "1"},
+                                 {"VBC_PLANAR_LANES": "1", "VBC_SIDE_FUSE": "1"}])
+def test_holey_rows_outside_the_fused_split(monkeypatch, env):
+    """runs with holes are built only for the buckets of the fused launch, whose bins run
+    the split product; a side bucket (VBC_SIDE_FUSE=1 leaves the dominant width out of the launch) and a
+    lane-stream layout (VBC_PLANAR_LANES=1) keep the plain rows.  Exact on integer data; create succeeds."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "4")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(47)
+    L = 900
+    # dominant 3-wide bucket (>= 80 % of the stripes) beside 1- and 2-wide side stripes
+    widths = np.where(np.arange(L) % 10 == 0, 1, np.where(np.arange(L) % 10 == 5, 2, 3))
+    B = _holey_matrix(rng, 500, L, widths)
+    R = ref_of(B)
+    x = rng.integers(-8, 9, B.m).astype(np.float64)
+    y = torch.full((B.n,), float("nan"), dtype=torch.float64, device=DEV)
+    V.mul_(y, B.T, dev(x))
+    assert np.array_equal(y.cpu().numpy(), O.mul(R, x, np.zeros(B.n), trans=True))
+    xr = rng.uniform(-1, 1, B.m)
+    V.mul_(y, B.T, dev(xr))
+    assert rel(y.cpu().numpy(), O.mul(R, xr, np.zeros(B.n), trans=True)) <= TOL64
+
+
+def test_holey_runs_never_pass_the_operand(monkeypatch):
+    """a run of R rows is gathered by one R-wide load, so hole_runs rejects an R whose
+    last group would run past m (m % 3 != 0, the last row stored): no load beyond x, exact result."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "4")
+    rng = np.random.default_rng(48)
+    L = 300
+    widths = np.where(np.arange(L) % 2 == 0, 1, 2)
+    for m in (3 * 400 + 1, 3 * 400 + 2):
+        B = _holey_matrix(rng, 400, L, widths, m=m, last_row_every=7)
+        assert B.info(trans=True)["planar_mask"] & 32
+        R = ref_of(B)
+        x = rng.integers(-8, 9, B.m).astype(np.float64)
+        y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
+        V.mul_(y, B.T, dev(x))
+        assert np.array_equal(y.cpu().numpy(), O.mul(R, x, np.zeros(B.n), trans=True)), m
+        xn = x.copy()
+        xn[-1] = np.nan  # the stored last row: NaN reaches exactly the stripes storing it
+        V.mul_(y, B.T, dev(xn))
+        ref = O.mul(R, xn, np.zeros(B.n), trans=True)
+        got = y.cpu().numpy()
+        assert np.array_equal(np.isnan(got), np.isnan(ref))
+        assert np.array_equal(got[~np.isnan(ref)], ref[~np.isnan(ref)])
+
+
 def _node_stripes(rng, N, L, widths, nodes_of, hole_every):
     """Stripes of node runs (rows 3 k .. 3 k + 2 of each chosen node), every hole_every-th missing one row."""
     rows = []
