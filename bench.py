@@ -48,6 +48,8 @@ WORKLOADS = {"ns": "NS-1DVBC-10Mx10M-1e8nnz-w4-uniform",
              "c5-fwd": "C5-VBC2D-8x8-tiles-2Mx2M-1e8nnz-16RHS forward Y = B*X (costs.jl:200-220 generator)",
              "c5-mesh": "C5-VBC2D-3x3-node-tiles-2Mx2M-1e8nnz-16RHS (structured: 3D stiffness stand-in, "
                         "AlternatingPacker(StrictChunker(8), StrictChunker(8)) tiles)",
+             "c5-mesh-fwd": "C5-VBC2D-3x3-node-tiles-2Mx2M-1e8nnz-16RHS forward Y = B*X (structured 3D stiffness "
+                            "stand-in)",
              "fe-fwd": "FE-2D-5pt-dof2-10Mx10M-1e8nnz-w2 (SuiteSparse-like mesh operator), forward y = B*x",
              "fe3d-fwd": "FE-3D-stiffness-dof3-1e7x1e7-1e8nnz-w3 (irregular: random 18-neighbour subsets), forward y = B*x",
              "ldoor": "C3/C4 GHS_psdef/ldoor stand-in 952203^2 42.5M nnz, StrictChunker(8) -> w=3",
@@ -94,7 +96,7 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
         return V.synthetic.fe_stiffness_3d_1dvbc(n, int(round(1e8 * scale)), 3, dtype=dtype, seed=seed)
     if workload in ("c5", "c5-fwd"):
         return V.synthetic.c5(dtype=dtype, scale=scale, seed=seed)
-    if workload == "c5-mesh":
+    if workload in ("c5-mesh", "c5-mesh-fwd"):
         return V.synthetic.c5_mesh(dtype=dtype, scale=scale, seed=seed)
     if workload in ("ldoor", "ct20stif", "ldoor-csc"):
         name = {"ldoor": "GHS_psdef/ldoor", "ct20stif": "Boeing/ct20stif", "ldoor-csc": "GHS_psdef/ldoor"}[workload]
@@ -113,6 +115,9 @@ def build_matrix(workload, dtype, scale=1.0, seed=0xDEADBEEF):
 
 def kernel_name(B, local, k, trans=True):
     if k > 1:
+        if B.info(local, trans, multi=True)["planar_mask"] & 512:
+            return ("vbc::spmm_tiles<T, UB, W, NBT, MASKU, BUF> (tile-granular: one key and one UB-row X block per "
+                    "u x w tile, 4 streams of stripes per wave, csrc/vbc_tiles.h)")
         if B.info(local, trans, multi=True)["planar_mask"] & 128:
             return ("vbc::spmm_quads<T, W, VEC> (VALU stripe quads: 16 stripes x 4 right-hand-side quads per wave, "
                     "csrc/vbc_panel.h)")
@@ -310,7 +315,7 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
     B = build_matrix(workload, dtype, args.scale)
     csc = not hasattr(B, "ofs")
     rng = np.random.default_rng(0xC0FFEE)
-    k = args.nrhs if workload in ("c5", "c5-fwd", "c5-mesh") else 1
+    k = args.nrhs if workload in ("c5", "c5-fwd", "c5-mesh", "c5-mesh-fwd") else 1
     trans = not workload.endswith("-fwd")
     nx, ny = (B.m, B.n) if trans else (B.n, B.m)
     x_host = rng.uniform(-1, 1, (nx, k) if k > 1 else nx).astype(dtype)
@@ -359,9 +364,9 @@ def measure(args, workload, dtype, device, local, with_cpu, with_parity, steps=N
                    ("mul!(y, B', x) -- transposed 1DVBC (multiply_1DVBC.jl:85-180)" if trans else
                     "mul!(y, B, x) -- forward 1DVBC (multiply_1DVBC.jl:9-83)") if k == 1 else
                    f"Y = B'X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:89-192 per column), "
-                   "matrix-core panel kernel" if trans else
+                   "multi-RHS kernel (roofline.kernel)" if trans else
                    f"Y = B*X, {k} row-major right-hand sides -- 2D VBC (multiply_VBC.jl:3-87 per column), "
-                   "matrix-core panel kernel on the panel layout of B' (the matrix read once)"),
+                   "multi-RHS kernel on the layout of B' (the matrix read once; roofline.kernel)"),
             "m": B.m, "n": B.n, "stripes": B.n if csc else len(B.Phi),
             "row_blocks": nnz if csc else int(B.pos[-1] - 1), "nnz": nnz, "W": 1 if csc else B.W,
             "index_bytes": 4, "nrhs": k, "launch": "hipGraph of K products" if graphed else "eager",
@@ -720,7 +725,8 @@ def main():
         if not args.no_secondary:
             sec = {}
             for wl, dt in (("fe-fwd", dtype), ("fe3d", dtype), ("fe3d-fwd", dtype), ("ns", dtype), ("c5", np.float32),
-                           ("c5-fwd", np.float32), ("c5-mesh", np.float32), ("ct20stif", np.float64),
+                           ("c5-fwd", np.float32), ("c5-mesh", np.float32), ("c5-mesh-fwd", np.float32),
+                           ("ct20stif", np.float64),
                            ("ct20stif-fwd", np.float64), ("ldoor", np.float64), ("ldoor-fwd", np.float64),
                            ("ldoor-csc", np.float32)):
                 if wl == args.workload:

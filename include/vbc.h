@@ -304,7 +304,9 @@ typedef struct vbc_info {
                                those stripes cut into 2 / 4 lane parts (long stripes); bit 7: the multi-RHS
                                layout has VALU stripe-quad buckets (widths <= 8, spmm_quads); bit 8: the
                                forward product runs on the transposed layout of C = Bᵀ (stripes of several
-                               widths: one fused launch instead of one per width) */
+                               widths: one fused launch instead of one per width); bit 9: the multi-RHS
+                               layout has tile-granular buckets (u, w <= 4 tiles: one key and one u-row X
+                               block per tile, spmm_tiles) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

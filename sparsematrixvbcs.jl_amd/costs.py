@@ -15,7 +15,7 @@ locality: "uniform" draws rows over all of x, exactly the reference's generator 
 the GPU those matrices run the row-swept kernel, whose cost is the x gathers (one per stored row,
 whatever the width), so the fitted model prices rows, not values, and its partitions trade fill for
 fewer rows ('min blocks'-like: the ct20stif stand-in 25.7 us against 5.4 us for 'strict',
-profiles/r03_table_ct20stif.log).  It is the default, so the model is the reference's protocol
+profiles/archive/r03_table_ct20stif.log).  It is the default, so the model is the reference's protocol
 unchanged.  "banded" (opt-in) draws each stripe's rows from a window around its own position -- the
 x locality of the mesh operators the table is run on -- so the fit sees the streaming kernels the
 partition will actually run (tools/test_table.py passes both).
@@ -120,7 +120,7 @@ class TimedChunker:
     partition is set by the layouts its width buckets get (a planar bucket streams at ~0.8 of HBM
     peak, a bucket with chunks too long to balance falls back to the merge kernel at ~1/3 of that) and
     by how many launches they need -- neither is a per-stripe term.  On the ct20stif stand-in the
-    fitted model's partition runs 28-36 us against 5.5 us for StrictChunker (profiles/r03_table_*).
+    fitted model's partition runs 28-36 us against 5.5 us for StrictChunker (profiles/archive/r03_table_*).
     Measuring the candidates is the GPU counterpart of the reference's autotuned 'min time' row.
     `timings` keeps (candidate index, us) of the last call."""
 

@@ -1931,6 +1931,8 @@ struct PendingPanel {
     PanelBin b;
     QuadBin qb;  // quad: a stripe-quad bucket (o_rgrp = its chunk rows)
     bool quad;
+    TileBin tb;  // tile: a small-tile bucket (vbc_tiles.h; o_rgrp = its range table)
+    bool tile = false;
     size_t o_key, o_val, o_out, o_rgrp, o_rseg;
 };
 
@@ -2006,11 +2008,343 @@ static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<std::
                 (long long)n, (long long)nch, (long long)rows, order.empty() ? "natural" : "sorted", (long long)sbeg[n]);
 }
 
+// Tile layout (vbc_tiles.h) of one width bucket (w <= 4, whole stripes) of the multi-RHS product: each
+// stripe's stored rows grouped into tiles of consecutive rows of one row group -- Π's block rows (tgrp:
+// their 0-based starts + m; a SparseMatrixVBC's u x w blocks, constructors_VBC.jl:95-105) or, for a 1DVBC,
+// aligned runs of R rows (R in {4, 3, 2}: the node runs of a stiffness operator; the R adding the fewest
+// tiles within kTilePad of padding).  A tile slot holds ub rows x w values (rows the tile does not store:
+// zeros, masked in its key).  Stripes in natural order are cut into ranges (one wave each) of at most
+// smax stripes (the LDS output stage) balanced by tiles, a whole number of rounds of resident waves; each
+// range into 4 streams of consecutive stripes balanced by tiles (the wave's 16-lane rows), every stream
+// padded to the longest with invalid tiles.  Returns false (nothing built) when the bucket does not fit:
+// a tile taller than 4 rows, too much padding, too few rows per tile (auto), rows >= 2^26.
+constexpr double kTilePad = 1.25;
+static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64_t> &stripes_in, int w,
+                        const std::vector<int64_t> *tgrp, const char *val, Arena &ar, PendingPanel &pp)
+{
+    std::vector<int64_t> stripes = stripes_in;  // (processing order: natural, or blob order below)
+    if (h->panel_tiles == 0 || w < 1 || w > 4 || stripes.empty() || s.m >= (int64_t)kTileRow) return false;
+    for (int64_t l : stripes)
+        if (s.w[l] != w || s.vstride(l) != w) return false;
+    const int esz = h->esz;
+    int64_t rows = 0;
+    for (int64_t l : stripes) rows += s.rbeg[l + 1] - s.rbeg[l];
+    // group of a row: base row and height
+    std::vector<int32_t> gk;  // tgrp: row -> block row
+    if (tgrp) {
+        gk.assign((size_t)s.m, 0);
+        for (size_t k = 0; k + 1 < tgrp->size(); k++)
+            for (int64_t i = (*tgrp)[k]; i < (*tgrp)[k + 1] && i < s.m; i++) gk[i] = (int32_t)k;
+    }
+    // tiles of a stripe under grouping R (R = 0: tgrp): consecutive stored rows of one group, a repeated
+    // slot row (a hand-built stripe storing a row twice) starting a new tile
+    auto group_of = [&](int64_t row, int R, int64_t &base, int &u) {
+        if (R == 0) {
+            const int32_t k = gk[row];
+            base = (*tgrp)[k];
+            u = (int)((*tgrp)[k + 1] - base);
+        } else {
+            base = row / R * R;
+            u = R;
+        }
+    };
+    auto count = [&](int R, int64_t &tiles, int &ub) {
+        tiles = 0;
+        ub = 1;
+        for (int64_t l : stripes) {
+            int64_t cb = -1;
+            unsigned seen = 0;
+            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+                int64_t base;
+                int u;
+                group_of(s.rows[q], R, base, u);
+                if (u > 4) return false;
+                const unsigned bit = 1u << (s.rows[q] - base);
+                if (base != cb || (seen & bit)) {
+                    tiles++;
+                    cb = base;
+                    seen = 0;
+                }
+                seen |= bit;
+                ub = std::max(ub, u);
+            }
+        }
+        return true;
+    };
+    int R = 0, ub = 1;
+    int64_t tiles = 0;
+    if (tgrp) {
+        if (!count(0, tiles, ub)) return false;
+        if ((double)tiles * ub > kTilePad * (double)std::max<int64_t>(rows, 1) && h->panel_tiles < 0) return false;
+    } else {
+        int64_t best = -1;
+        for (int Rc = 4; Rc >= 1; Rc--) {
+            int64_t t;
+            int u;
+            count(Rc, t, u);
+            if (Rc > 1 && (double)t * Rc > kTilePad * (double)std::max<int64_t>(rows, 1)) continue;
+            if (best < 0 || t < best) {
+                best = t;
+                R = Rc;
+                ub = Rc;
+                tiles = t;
+            }
+        }
+    }
+    // auto: only when tiles carry work (>= 1.5 rows each); VBC_PANEL_TILES=1 takes any
+    if (h->panel_tiles < 0 && (double)rows < 1.5 * (double)std::max<int64_t>(tiles, 1)) return false;
+    const int TV = ub * w;
+    const int64_t n = (int64_t)stripes.size();
+    // Blob order (VBC_TILE_ORDER=1): the stripes are processed in compact blobs of the stripe graph
+    // (two stripes adjacent when they store tiles of one row group, i.e. gather the same X rows): each
+    // blob a BFS ball of tile_blob stripes from a seed on the previous blob's frontier.  A 3D mesh's
+    // natural order reuses an X row across +-g^2 stripes (three planes), beyond what an XCD's L2 holds
+    // while the front of concurrent stripes sweeps on; compact blobs keep a stripe's X rows within a
+    // few consecutive blobs.  Outputs are unaffected (each stripe writes its own columns).
+    if (h->tile_order == 1 && n > h->tile_blob) {
+        std::vector<int64_t> sgb(n + 1, 0), sg;  // per stripe: its groups (base rows)
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t l = stripes[i];
+            int64_t cb = -1;
+            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+                int64_t base;
+                int u;
+                group_of(s.rows[q], R, base, u);
+                if (base != cb) sg.push_back(base);
+                cb = base;
+            }
+            sgb[i + 1] = (int64_t)sg.size();
+        }
+        std::vector<int64_t> gsb(s.m + 1, 0), gs(sg.size());  // per group (base row): its stripes
+        for (int64_t g : sg) gsb[g + 1]++;
+        for (int64_t r = 0; r < s.m; r++) gsb[r + 1] += gsb[r];
+        {
+            std::vector<int64_t> at(gsb.begin(), gsb.end() - 1);
+            for (int64_t i = 0; i < n; i++)
+                for (int64_t e = sgb[i]; e < sgb[i + 1]; e++) gs[at[sg[e]]++] = i;
+        }
+        std::vector<char> taken(n, 0);
+        std::vector<int64_t> mark_s(n, -1), mark_g(s.m, -1), order, queue;
+        order.reserve(n);
+        int64_t scan = 0, seed = -1, blob = 0;
+        const int64_t C = h->tile_blob;
+        while ((int64_t)order.size() < n) {
+            if (seed < 0 || taken[seed]) {
+                while (taken[scan]) scan++;
+                seed = scan;
+            }
+            queue.assign(1, seed);
+            mark_s[seed] = blob;
+            int64_t cnt = 0, next = -1;
+            for (size_t hd = 0; hd < queue.size(); hd++) {
+                const int64_t st = queue[hd];
+                if (cnt == C) {  // the ball is full: the first frontier stripe seeds the next blob
+                    next = st;
+                    break;
+                }
+                order.push_back(st);
+                taken[st] = 1;
+                cnt++;
+                for (int64_t e = sgb[st]; e < sgb[st + 1]; e++) {
+                    const int64_t g = sg[e];
+                    if (mark_g[g] == blob) continue;
+                    mark_g[g] = blob;
+                    for (int64_t f = gsb[g]; f < gsb[g + 1]; f++) {
+                        const int64_t t = gs[f];
+                        if (!taken[t] && mark_s[t] != blob) {
+                            mark_s[t] = blob;
+                            queue.push_back(t);
+                        }
+                    }
+                }
+            }
+            seed = next;
+            blob++;
+        }
+        std::vector<int64_t> re(n);
+        for (int64_t i = 0; i < n; i++) re[i] = stripes[order[i]];
+        stripes.swap(re);
+        if (getenv("VBC_VERBOSE"))
+            fprintf(stderr, "[vbc] tiles: blob order, %lld blobs of <= %lld stripes\n", (long long)blob, (long long)C);
+    }
+    std::vector<int64_t> tl(n);  // tiles per stripe (an empty stripe: one invalid LAST tile)
+    {
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t l = stripes[i];
+            int64_t t = 0, cb = -1;
+            unsigned seen = 0;
+            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+                int64_t base;
+                int u;
+                group_of(s.rows[q], R, base, u);
+                const unsigned bit = 1u << (s.rows[q] - base);
+                if (base != cb || (seen & bit)) {
+                    t++;
+                    cb = base;
+                    seen = 0;
+                }
+                seen |= bit;
+            }
+            tl[i] = std::max<int64_t>(t, 1);
+        }
+    }
+    // ranges: <= smax stripes (the LDS stage), a whole number of rounds of resident waves, balanced by tiles
+    // (the 16-B fp32 form stages every slot row's partial sums: ub x the outputs of a stripe)
+#ifdef VBC_TILE_REDUCE_DPP
+    const int stage_rows = 1;
+#else
+    const int stage_rows = esz == 4 && h->tile_x4 ? ub : 1;
+#endif
+    const int64_t smax = std::max<int64_t>(1, kTileStageBytes / (w * 16 * esz * stage_rows));
+    const int64_t slots = (int64_t)h->cus * std::max(1, h->occ_tiles);
+    int64_t total = 0;
+    for (int64_t t : tl) total += t;
+    const int nbt = h->tile_nbt;  // the kernel's batch (streams padded to whole pairs of batches)
+    // Ranges of ~tile_spr stripes: the hardware dispatches workgroups in order and each XCD takes a
+    // contiguous run of ranges (xcd_block), so the stripes in flight on an XCD span its resident waves x
+    // the range length -- and a 3D mesh's X rows are reused across +-g^2 nodes, so that front must stay
+    // narrow for the X tiles to hit in the XCD's 4 MB L2 (c5-mesh: 28 stripes per range, L2 hit rate 57 %).
+    int64_t nr = std::max<int64_t>((n + smax - 1) / smax, 1);
+    nr = std::max<int64_t>(nr, (n + h->tile_spr - 1) / std::max(1, h->tile_spr));
+    // few ranges: a whole number of rounds of resident waves, but no range so short that its streams'
+    // padding to whole key pairs dominates (>= 4 batch pairs per stream on average)
+    if (nr < 2 * slots) {
+        const int64_t nr_cap = std::max<int64_t>(nr, total / (4 * 8 * nbt));
+        nr = std::min<int64_t>(nr_cap, (nr + slots - 1) / slots * slots);
+    }
+    nr = std::min<int64_t>(n, nr);
+    if (const char *e = getenv("VBC_TILE_RANGES")) nr = std::min<int64_t>(n, std::max<int64_t>(1, atoll(e)));
+    std::vector<int64_t> rb{0};  // range starts (stripe index)
+    {
+        int64_t cum = 0;
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t cnt = i - rb.back();
+            if (cnt > 0 && (cnt >= smax || (cum * nr >= (int64_t)rb.size() * total && (int64_t)rb.size() < nr))) rb.push_back(i);
+            cum += tl[i];
+        }
+        rb.push_back(n);
+    }
+    const int64_t nrg = (int64_t)rb.size() - 1;
+    // streams of each range: 4 runs of consecutive stripes balanced by tiles
+    std::vector<int32_t> rinfo((size_t)nrg * 8, 0);
+    std::vector<std::array<int64_t, 5>> sb(nrg);
+    int64_t slot_total = 0;
+    for (int64_t r = 0; r < nrg; r++) {
+        const int64_t a = rb[r], e = rb[r + 1];
+        int64_t rt = 0;
+        for (int64_t i = a; i < e; i++) rt += tl[i];
+        auto &b = sb[r];
+        b[0] = a;
+        int64_t cum = 0, i = a;
+        for (int k = 1; k < 4; k++) {
+            // first stripe of stream k: where the cumulative tiles pass k / 4 of the range's (closer side)
+            while (i < e && (cum + tl[i]) * 4 <= k * rt) cum += tl[i++];
+            if (i < e && (cum + tl[i]) * 4 - k * rt < k * rt - cum * 4) cum += tl[i++];
+            b[k] = i;
+        }
+        b[4] = e;
+        int64_t len = 0;
+        for (int k = 0; k < 4; k++) {
+            int64_t t = 0;
+            for (int64_t q = b[k]; q < b[k + 1]; q++) t += tl[q];
+            len = std::max(len, t);
+        }
+        len = (len + 2 * nbt - 1) / (2 * nbt) * (2 * nbt);  // whole key pairs (vbc_tiles.h)
+        int32_t *ri = &rinfo[(size_t)r * 8];
+        ri[0] = (int32_t)slot_total;
+        ri[1] = (int32_t)len;
+        ri[2] = (int32_t)a;
+        ri[3] = (int32_t)(e - a);
+        for (int k = 1; k < 4; k++) ri[3 + k] = (int32_t)(b[k] - a);
+        slot_total += 4 * len;
+        if (slot_total >= (int64_t(1) << 31) / std::max(1, TV)) return false;
+    }
+    const int64_t kpad = 3 * nbt + 16, vpad = (int64_t)(2 * nbt + 2) * TV + 64;
+    pp = PendingPanel{};
+    pp.tile = true;
+    TileBin &tb = pp.tb;
+    tb.w = w;
+    tb.ub = ub;
+    tb.nbt = nbt;
+    if (const char *e = getenv("VBC_TILE_DIAG")) tb.diag = atoi(e);
+    {
+        int64_t most = 1;
+        for (size_t r = 0; r + 1 < rb.size(); r++) most = std::max<int64_t>(most, rb[r + 1] - rb[r]);
+        // (the 16-B fp32 form stages every slot row's partial sums: ub x the outputs)
+        tb.stage_bytes = (int32_t)((most * w * 16 * esz * (stage_rows > 1 ? ub : 1) + 15) / 16 * 16);
+    }
+    tb.nranges = (int32_t)nrg;
+    std::vector<int32_t> out(n);
+    for (int64_t i = 0; i < n; i++) out[i] = (int32_t)s.col0[stripes[i]];
+    tb.out_affine = 1;
+    tb.out_base = out[0];
+    tb.out_stride = n > 1 ? out[1] - out[0] : w;
+    for (int64_t i = 1; i < n && tb.out_affine; i++) tb.out_affine = (int64_t)out[i] == (int64_t)out[0] + i * tb.out_stride;
+    pp.o_key = ar.reserve((slot_total + kpad) * 4);
+    pp.o_val = ar.reserve((slot_total * TV + vpad) * esz);
+    pp.o_out = ar.reserve(n * 4);
+    pp.o_rgrp = ar.reserve(rinfo.size() * 4);
+    std::memcpy(ar.at<int32_t>(pp.o_out), out.data(), out.size() * 4);
+    std::memcpy(ar.at<int32_t>(pp.o_rgrp), rinfo.data(), rinfo.size() * 4);
+    uint32_t *key = ar.at<uint32_t>(pp.o_key);
+    char *vv = ar.at<char>(pp.o_val);
+    std::fill(key, key + slot_total + kpad, kTileRow);  // padding: invalid tiles (row field all ones)
+    std::memset(vv, 0, (size_t)(slot_total * TV + vpad) * esz);
+    bool masku = false;
+    for (int64_t r = 0; r < nrg; r++) {
+        const int32_t *ri = &rinfo[(size_t)r * 8];
+        const int64_t len = ri[1];
+        for (int k = 0; k < 4; k++) {
+            int64_t slot = ri[0] + k * len;  // this stream's next tile slot
+            for (int64_t i = sb[r][k]; i < sb[r][k + 1]; i++) {
+                const int64_t l = stripes[i];
+                if (s.rbeg[l + 1] == s.rbeg[l]) {  // empty stripe: one invalid LAST tile (its columns get beta * Y)
+                    key[slot++] = kTileLast | kTileRow;
+                    continue;
+                }
+                int64_t cb = -1, kbase = 0;
+                unsigned seen = 0;
+                for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+                    int64_t base;
+                    int u;
+                    group_of(s.rows[q], R, base, u);
+                    const int rr = (int)(s.rows[q] - base);
+                    const unsigned bit = 1u << rr;
+                    if (base != cb || (seen & bit)) {
+                        if (cb >= 0) {
+                            key[slot] = (uint32_t)kbase | kTileValid | (seen << kTileMaskShift);
+                            masku = masku || seen != (1u << ub) - 1;
+                            slot++;
+                        }
+                        cb = base;
+                        kbase = base;
+                        seen = 0;
+                    }
+                    seen |= bit;
+                    std::memcpy(vv + (slot * TV + (int64_t)rr * w) * esz, val + (s.voff[l] + (q - s.rbeg[l]) * w) * esz,
+                                (size_t)w * esz);
+                }
+                key[slot] = (uint32_t)kbase | kTileValid | (seen << kTileMaskShift) | kTileLast;
+                masku = masku || seen != (1u << ub) - 1;
+                slot++;
+            }
+        }
+    }
+    tb.masku = masku ? 1 : 0;
+    h->bytes_m += slot_total * (4 + (int64_t)TV * esz) + nrg * 32;
+    if (getenv("VBC_VERBOSE"))
+        fprintf(stderr, "[vbc] tiles: w %d, %lld stripes, %lld rows -> %lld tiles of <= %d rows (%s), %lld ranges, %lld slots%s\n",
+                w, (long long)n, (long long)rows, (long long)total, ub, R == 0 ? "block rows" : "row runs", (long long)nrg,
+                (long long)slot_total, masku ? ", masked rows" : "");
+    return true;
+}
+
 // Panel layout (vbc_panel.h) of the transposed product: per width bucket (stripes wider than 16 are
 // cut into 16-column pieces that share the stripe's rows), S = 16/w consecutive stripes per panel,
 // each panel's rows padded to a multiple of 4, ranges of whole panels balanced by rows.
 static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &ar,
-                       std::vector<PendingPanel> &pps, PanelLaunch &L, std::vector<int32_t> &fill)
+                       std::vector<PendingPanel> &pps, PanelLaunch &L, std::vector<int32_t> &fill,
+                       const std::vector<int64_t> *tgrp = nullptr)
 {
     struct Piece {
         int64_t l;
@@ -2022,6 +2356,23 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     (void)fill;
     for (int64_t l = 0; l < s.L; l++)
         for (int c0 = 0; c0 < s.w[l]; c0 += 16) buckets[std::min(16, s.w[l] - c0)].push_back({l, c0});
+    // small tiles (u, w <= 4): the tile-granular layout (vbc_tiles.h) instead of panels
+    if (!tgrp && !s.grp.empty()) tgrp = &s.grp;
+    for (auto it = buckets.begin(); it != buckets.end();) {
+        bool whole = it->first <= 4;
+        std::vector<int64_t> st;
+        for (const Piece &pc : it->second) {
+            whole = whole && pc.c0 == 0;
+            st.push_back(pc.l);
+        }
+        PendingPanel pp;
+        if (whole && build_tiles(h, s, st, it->first, tgrp, val, ar, pp)) {
+            pps.push_back(pp);
+            it = buckets.erase(it);
+        } else {
+            ++it;
+        }
+    }
     const int esz = h->esz;
     // groups of every bucket first: ranges are spread over the launch in proportion to them
     std::map<int, std::vector<int64_t>> pgroups;  // w -> groups per panel
@@ -2252,7 +2603,11 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
     h->mf_group = widest;
     const int64_t bytes0 = h->bytes_m;
     std::vector<int32_t> fill;
-    const int st = build_panel(h, c, cv.data(), ar, pps, L, fill);
+    // tile groups of C's rows (B's columns): B's stripes (Φ), so a u x w block of B is a w x u tile of C
+    std::vector<int64_t> cg;
+    for (int64_t l = 0; l < s.L; l++) cg.push_back(s.col0[l]);
+    cg.push_back(s.n);
+    const int st = build_panel(h, c, cv.data(), ar, pps, L, fill, &cg);
     h->bytes_mf = h->bytes_m - bytes0;
     h->bytes_m = bytes0;
     return st;
@@ -2262,8 +2617,18 @@ static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, P
 {
     L.bins.clear();
     L.qbins.clear();
+    L.tbins.clear();
     char *base = static_cast<char *>(h->d_arena);
     for (const PendingPanel &pp : pps) {
+        if (pp.tile) {
+            TileBin t = pp.tb;
+            t.key = reinterpret_cast<const uint32_t *>(base + pp.o_key);
+            t.val = base + pp.o_val;
+            t.out = reinterpret_cast<const int32_t *>(base + pp.o_out);
+            t.rinfo = reinterpret_cast<const int32_t *>(base + pp.o_rgrp);
+            L.tbins.push_back(t);
+            continue;
+        }
         if (pp.quad) {
             QuadBin q = pp.qb;
             q.key = reinterpret_cast<const uint32_t *>(base + pp.o_key);
@@ -2616,6 +2981,13 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = getenv("VBC_PANEL_DIAG")) h->panel_valu |= atoi(e) & ~1;
         if (const char *e = getenv("VBC_PANEL_NOBUF")) h->panel_nobuf = atoi(e) != 0;
         if (const char *e = getenv("VBC_PANEL_QUADS")) h->panel_quads = atoi(e);
+        if (const char *e = getenv("VBC_PANEL_TILES")) h->panel_tiles = atoi(e) < 0 ? -1 : atoi(e) != 0;
+        if (const char *e = getenv("VBC_TILE_NBT")) h->tile_nbt = atoi(e) >= 8 ? 8 : 4;
+        if (const char *e = getenv("VBC_TILE_SPR")) h->tile_spr = std::max(1, atoi(e));
+        if (const char *e = getenv("VBC_TILE_X4")) h->tile_x4 = atoi(e) != 0;
+        if (const char *e = getenv("VBC_TILE_ORDER")) h->tile_order = atoi(e);
+        if (const char *e = getenv("VBC_TILE_BLOB")) h->tile_blob = std::max(1, atoi(e));
+        h->occ_tiles = occupancy_tiles(h->esz);
     }
 
     Arena ar;
@@ -2958,8 +3330,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->device_bytes = (int64_t)h->arena_bytes;
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
-    info->bins_m = h->has_m ? (int32_t)(h->lm.bins.size() + h->lm.qbins.size())
-                 : h->has_mf ? (int32_t)(h->lmf.bins.size() + h->lmf.qbins.size()) : 0;
+    info->bins_m = h->has_m ? (int32_t)(h->lm.bins.size() + h->lm.qbins.size() + h->lm.tbins.size())
+                 : h->has_mf ? (int32_t)(h->lmf.bins.size() + h->lmf.qbins.size() + h->lmf.tbins.size()) : 0;
+    if ((h->has_m && !h->lm.tbins.empty()) || (h->has_mf && !h->lmf.tbins.empty()))
+        info->planar_mask |= 512;  // multi-RHS buckets in the tile-granular layout (spmm_tiles)
     if ((h->has_m && !h->lm.qbins.empty()) || (h->has_mf && !h->lmf.qbins.empty()))
         info->planar_mask |= 128;  // multi-RHS buckets in the VALU stripe-quad layout (spmm_quads)
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too

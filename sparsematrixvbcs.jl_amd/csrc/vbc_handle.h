@@ -10,6 +10,7 @@
 #include "vbc_internal.h"
 #include "vbc_kernels.h"
 #include "vbc_panel.h"
+#include "vbc_tiles.h"
 
 namespace vbc {
 
@@ -60,6 +61,7 @@ struct PanelLaunch {
     std::vector<PanelBin> bins;
     PanelBin *d_bins = nullptr;
     std::vector<QuadBin> qbins;  // stripe-quad buckets (VALU, w <= 8): one launch each
+    std::vector<TileBin> tbins;  // small-tile buckets (vbc_tiles.h, u, w <= 4): one launch each
     int total_ranges = 0;
     int nfill = 0;
     size_t o_fill = 0;
@@ -110,6 +112,16 @@ struct vbc_handle {
     int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
     int panel_quads = 0;          // VBC_PANEL_QUADS: widest stripe of the VALU stripe-quad layout (0: MFMA panels only)
+    int panel_tiles = -1;         // VBC_PANEL_TILES: small-tile buckets tile-granular (vbc_tiles.h): -1 auto, 0 never,
+                                  // 1 whenever representable (any fill)
+    int occ_tiles = 24;           // resident waves per CU of the tile kernel (the layout's range count)
+    int tile_nbt = vbc::kTileBatch;  // VBC_TILE_NBT: tiles per stream per pipeline stage of the tile kernel (4 / 8)
+    int tile_spr = vbc::kTileStripes;  // VBC_TILE_SPR: stripes per range (wave) of the tile layout
+    int tile_x4 = 0;              // VBC_TILE_X4=1: the 16-B fp32 form of the tile kernel (spmm_tiles4; c5-mesh 308-333 us
+                                  // against 298-305 us for the dword form, profiles/r05_tiles_ab.log)
+    int tile_order = 0;           // VBC_TILE_ORDER: 0 natural stripe order, 1 blob order (vbc_device.hip build_tiles;
+                                  // c5-mesh 305 -> 310 us dword, 334 -> 370 us 16-B form: not kept)
+    int tile_blob = 512;          // VBC_TILE_BLOB: stripes per blob of the blob order
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch
@@ -228,5 +240,9 @@ int convert_scatter(const void *src, int src_dtype, void *dst, int dst_dtype, in
 int mulmat_panel_any(const vbc_handle *h, int trans, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
                      int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s);
 int occupancy_panel(int esz);
+// vbc_tiles.hip
+int mulmat_tiles_any(const vbc_handle *h, int trans, int64_t nrhs, const char *X, int64_t sxr, int64_t sxc, char *Y,
+                     int64_t syr, int64_t syc, double alpha, double beta, hipStream_t s);
+int occupancy_tiles(int esz);
 
 }  // namespace vbc

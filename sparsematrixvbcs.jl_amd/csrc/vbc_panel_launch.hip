@@ -18,6 +18,8 @@ static int mulmat_panel(const vbc_handle *h, int trans, int64_t nrhs, const char
     const PanelLaunch &L = trans ? h->lm : h->lmf;
     const int64_t xrows = trans ? h->m : h->n, yrows = trans ? h->n : h->m;
     const bool rd = beta != 0.0;
+    // small-tile buckets (vbc_tiles.h): their own launches, disjoint columns of Y
+    if (int st = mulmat_tiles_any(h, trans, nrhs, X, sxr, sxc, Y, syr, syc, alpha, beta, s)) return st;
     // stripe-quad buckets (VALU, vbc_panel.h spmm_quads): 16 right-hand sides per launch, one launch per bucket
     for (int64_t c0 = 0; c0 < nrhs && !L.qbins.empty(); c0 += 16) {
         const int nr = (int)std::min<int64_t>(16, nrhs - c0);

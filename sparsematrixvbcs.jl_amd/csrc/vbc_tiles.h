@@ -1,0 +1,551 @@
+// gfx950 multi-RHS transposed product for SMALL dense tiles, one tile at a time (device code).
+//
+// Y = alpha * B' X + beta * Y for up to 16 right-hand sides per launch, for stripes of width w <= 4 whose
+// stored rows come in tiles of u <= 4 consecutive x rows: the u x w blocks of a SparseMatrixVBC
+// (constructors_VBC.jl:95-105, a 3D stiffness operator's 3 x 3 node tiles) or a 1DVBC's node runs.
+// The reference's per-stripe loop (multiply_VBC.jl:93-147, `_VBR_mul!`) walks a stripe's blocks in stored
+// order and, per block row Δi, adds val[q + wΔi : ...] * x[i + Δi] into the w-wide accumulator (:131); per
+// right-hand side that is the same fma chain over (block, Δi), which this kernel keeps -- so every column
+// equals the reference's column product bit for bit.
+//
+// The unit of work is the TILE, not the stored row (the MFMA panel of vbc_panel.h pays a key, a value
+// row and a 64-B X gather per stored row and puts 3 of its 16 M rows to use on 3 x 3 tiles):
+//   * a wave is 4 rows of 16 lanes; 16-lane row g walks its own *stream* -- a run of consecutive stripes
+//     of the range -- one tile per step; lane j of the row owns right-hand side j, so the tile's u x 16
+//     block of X (u contiguous 64-B rows of a row-major X with 16 RHS) is u coalesced dword loads;
+//   * per tile ONE 32-bit key: the first x row of the tile slot, the present-row mask (bits 26..29: a
+//     1DVBC run with a hole, or u < the slot height), VALID and LAST (the stripe's last tile);
+//   * a stream's tiles and values are contiguous (stream-major inside the range), so a row loads NBT
+//     tiles' values with ceil(NBT * u * w / 64) 16-B loads per lane and each lane takes the value it
+//     needs from lane f of its row with a DPP row_newbcast (v_mov_b32_dpp row_newbcast:f);
+//   * a LAST tile closes the row's stripe: its w x 16 sums go to the wave's LDS stage at the stripe's slot
+//     (LDS only -- no store interrupts the vector-memory pipeline) and the range's outputs are written as
+//     one contiguous run after the loop.
+// Software pipeline: the keys run two batches ahead, the values and X gathers one batch ahead of the fold.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "vbc_kernels.h"
+#include "vbc_panel.h"
+
+namespace vbc {
+
+constexpr uint32_t kTileLast = 0x80000000u;
+constexpr uint32_t kTileValid = 0x40000000u;
+constexpr int kTileMaskShift = 26;           // bits 26..29: rows of the slot the tile stores
+constexpr uint32_t kTileRow = 0x00FFFFFFu;   // first x row of the tile slot (< 2^24 - 1); all ones: no tile
+                                             // (an invalid key's row times the row stride lies past X)
+constexpr int kTileStageBytes = 8192;        // largest LDS output stage per wave (the range's w x 16 sums per stripe)
+constexpr int kTileStripes = 32;             // default stripes per range (c5-mesh 8 / 16 / 32: 338 / 327 / 298 us)
+constexpr int kTileBatch = 8;                // default tiles per stream per pipeline stage (4 or 8: one key load per two)
+
+// One width bucket of the tile layout (one launch per 16 right-hand sides).
+struct TileBin {
+    int32_t w;            // stripe width (1..4)
+    int32_t ub;           // rows per tile slot (1..4)
+    int32_t nranges;      // ranges = waves
+    int32_t masku;        // some tile stores fewer rows than its slot (the kernel masks those x rows)
+    int32_t out_affine;   // out[s] == out_base + s * out_stride
+    int32_t out_base;
+    int32_t out_stride;
+    int32_t nbt;          // tiles per stream per pipeline stage (the kernel's NBT; streams padded to 2 NBT)
+    int32_t stage_bytes;  // LDS output stage per wave: the most stripes of a range x w x 16 sums (dynamic LDS)
+    int32_t diag;         // VBC_TILE_DIAG ablations (tools/ab.py only): 1 X tiles from 256 rows (cache-resident),
+                          // 2 values from the range's first batch (cache-resident)
+    const uint32_t *key;  // per range: 4 streams x len keys, stream-major (+ over-read padding)
+    const void *val;      // per range: 4 streams x len x (ub * w) values (+ padding)
+    const int32_t *rinfo; // per range: {first tile slot, len, first stripe, stripes, stream 1..3 first stripe, 0}
+    const int32_t *out;   // per stripe: first y column
+};
+
+// v from lane N of each 16-lane row (DPP row_newbcast, gfx90a+)
+template <int N>
+__device__ __forceinline__ int row_bcast_i(int v)
+{
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + N, 0xF, 0xF, true);
+}
+__device__ __forceinline__ int row_bcast_rt(int v, int n)
+{
+    switch (n & 15) {
+    case 0: return row_bcast_i<0>(v);
+    case 1: return row_bcast_i<1>(v);
+    case 2: return row_bcast_i<2>(v);
+    case 3: return row_bcast_i<3>(v);
+    case 4: return row_bcast_i<4>(v);
+    case 5: return row_bcast_i<5>(v);
+    case 6: return row_bcast_i<6>(v);
+    case 7: return row_bcast_i<7>(v);
+    case 8: return row_bcast_i<8>(v);
+    case 9: return row_bcast_i<9>(v);
+    case 10: return row_bcast_i<10>(v);
+    case 11: return row_bcast_i<11>(v);
+    case 12: return row_bcast_i<12>(v);
+    case 13: return row_bcast_i<13>(v);
+    case 14: return row_bcast_i<14>(v);
+    default: return row_bcast_i<15>(v);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T row_bcast(T v, int n)
+{
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, row_bcast_rt(__builtin_bit_cast(int, v), n));
+    } else {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = (uint32_t)row_bcast_rt((int)(uint32_t)u, n);
+        const uint32_t hi = (uint32_t)row_bcast_rt((int)(uint32_t)(u >> 32), n);
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+    }
+}
+
+// acc += (v from lane N of the row) * x in ONE instruction: v_fmac_f32 with a DPP row_newbcast source (the
+// compiler keeps a separate v_mov_b32_dpp).  v is always a register a vector-memory load wrote (the tile's
+// values), never a VALU result, so the DPP read-after-VALU-write hazard cannot arise; the checker in
+// tools/isa_check.py verifies that in the built ISA.
+template <int N>
+__device__ __forceinline__ void fmac_bcast(float &acc, float v, float x)
+{
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(v), "v"(x), "n"(N));
+}
+template <typename T>
+__device__ __forceinline__ void fmac_bcast_rt(T &acc, T v, T x, int n)
+{
+    if constexpr (sizeof(T) == 4) {
+        switch (n & 15) {
+        case 0: fmac_bcast<0>(acc, v, x); break;
+        case 1: fmac_bcast<1>(acc, v, x); break;
+        case 2: fmac_bcast<2>(acc, v, x); break;
+        case 3: fmac_bcast<3>(acc, v, x); break;
+        case 4: fmac_bcast<4>(acc, v, x); break;
+        case 5: fmac_bcast<5>(acc, v, x); break;
+        case 6: fmac_bcast<6>(acc, v, x); break;
+        case 7: fmac_bcast<7>(acc, v, x); break;
+        case 8: fmac_bcast<8>(acc, v, x); break;
+        case 9: fmac_bcast<9>(acc, v, x); break;
+        case 10: fmac_bcast<10>(acc, v, x); break;
+        case 11: fmac_bcast<11>(acc, v, x); break;
+        case 12: fmac_bcast<12>(acc, v, x); break;
+        case 13: fmac_bcast<13>(acc, v, x); break;
+        case 14: fmac_bcast<14>(acc, v, x); break;
+        default: fmac_bcast<15>(acc, v, x); break;
+        }
+    } else {
+        acc = fmadd(row_bcast(v, n), x, acc);
+    }
+}
+
+// BUF: X addressed by 32-bit buffer offsets (X below 2 GiB; an invalid key reads past the buffer: 0);
+// else 64-bit addresses with the value selected to 0.  FAST: the range's outputs are one contiguous run of
+// Y (affine stripe map with stride w, Y row-major with 16 contiguous right-hand sides): 16-B stores.
+template <typename T, int UB, int W, int NBT, bool MASKU, bool BUF>
+__global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, const T *__restrict__ X, int64_t sxr,
+                                                            int64_t sxc, uint32_t xbytes, T *__restrict__ Y, int64_t syr,
+                                                            int64_t syc, int nrhs, T alpha, T beta, int rd_i, int fast)
+{
+    constexpr int TV = UB * W;               // values per tile slot
+    constexpr int EPL = 16 / (int)sizeof(T); // elements per lane per 16-B value load
+    constexpr int PER = 16 * EPL;            // elements per value load per 16-lane row
+    constexpr int NV = (NBT * TV + PER - 1) / PER;
+    typedef T tv __attribute__((ext_vector_type(EPL)));
+    extern __shared__ __attribute__((aligned(16))) char tile_stage[];  // kWavesPerBlock x b.stage_bytes
+    const int wv = threadIdx.x >> 6;
+    const int blk = xcd_block(blockIdx.x, gridDim.x);
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + wv));
+    if (rg >= b.nranges) return;
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const gptr<const int32_t> ri = G(b.rinfo) + (size_t)rg * 8;
+    const int tile0 = __builtin_amdgcn_readfirstlane(ri[0]), len = __builtin_amdgcn_readfirstlane(ri[1]);
+    const int s0 = __builtin_amdgcn_readfirstlane(ri[2]), ns = __builtin_amdgcn_readfirstlane(ri[3]);
+    int sidx = g == 0 ? 0 : ri[3 + g];  // this row's stripe (range-relative)
+    const int64_t kb = (int64_t)tile0 + (int64_t)g * len;  // this row's first tile slot
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    constexpr int esz = (int)sizeof(T);
+    const int jc = j < nrhs ? j : nrhs - 1;  // right-hand sides past nrhs: a valid column, never stored
+    const uint32_t sxr_b = (uint32_t)(sxr * esz), jb = (uint32_t)(jc * sxc * esz);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(X), 0, (int)xbytes, 0x00020000);
+    const gptr<const T> xg = G(X);
+    T *st = reinterpret_cast<T *>(tile_stage + wv * b.stage_bytes);
+    const T zero = T(0);
+    T acc[W];
+#pragma unroll
+    for (int c = 0; c < W; c++) acc[c] = zero;
+
+    // lane j of the row holds the key of step t0 + j, j < 2 NBT (the bin carries padding past its end)
+    static_assert(2 * NBT <= 16, "one key load covers two batches of a 16-lane row");
+    auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < 2 * NBT ? j : 2 * NBT - 1)]; };
+    auto load_vals = [&](int t0, tv (&V)[NV]) {
+        const gptr<const T> p = val + (kb + t0) * TV + j * EPL;
+#pragma unroll
+        for (int v = 0; v < NV; v++) V[v] = __builtin_nontemporal_load((gptr<const tv>)(p + v * PER));
+    };
+    auto load_x = [&](uint32_t K, int k0, T (&xs)[NBT][UB]) {
+#pragma unroll
+        for (int s = 0; s < NBT; s++) {
+            const uint32_t ks = (uint32_t)row_bcast_rt((int)K, k0 + s);
+            const bool ok = (ks & kTileValid) != 0;
+            if constexpr (BUF) {
+                // v_mad_u32_u24 reads the key's low 24 bits (the row): an invalid key's all-ones row lands
+                // past X (the launcher guarantees it), whose buffer loads return 0 -- no select
+                const uint32_t xo = __umul24(ks, sxr_b) + jb;
+#pragma unroll
+                for (int r = 0; r < UB; r++) xs[s][r] = buf_load<T>(xrs, xo, (uint32_t)r * sxr_b);
+            } else {
+                const int64_t xr = ok ? (int64_t)(ks & kTileRow) * sxr + (int64_t)jc * sxc : 0;
+#pragma unroll
+                for (int r = 0; r < UB; r++) {
+                    // a slot row the tile does not store may lie past X: read row 0 of the slot instead
+                    const bool has = !MASKU || ((ks >> (kTileMaskShift + r)) & 1);
+                    const T t = xg[xr + (has ? (int64_t)r * sxr : 0)];
+                    xs[s][r] = ok ? t : zero;
+                }
+            }
+        }
+    };
+    // per key pair: bit 16 g + k of `lastm` = LAST of step k of row g (lanes k >= 2 NBT hold copies)
+    auto fold = [&](int t0, uint32_t K, uint64_t lastm, int k0, const tv (&V)[NV], const T (&xs)[NBT][UB]) {
+#pragma unroll
+        for (int s = 0; s < NBT; s++) {
+            // (every stream is padded to a whole number of key pairs: no step past its end)
+#pragma unroll
+            for (int r = 0; r < UB; r++) {
+                T xr = xs[s][r];
+                // a slot row the tile does not store: x taken as 0 (its values are 0), so a non-finite x
+                // of a row the stripe does not store never reaches it, as in the reference
+                if constexpr (MASKU) {
+                    const uint32_t ks = (uint32_t)row_bcast_rt((int)K, k0 + s);
+                    xr = ((ks >> (kTileMaskShift + r)) & 1) ? xr : zero;
+                }
+#pragma unroll
+                for (int c = 0; c < W; c++) {
+                    const int f = s * TV + r * W + c;  // value (r, c) of step s: lane (f % PER) / EPL of the row
+                    fmac_bcast_rt(acc[c], V[f / PER][f % EPL], xr, (f % PER) / EPL);
+                }
+            }
+            // a stripe of some row ends at this step (uniform test of the pair's ballot)
+            if ((lastm >> (k0 + s)) & 0x0001000100010001ull) {
+                const bool last = ((lastm >> (16 * g + k0 + s)) & 1) != 0;
+                if (last) {
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        st[(sidx * W + c) * 16 + j] = acc[c];
+                        acc[c] = zero;
+                    }
+                }
+                sidx += last ? 1 : 0;
+            }
+        }
+    };
+
+    // Two register sets in ping-pong (copying a set would wait for its loads): while batch b is folded
+    // from one set, batch b + 1's values and X gathers fill the other.  One key load covers two batches
+    // (lane j of the row: step t0 + j), issued a pair ahead; the pair's register is copied only once its
+    // keys have been consumed by the X gathers.
+    uint32_t KA = load_keys(0);
+    tv V0[NV], V1[NV];
+    T X0[NBT][UB], X1[NBT][UB];
+    load_vals(0, V0);
+    load_x(KA, 0, X0);
+    // (sched_barrier: the fold's DPP reads of a set must not be hoisted above the other set's loads,
+    // which would make those loads wait for this set's data)
+    for (int t0 = 0; t0 < len; t0 += 2 * NBT) {
+        const uint32_t KB = load_keys(t0 + 2 * NBT);
+        load_vals(t0 + NBT, V1);
+        load_x(KA, NBT, X1);
+        const uint64_t lastm = __builtin_amdgcn_ballot_w64((KA & kTileLast) != 0);
+        __builtin_amdgcn_sched_barrier(0);
+        fold(t0, KA, lastm, 0, V0, X0);
+        __builtin_amdgcn_sched_barrier(0);
+        load_vals(t0 + 2 * NBT, V0);
+        load_x(KB, 0, X0);
+        __builtin_amdgcn_sched_barrier(0);
+        fold(t0 + NBT, KA, lastm, NBT, V1, X1);
+        __builtin_amdgcn_sched_barrier(0);
+        KA = KB;
+    }
+    // the range's outputs (stripes s0 .. s0 + ns - 1, every slot written once) from the LDS stage
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int total = ns * W * 16;
+    const bool rd = rd_i != 0;
+    if (fast) {
+        gptr<T> yb = G(Y) + ((int64_t)b.out_base + (int64_t)s0 * W) * 16;
+        for (int e = lane * EPL; e < total; e += 64 * EPL) {
+            tv v = *reinterpret_cast<const tv *>(st + e);
+            tv o;
+#pragma unroll
+            for (int q = 0; q < EPL; q++) o[q] = alpha * v[q];
+            if (rd) {
+                const tv yo = *(gptr<const tv>)(yb + e);
+#pragma unroll
+                for (int q = 0; q < EPL; q++) o[q] = fmadd(beta, yo[q], o[q]);
+            }
+            *(gptr<tv>)(yb + e) = o;
+        }
+    } else {
+        for (int e = lane; e < total; e += 64) {
+            const int i = e / (W * 16), rem = e - i * (W * 16), c = rem >> 4, jj = rem & 15;
+            if (jj >= nrhs) continue;
+            const int64_t col = (b.out_affine ? (int64_t)b.out_base + (int64_t)(s0 + i) * b.out_stride
+                                              : (int64_t)G(b.out)[s0 + i]) + c;
+            gptr<T> yo = G(Y) + col * syr + (int64_t)jj * syc;
+            T o = alpha * st[e];
+            if (rd) o = fmadd(beta, *yo, o);
+            *yo = o;
+        }
+    }
+}
+
+
+// The 16-B form (fp32, X row-major with 16 contiguous right-hand sides): the tile's u x 16 block of X is
+// u x 64 contiguous bytes, loaded by ONE dwordx4 instruction per step -- lane j = 4 r + q of the row takes
+// X[r][4q .. 4q+3] (lanes j >= 4 ub idle) -- instead of u dword loads (measured on gfx950,
+// tools/exp/ta_probe.hip: a dword load of 4 x 64-B lines costs the CU 11 cycles of address / data path,
+// a dwordx4 of 4 x 192 B 20: the dword form of a 3-row tile is 33).  Lane (r, q) then needs T[r][c], a
+// value of its own row r of the tile: three DPP row_newbcast moves per column c, each writing only the
+// lanes of bank r (bank_mask = 1 << r; the other banks keep what they hold), put T[r_lane][c] in one
+// register, and the lane folds acc[c][k] += T[r][c] * X[r][4q + k] with packed fmas.  The u banks hold
+// partial sums per slot row; a LAST tile adds them in the row (DPP row_shl 4 / 8 / 12: ((r0 + r1) + r2)
+// + r3) and bank 0 stages the stripe's 16 x w sums.  Each column is the sum over the stripe's tiles of its
+// per-slot-row chains -- the reference's products, associated by slot row (within fp32 rounding of the
+// reference's single chain, multiply_VBC.jl:131).
+template <int N, int BANK>
+__device__ __forceinline__ float bank_bcast(float old, float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                 0x150 + N, 0xF, 1 << BANK, false));
+}
+template <int BANK>
+__device__ __forceinline__ float bank_bcast_rt(float old, float v, int n)
+{
+    switch (n & 15) {
+    case 0: return bank_bcast<0, BANK>(old, v);
+    case 1: return bank_bcast<1, BANK>(old, v);
+    case 2: return bank_bcast<2, BANK>(old, v);
+    case 3: return bank_bcast<3, BANK>(old, v);
+    case 4: return bank_bcast<4, BANK>(old, v);
+    case 5: return bank_bcast<5, BANK>(old, v);
+    case 6: return bank_bcast<6, BANK>(old, v);
+    case 7: return bank_bcast<7, BANK>(old, v);
+    case 8: return bank_bcast<8, BANK>(old, v);
+    case 9: return bank_bcast<9, BANK>(old, v);
+    case 10: return bank_bcast<10, BANK>(old, v);
+    case 11: return bank_bcast<11, BANK>(old, v);
+    case 12: return bank_bcast<12, BANK>(old, v);
+    case 13: return bank_bcast<13, BANK>(old, v);
+    case 14: return bank_bcast<14, BANK>(old, v);
+    default: return bank_bcast<15, BANK>(old, v);
+    }
+}
+template <int R>
+__device__ __forceinline__ float bank_bcast_r(float old, float v, int n)
+{
+    if constexpr (R == 0) return bank_bcast_rt<0>(old, v, n);
+    else if constexpr (R == 1) return bank_bcast_rt<1>(old, v, n);
+    else if constexpr (R == 2) return bank_bcast_rt<2>(old, v, n);
+    else return bank_bcast_rt<3>(old, v, n);
+}
+// v from lane + N of the row (row_shl:N; lanes past the row's end read 0)
+template <int N>
+__device__ __forceinline__ float row_shl(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x100 + N, 0xF, 0xF, true));
+}
+
+template <int UB, int W, int NBT, bool MASKU>
+__global__ __launch_bounds__(kBlockThreads) void spmm_tiles4(const TileBin b, const float *__restrict__ X, int64_t sxr,
+                                                             uint32_t xbytes, float *__restrict__ Y, int64_t syr,
+                                                             int64_t syc, float alpha, float beta, int rd_i, int fast)
+{
+    typedef float T;
+    constexpr int TV = UB * W;
+    constexpr int EPL = 4, PER = 64;
+    constexpr int NV = (NBT * TV + PER - 1) / PER;
+    typedef float tv __attribute__((ext_vector_type(4)));
+    typedef float t2 __attribute__((ext_vector_type(2)));
+    extern __shared__ __attribute__((aligned(16))) char tile_stage[];
+    const int wv = threadIdx.x >> 6;
+    const int blk = xcd_block(blockIdx.x, gridDim.x);
+    const int rg = __builtin_amdgcn_readfirstlane((int)(blk * kWavesPerBlock + wv));
+    if (rg >= b.nranges) return;
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, rl = j >> 2, q = j & 3;
+    const gptr<const int32_t> ri = G(b.rinfo) + (size_t)rg * 8;
+    const int tile0 = __builtin_amdgcn_readfirstlane(ri[0]), len = __builtin_amdgcn_readfirstlane(ri[1]);
+    const int s0 = __builtin_amdgcn_readfirstlane(ri[2]), ns = __builtin_amdgcn_readfirstlane(ri[3]);
+    int sidx = g == 0 ? 0 : ri[3 + g];
+    const int64_t kb = (int64_t)tile0 + (int64_t)g * len;
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const uint32_t sxr_b = (uint32_t)(sxr * 4);
+    // lane (r, q): bytes r * row + 16 q of the tile's block; idle lanes (r >= ub) read past X: zeros
+    const uint32_t lb = rl < UB ? (uint32_t)rl * sxr_b + (uint32_t)q * 16u : 0x80000000u;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(X), 0, (int)xbytes, 0x00020000);
+    T *st = reinterpret_cast<T *>(tile_stage + wv * b.stage_bytes);
+    t2 acc[W][2];
+    float tc[W];  // this step's T[r_lane][c] (kept across steps: a bank only ever needs its own row)
+#pragma unroll
+    for (int c = 0; c < W; c++) {
+        acc[c][0] = acc[c][1] = t2{0.f, 0.f};
+        tc[c] = 0.f;
+    }
+
+    static_assert(2 * NBT <= 16, "one key load covers two batches of a 16-lane row");
+    auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < 2 * NBT ? j : 2 * NBT - 1)]; };
+    auto load_vals = [&](int t0, tv (&V)[NV]) {
+#ifdef VBC_TILE_DIAG_BUILD
+        const gptr<const T> p = val + (kb + ((b.diag & 2) ? 0 : t0)) * TV + j * EPL;
+#else
+        const gptr<const T> p = val + (kb + t0) * TV + j * EPL;
+#endif
+#pragma unroll
+        for (int v = 0; v < NV; v++) V[v] = __builtin_nontemporal_load((gptr<const tv>)(p + v * PER));
+    };
+    auto load_x = [&](uint32_t K, int k0, tv (&xs)[NBT]) {
+#pragma unroll
+        for (int s = 0; s < NBT; s++) {
+            const uint32_t ks = (uint32_t)row_bcast_rt((int)K, k0 + s);
+            // (an invalid key's all-ones 24-bit row lands past X: zeros, see spmm_tiles)
+#ifdef VBC_TILE_DIAG_BUILD
+            const uint32_t xo = __umul24((b.diag & 1) ? (ks & 0xFFu) : ks, sxr_b) + lb;
+#else
+            const uint32_t xo = __umul24(ks, sxr_b) + lb;
+#endif
+            xs[s] = __builtin_bit_cast(tv, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
+        }
+    };
+    auto fold = [&](uint32_t K, uint64_t lastm, int k0, const tv (&V)[NV], const tv (&xs)[NBT]) {
+#pragma unroll
+        for (int s = 0; s < NBT; s++) {
+            tv xv = xs[s];
+            if constexpr (MASKU) {
+                const uint32_t ks = (uint32_t)row_bcast_rt((int)K, k0 + s);
+                if (!((ks >> (kTileMaskShift + rl)) & 1)) xv = tv{0.f, 0.f, 0.f, 0.f};
+            }
+            const t2 x01 = t2{xv[0], xv[1]}, x23 = t2{xv[2], xv[3]};
+            // tc[c] = T[r_lane][c]: bank r receives row r's value (r outer: consecutive moves into one
+            // register are W apart, past the DPP read-after-write distance).  The banks >= ub keep stale
+            // values: their lanes load no X (zeros) and their partial sums are never read.
+#pragma unroll
+            for (int r = 0; r < UB; r++) {
+#pragma unroll
+                for (int c = 0; c < W; c++) {
+                    const int f = s * TV + r * W + c;
+                    if (r == 0) tc[c] = bank_bcast_r<0>(tc[c], V[f / PER][f % EPL], (f % PER) / EPL);
+                    else if (r == 1) tc[c] = bank_bcast_r<1>(tc[c], V[f / PER][f % EPL], (f % PER) / EPL);
+                    else if (r == 2) tc[c] = bank_bcast_r<2>(tc[c], V[f / PER][f % EPL], (f % PER) / EPL);
+                    else tc[c] = bank_bcast_r<3>(tc[c], V[f / PER][f % EPL], (f % PER) / EPL);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < W; c++) {
+                const t2 tt = t2{tc[c], tc[c]};
+                acc[c][0] = __builtin_elementwise_fma(tt, x01, acc[c][0]);
+                acc[c][1] = __builtin_elementwise_fma(tt, x23, acc[c][1]);
+            }
+            if ((lastm >> (k0 + s)) & 0x0001000100010001ull) {
+                const bool last = ((lastm >> (16 * g + k0 + s)) & 1) != 0;
+                if (last) {
+#ifdef VBC_TILE_REDUCE_DPP
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        float o[4] = {acc[c][0][0], acc[c][0][1], acc[c][1][0], acc[c][1][1]};
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            float v = o[k];
+                            if constexpr (UB > 1) v = v + row_shl<4>(o[k]);
+                            if constexpr (UB > 2) v = v + row_shl<8>(o[k]);
+                            if constexpr (UB > 3) v = v + row_shl<12>(o[k]);
+                            o[k] = v;
+                        }
+                        if (rl == 0) *reinterpret_cast<tv *>(st + (sidx * W + c) * 16 + 4 * q) = tv{o[0], o[1], o[2], o[3]};
+                        acc[c][0] = acc[c][1] = t2{0.f, 0.f};
+                    }
+#else
+                    // each slot row's partial sums to the stage: [stripe][r][c][16 right-hand sides]
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        if (rl < UB)
+                            *reinterpret_cast<tv *>(st + ((sidx * UB + rl) * W + c) * 16 + 4 * q) =
+                                tv{acc[c][0][0], acc[c][0][1], acc[c][1][0], acc[c][1][1]};
+                        acc[c][0] = acc[c][1] = t2{0.f, 0.f};
+                    }
+#endif
+                }
+                sidx += last ? 1 : 0;
+            }
+        }
+    };
+
+    uint32_t KA = load_keys(0);
+    tv V0[NV], V1[NV];
+    tv X0[NBT], X1[NBT];
+    load_vals(0, V0);
+    load_x(KA, 0, X0);
+    for (int t0 = 0; t0 < len; t0 += 2 * NBT) {
+        const uint32_t KB = load_keys(t0 + 2 * NBT);
+        load_vals(t0 + NBT, V1);
+        load_x(KA, NBT, X1);
+        const uint64_t lastm = __builtin_amdgcn_ballot_w64((KA & kTileLast) != 0);
+        __builtin_amdgcn_sched_barrier(0);
+        fold(KA, lastm, 0, V0, X0);
+        __builtin_amdgcn_sched_barrier(0);
+        load_vals(t0 + 2 * NBT, V0);
+        load_x(KB, 0, X0);
+        __builtin_amdgcn_sched_barrier(0);
+        fold(KA, lastm, NBT, V1, X1);
+        __builtin_amdgcn_sched_barrier(0);
+        KA = KB;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int total = ns * W * 16;
+    const bool rd = rd_i != 0;
+    // stripe i's sums: ((r0 + r1) + r2) + r3 of its slot rows' partials
+    auto staged = [&](int e) -> tv {
+        const int i = e / (W * 16), rem = e - i * (W * 16);
+#ifdef VBC_TILE_REDUCE_DPP
+        return *reinterpret_cast<const tv *>(st + e);
+#else
+        const T *p = st + i * UB * W * 16 + rem;
+        tv v = *reinterpret_cast<const tv *>(p);
+#pragma unroll
+        for (int r = 1; r < UB; r++) v += *reinterpret_cast<const tv *>(p + r * W * 16);
+        return v;
+#endif
+    };
+    if (fast) {
+        gptr<T> yb = G(Y) + ((int64_t)b.out_base + (int64_t)s0 * W) * 16;
+        for (int e = lane * EPL; e < total; e += 64 * EPL) {
+            const tv v = staged(e);
+            tv o;
+#pragma unroll
+            for (int k = 0; k < 4; k++) o[k] = alpha * v[k];
+            if (rd) {
+                const tv yo = *(gptr<const tv>)(yb + e);
+#pragma unroll
+                for (int k = 0; k < 4; k++) o[k] = fmadd(beta, yo[k], o[k]);
+            }
+            *(gptr<tv>)(yb + e) = o;
+        }
+    } else {
+        for (int e = lane * EPL; e < total; e += 64 * EPL) {
+            const int i = e / (W * 16), rem = e - i * (W * 16), c = rem >> 4, jj = rem & 15;
+            const int64_t col = (b.out_affine ? (int64_t)b.out_base + (int64_t)(s0 + i) * b.out_stride
+                                              : (int64_t)G(b.out)[s0 + i]) + c;
+            const tv v = staged(e);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                gptr<T> yo = G(Y) + col * syr + (int64_t)(jj + k) * syc;
+                T o = alpha * v[k];
+                if (rd) o = fmadd(beta, *yo, o);
+                *yo = o;
+            }
+        }
+    }
+}
+
+}  // namespace vbc

@@ -18,12 +18,19 @@ DEV = "cuda:0"
 TOL64, TOL32 = 1e-12, 1e-5
 
 
-@pytest.fixture(autouse=True, params=["8", "0"], ids=["quads", "panels"])
+@pytest.fixture(autouse=True, params=["tiles", "8", "0"], ids=["tiles", "quads", "panels"])
 def multi_layout(request, monkeypatch):
-    """Every test on both multi-RHS layouts: every width on the MFMA panels (the default,
-    VBC_PANEL_QUADS=0) and, with VBC_PANEL_QUADS=8, stripes of width <= 8 in the VALU stripe-quad layout
-    (spmm_quads; measured slower on both C5 inputs, kept as the A/B alternative)."""
-    monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
+    """Every test on the three multi-RHS layouts: every width on the MFMA panels (VBC_PANEL_QUADS=0,
+    VBC_PANEL_TILES=0); stripes of width <= 8 in the VALU stripe-quad layout (VBC_PANEL_QUADS=8; spmm_quads,
+    measured slower on both C5 inputs, kept as the A/B alternative); and (round 5) every bucket of width <= 4
+    whose tiles are <= 4 rows in the tile-granular layout (VBC_PANEL_TILES=1, spmm_tiles -- the default
+    for such buckets when their rows come in tiles)."""
+    if request.param == "tiles":
+        monkeypatch.setenv("VBC_PANEL_TILES", "1")
+        monkeypatch.setenv("VBC_PANEL_QUADS", "0")
+    else:
+        monkeypatch.setenv("VBC_PANEL_TILES", "0")
+        monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
     return request.param
 
 
@@ -221,3 +228,96 @@ def test_quads_layout_flag_and_mixed_widths(multi_layout):
     Yd = as_dev(np.zeros((B.n, 16), np.float32), "R")
     V.mul_(Yd, B.T, as_dev(X, "R"), engine="mfma")
     assert rel(Yd.cpu().numpy(), ref_cols(R, X, np.zeros((B.n, 16)), 1.0, 0.0)) <= TOL32
+
+
+def _vbc2d_mixed_heights(rng, K, L, q, heights, widths, dtype):
+    """A SparseMatrixVBC whose block rows have the given heights (cycled) and stripes the given widths:
+    q distinct random (k, l) tiles, dense u_k x w_l blocks (constructors_VBC.jl:95-105 layout)."""
+    u = np.array([heights[i % len(heights)] for i in range(K)])
+    w = np.array([widths[i % len(widths)] for i in range(L)])
+    pspl = np.concatenate([[1], 1 + np.cumsum(u)])
+    spl = np.concatenate([[1], 1 + np.cumsum(w)])
+    keys = np.unique(rng.integers(0, K * L, q))
+    l, k = keys // K, keys % K  # sorted by stripe, then block row
+    cnt = np.bincount(l, minlength=L)
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)])
+    sizes = u[k] * w[l]
+    ofs = np.concatenate([[1], 1 + np.cumsum(np.bincount(l, weights=sizes, minlength=L).astype(np.int64))])
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + 64, dtype)
+    val[:nv] = rng.uniform(-1, 1, nv)
+    return V.SparseMatrixVBC(4, 4, int(pspl[-1] - 1), int(spl[-1] - 1), V.SplitPartition(pspl), V.SplitPartition(spl),
+                             pos, k + 1, ofs, val)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_tiles_mixed_heights_widths_every_column(dtype, multi_layout):
+    """Tile layout (spmm_tiles): block rows of heights 1..4 in one stripe (slot rows past a tile's height
+    masked), widths 1..4 (one bucket each, non-affine columns), empty stripes, 5 / 16 / 21 right-hand sides,
+    row- and column-major operands, alpha / beta, both directions -- every column against the oracle, and
+    with VBC_PANEL_TILES=1 the layout flag (vbc_info planar_mask bit 9)."""
+    rng = np.random.default_rng(61)
+    tol = TOL64 if dtype == np.float64 else TOL32
+    B = _vbc2d_mixed_heights(rng, 300, 400, 1200, (3, 1, 4, 2, 3), (1, 3, 2, 4, 3), dtype)
+    assert (np.diff(B.pos) == 0).any()
+    if multi_layout == "tiles":
+        assert B.info(multi=True)["planar_mask"] & 512
+        assert B.info(trans=False, multi=True)["planar_mask"] & 512
+    R = ref_2d(B)
+    for nrhs in (5, 16, 21):
+        for layout in ("R", "C"):
+            for trans in (True, False):
+                nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+                X = rng.uniform(-1, 1, (nx, nrhs)).astype(dtype)
+                Y0 = rng.uniform(-1, 1, (ny, nrhs)).astype(dtype)
+                alpha, beta = (1.0, 0.0) if nrhs == 16 else (0.5, -1.25)
+                Yd = as_dev(Y0, layout)
+                V.mul_(Yd, B.T if trans else B, as_dev(X, layout), alpha, beta, engine="mfma")
+                Rd = R
+                if dtype != np.float64:
+                    Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+                want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64),
+                                       np.ascontiguousarray(Y0[:, j], dtype=np.float64), alpha, beta, trans=trans,
+                                       ref_semantics=False) for j in range(nrhs)], axis=1)
+                assert rel(Yd.cpu().numpy(), want) <= tol, (nrhs, layout, trans)
+
+
+def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
+    """A 1DVBC whose stripes store node runs of 3 rows, some missing one row (the hole is a masked slot row
+    of its tile): integer data bit for bit on all 16 columns (each column is the reference's fma chain);
+    an Inf / NaN in X at a hole row reaches no stripe that does not store it."""
+    rng = np.random.default_rng(62)
+    N, L = 500, 300
+    rows, cnt = [], []
+    for l in range(L):
+        nodes = np.sort(rng.choice(N, 10, replace=False))
+        r = (nodes[:, None] * 3 + np.arange(3)[None, :]).reshape(-1)
+        if l % 4 == 0:
+            r = np.delete(r, rng.integers(0, len(r)))
+        rows.append(r)
+    widths = 1 + np.arange(L) % 3
+    cnt = np.array([len(r) for r in rows])
+    pos = np.concatenate([[1], 1 + np.cumsum(cnt)])
+    ofs = np.concatenate([[1], 1 + np.cumsum(cnt * widths)])
+    spl = np.concatenate([[1], 1 + np.cumsum(widths)])
+    nv = int(ofs[-1] - 1)
+    val = np.zeros(nv + 8)
+    val[:nv] = rng.integers(-8, 9, nv)
+    B = V.SparseMatrix1DVBC(8, 3 * N, int(spl[-1] - 1), V.SplitPartition(spl), pos, np.concatenate(rows) + 1, ofs, val)
+    if multi_layout == "tiles":
+        assert B.info(multi=True)["planar_mask"] & 512
+    R = ref_1d(B)
+    X = rng.integers(-8, 9, (B.m, 16)).astype(np.float64)
+    Yd = as_dev(np.full((B.n, 16), np.nan), "R")
+    V.mul_(Yd, B.T, as_dev(X, "R"), engine="mfma")
+    assert np.array_equal(Yd.cpu().numpy(), ref_cols(R, X, np.zeros((B.n, 16)), 1.0, 0.0))
+    hole = [r for r in range(3 * (rows[0][0] // 3), 3 * (rows[0][-1] // 3) + 3)
+            if r not in set(rows[0].tolist()) and (r // 3) in set((rows[0] // 3).tolist())]
+    assert hole
+    X[hole[0], :] = np.nan
+    X[hole[0], 5] = np.inf
+    V.mul_(Yd, B.T, as_dev(X, "R"), engine="mfma")
+    got, ref = Yd.cpu().numpy(), ref_cols(R, X, np.zeros((B.n, 16)), 1.0, 0.0)
+    assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    assert np.array_equal(got[fin], ref[fin])

@@ -17,12 +17,16 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(autouse=True, params=["8", "0"], ids=["quads", "panels"])
+@pytest.fixture(autouse=True, params=["tiles", "8", "0"], ids=["tiles", "quads", "panels"])
 def multi_layout(request, monkeypatch):
-    """Every test on both multi-RHS layouts: every width on the MFMA panels (the default,
-    VBC_PANEL_QUADS=0) and, with VBC_PANEL_QUADS=8, stripes of width <= 8 in the VALU stripe-quad layout
-    (spmm_quads; measured slower on both C5 inputs, kept as the A/B alternative)."""
-    monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
+    """Every test on the three multi-RHS layouts (test_gpu_mfma.py): MFMA panels, VALU stripe quads, and
+    the tile-granular layout of C = Bᵀ's small tiles (VBC_PANEL_TILES=1)."""
+    if request.param == "tiles":
+        monkeypatch.setenv("VBC_PANEL_TILES", "1")
+        monkeypatch.setenv("VBC_PANEL_QUADS", "0")
+    else:
+        monkeypatch.setenv("VBC_PANEL_TILES", "0")
+        monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
     return request.param
 
 

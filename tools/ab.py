@@ -98,7 +98,9 @@ def main():
                 os.environ[ek.strip()] = ev_.strip()
         hp = C.c_void_p()
         flags = L.VBC_CREATE_TRANSPOSED if trans else L.VBC_CREATE_FORWARD
-        if "@multi" in v:  # matrix-core panel layout (multi-RHS transposed product)
+        if "@multifwd" in v:  # multi-RHS forward product (panel / tile layout of B')
+            flags = L.VBC_CREATE_MULTI_FORWARD
+        elif "@multi" in v:  # matrix-core panel layout (multi-RHS transposed product)
             flags = L.VBC_CREATE_MULTI
         L.check(B._create(C.byref(hp), 0, flags, L.compute_code(B.val.dtype)), "create")
         os.environ.clear()
