@@ -483,7 +483,10 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
                 // shard (2500 chunks) and the whole ldoor keep the lane pairs (37.6 vs P = 2 40.6; 67 vs 87)
                 const double avg = (double)rows * (pair ? 3 : 1) / (double)std::max<int64_t>(nch, 1);  // x rows
                 const double minrows = (double)h->split_rows * esz / 8.0;
-                while (split < 8 && (double)nch / (pair ? 2 : 1) * split * 2 <= 2 * share && avg / (split * 2) >= minrows)
+                // (round 5: the doubled grid stays within ONE round of wave slots -- ldoor's 1/4 stripe shard,
+                // 1249 chunks: P = 2 19.7 us, P = 4 20.5; the 1/8 shard keeps P = 4, 11.0 us against P = 2 11.8,
+                // profiles/r05_shards_ab.log)
+                while (split < 8 && (double)nch / (pair ? 2 : 1) * split * 2 <= share && avg / (split * 2) >= minrows)
                     split *= 2;
             }
         }
@@ -507,7 +510,10 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     // waves' x window in L2: ldoor fp64 lane pairs 3 -> 2 waves per SIMD 67.8 -> 65.4 us, fp32 4 -> 2
     // 36.5 -> 34.7 us, the C4 CSC product 36.7 -> 34.6 us; 1.5 or 2.5 per SIMD are slower,
     // profiles/r03_bxranges2_*.log, r03_wps_*.log)
-    if (planar && split == 1 && h->planar_wps > 0) nr = std::min<int64_t>(nr, std::max<int64_t>(1, std::llround(quantum * h->planar_wps)));
+    // (round 5: the fp64 lane-pair layout takes one wave per SIMD -- ldoor 64.4 -> 63.2 us, its 1/2 stripe
+    // shard 36.5 -> 34.7 us; fp32 planar keeps two: ldoor fp32 34.9 vs 36.9, profiles/r05_shards_ab.log)
+    const int wps = (pair && h->planar_wps_pair > 0) ? h->planar_wps_pair : h->planar_wps;
+    if (planar && split == 1 && wps > 0) nr = std::min<int64_t>(nr, std::max<int64_t>(1, std::llround(quantum * wps)));
     nr = std::max<int64_t>(1, std::min<int64_t>(nr, nch));
     // fewer chunks than wave slots: whole waves per SIMD (ldoor's 1/4 shard: 2500 pair chunks as 2500
     // ranges 33.0 us, as 2048 ranges 27.7 us)
@@ -2963,7 +2969,8 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_SPLIT_DEEP")) h->split_deep = std::max(0.0, atof(e));
     if (const char *e = getenv("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
     if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
-    if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = std::max(0, atoi(e));
+    if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = h->planar_wps_pair = std::max(0, atoi(e));
+    if (const char *e = getenv("VBC_PLANAR_WPS_PAIR")) h->planar_wps_pair = std::max(0, atoi(e));
     if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     h->cus = std::max(1, prop.multiProcessorCount);

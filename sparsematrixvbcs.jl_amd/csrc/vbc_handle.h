@@ -194,6 +194,7 @@ struct vbc_handle {
     int split_rows = 12;              // VBC_SPLIT_ROWS: fewest chunk rows per wave of an automatic split
     int fwd_min_rows = 16;            // VBC_FWD_MIN_ROWS: fewest chunk rows per range of the forward run layout
     int planar_wps = 2;               // VBC_PLANAR_WPS: most resident waves per SIMD of a plain planar bin (0: occupancy)
+    int planar_wps_pair = 1;          // VBC_PLANAR_WPS_PAIR: the same for the fp64 lane-pair layout
     int lanes_pair = 0;               // VBC_LANES_PAIR=1: a lane pair per stream in the lane-stream layout (fp64 w = 3,
                                       // runs of 3; one 16-B x gather per lane per run).  FE-3D measured 217 -> 223 us
                                       // with pairs (profiles/r03_ab_pairlanes_fe3d.log), so off by default

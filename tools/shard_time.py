@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--forward", action="store_true", help="also time the forward product B_r x_r of every shard")
     args = ap.parse_args()
     import torch
 
@@ -40,6 +41,7 @@ def main():
     x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, B.m).astype(dtype)).to(device)
     stream = torch.cuda.Stream(device)
     base = None
+    fbase = [None]
     for world in (int(w) for w in args.worlds.split(",")):
         cuts = V.distributed.stripe_split(B, world)
         per = []
@@ -53,18 +55,41 @@ def main():
                     V.mul_(y, St, x)
             torch.cuda.synchronize(device)
             wall, ev_ms, _ = bench.timed_products(lambda: V.mul_(y, St, x), args.steps, device, stream, 1)
-            per.append({"rank": r, "stripes": int(cuts[r + 1] - cuts[r]), "bytes": bench.algorithmic_bytes(S, esz),
-                        "us_event": round(ev_ms * 1e3, 2), "us_wall": round(wall / args.steps * 1e6, 2),
-                        "kernel": bench.kernel_name(S, 0, 1)})
+            rec = {"rank": r, "stripes": int(cuts[r + 1] - cuts[r]), "bytes": bench.algorithmic_bytes(S, esz),
+                   "us_event": round(ev_ms * 1e3, 2), "us_wall": round(wall / args.steps * 1e6, 2),
+                   "kernel": bench.kernel_name(S, 0, 1)}
+            if args.forward:  # C3's forward leg: mul!(y, B_r, x_r) on the shard -> a partial y of length m
+                xf = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, S.n).astype(dtype)).to(device)
+                yf = torch.empty(S.m, dtype=x.dtype, device=device)
+                with torch.cuda.stream(stream):
+                    S.handle(0, False)
+                    for _ in range(args.warmup):
+                        V.mul_(yf, S, xf)
+                torch.cuda.synchronize(device)
+                fw, fev, _ = bench.timed_products(lambda: V.mul_(yf, S, xf), args.steps, device, stream, 1)
+                rec.update(fwd_us_event=round(fev * 1e3, 2), fwd_us_wall=round(fw / args.steps * 1e6, 2),
+                           fwd_kernel=bench.kernel_name(S, 0, 1, trans=False),
+                           allreduce_bytes=int(S.m * esz) if world > 1 else 0)
+                del xf, yf
+            per.append(rec)
             if world > 1:
                 S.release()
             del y
         slow = max(p["us_wall"] for p in per)
         if base is None:
             base = slow
-        print(json.dumps({"workload": args.workload, "dtype": args.dtype, "world": world,
-                          "max_us_wall": slow, "speedup_vs_first": round(base / slow, 3),
-                          "value_GBs": round(total / (slow * 1e-6) / 1e9, 1), "shards": per}), flush=True)
+        line = {"workload": args.workload, "dtype": args.dtype, "world": world,
+                "max_us_wall": slow, "speedup_vs_first": round(base / slow, 3),
+                "value_GBs": round(total / (slow * 1e-6) / 1e9, 1), "shards": per}
+        if args.forward:
+            fslow = max(p["fwd_us_wall"] for p in per)
+            if fbase[0] is None:
+                fbase[0] = fslow
+            line.update(fwd_max_us_wall=fslow, fwd_speedup_vs_first=round(fbase[0] / fslow, 3),
+                        fwd_allreduce_bytes=per[0]["allreduce_bytes"],
+                        fwd_note="kernel only: each rank's partial y then goes through one all_reduce(sum) of "
+                                 "allreduce_bytes over RCCL (not timed on one GPU)")
+        print(json.dumps(line), flush=True)
         torch.cuda.empty_cache()
 
 
