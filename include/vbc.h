@@ -306,7 +306,9 @@ typedef struct vbc_info {
                                forward product runs on the transposed layout of C = Bᵀ (stripes of several
                                widths: one fused launch instead of one per width); bit 9: the multi-RHS
                                layout has tile-granular buckets (u, w <= 4 tiles: one key and one u-row X
-                               block per tile, spmm_tiles) */
+                               block per tile, spmm_tiles); bit 10: some of those buckets in the staged-X
+                               form (clusters of stripes sharing row groups, the groups staged in LDS,
+                               spmm_tiles_x) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

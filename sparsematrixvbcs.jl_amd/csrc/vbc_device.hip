@@ -1940,6 +1940,9 @@ struct PendingPanel {
     TileBin tb;  // tile: a small-tile bucket (vbc_tiles.h; o_rgrp = its range table)
     bool tile = false;
     size_t o_key, o_val, o_out, o_rgrp, o_rseg;
+    size_t o_xrow = 0;  // staged tile bucket: the clusters' row groups
+    size_t o_wg = 0;    // staged tile bucket: per persistent workgroup {first cluster, clusters}
+    size_t zoff = 0;    // staged tile bucket: byte offset of >= 16 zero bytes in the value array (its padding)
 };
 
 // Stripe-quad bucket (vbc_panel.h spmm_quads): chunks of 16 stripes of width w <= 8, chunk rows = its
@@ -2192,6 +2195,265 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
                 seen |= bit;
             }
             tl[i] = std::max<int64_t>(t, 1);
+        }
+    }
+    // Staged-X form (round 5b, vbc_tiles.h spmm_tiles_x): clusters of stripes that gather the same row groups,
+    // one workgroup each, the cluster's distinct row groups staged in LDS once per product.  A cluster is a
+    // BFS ball of the stripe graph (two stripes adjacent when they store tiles of one row group), grown from
+    // a seed on the previous cluster's frontier (consecutive clusters -- one XCD's run of workgroups -- share
+    // their border groups in L2) until it holds tile_smax stripes or its groups would pass the LDS stage.
+    // Auto (tile_stage < 0): only when the clusters gather each staged group >= tile_reuse times.
+    if (h->tile_stage != 0) {
+        constexpr int NB = kTileXBatch, D = kTileXDepth;
+        // fp32: the persistent kernel (spmm_tiles_xp) double-buffers both LDS stages, so its clusters are smaller
+        const bool persist = h->tile_persist && esz == 4;
+        // stripes per cluster: the kernels' epilogues hold kTileXOutPieces 16-B output pieces per thread (the
+        // persistent writer wave kTileXPOut per lane)
+        int64_t Smax = h->tile_smax > 0 ? h->tile_smax : (persist ? 48 : 64);
+        Smax = std::min<int64_t>(Smax, (int64_t)kTileXOutPieces * kBlockThreads * 16 / ((int64_t)w * 16 * esz));
+        if (persist) Smax = std::min<int64_t>(Smax, (int64_t)kTileXPOut * 64 * 16 / ((int64_t)w * 16 * esz));
+        Smax = std::max<int64_t>(1, Smax);
+        const int64_t stage = (Smax * w * 16 * esz + 15) / 16 * 16;
+        const int64_t slot_b = (int64_t)ub * 16 * esz;
+        // the LDS stage, and the kernels' staging pieces per thread (16-B pieces: (U + 1) x ub x 16 elements)
+        int64_t Umax = h->tile_umax > 0 ? h->tile_umax : (persist ? 160 : 192);
+        Umax = std::min<int64_t>({Umax, (kTileXLds - stage) / slot_b - 1, (int64_t)kTileXPieces * kBlockThreads * 16 / slot_b - 1});
+        if (persist)  // both stages double-buffered in the CU's LDS share of one of tile_wgpc workgroups
+            Umax = std::min<int64_t>({Umax, (kTileXPLds / std::max(1, h->tile_wgpc) - 2 * stage - 128) / (2 * slot_b) - 1,
+                                      (int64_t)kTileXPLoad * 64 * 16 / slot_b - 1});
+        std::vector<int64_t> sgb(n + 1, 0), sg;  // per stripe: its row groups (base rows), stored order
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t l = stripes[i];
+            int64_t cb = -1;
+            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+                int64_t base;
+                int u;
+                group_of(s.rows[q], R, base, u);
+                if (base != cb) sg.push_back(base);
+                cb = base;
+            }
+            sgb[i + 1] = (int64_t)sg.size();
+        }
+        std::vector<int64_t> gsb(s.m + 1, 0), gs(sg.size());  // per group: its stripes
+        for (int64_t g : sg) gsb[g + 1]++;
+        for (int64_t r = 0; r < s.m; r++) gsb[r + 1] += gsb[r];
+        {
+            std::vector<int64_t> at(gsb.begin(), gsb.end() - 1);
+            for (int64_t i = 0; i < n; i++)
+                for (int64_t e = sgb[i]; e < sgb[i + 1]; e++) gs[at[sg[e]]++] = i;
+        }
+        std::vector<char> taken(n, 0);
+        std::vector<int64_t> mark_s(n, -1), mark_g(s.m, -1), corder, cbeg{0}, queue, ug;
+        std::vector<int32_t> xrow, xbeg{0};
+        corder.reserve(n);
+        int64_t scan = 0, seed = -1, cid = 0;
+        bool fits = Umax >= 1;
+        while (fits && (int64_t)corder.size() < n) {
+            if (seed < 0 || taken[seed]) {
+                while (taken[scan]) scan++;
+                seed = scan;
+            }
+            queue.assign(1, seed);
+            mark_s[seed] = cid;
+            ug.clear();
+            int64_t cnt = 0, next = -1;
+            for (size_t hd = 0; hd < queue.size(); hd++) {
+                const int64_t st = queue[hd];
+                int64_t add = 0;
+                for (int64_t e = sgb[st]; e < sgb[st + 1]; e++) add += mark_g[sg[e]] != cid;
+                if (cnt == Smax || (int64_t)ug.size() + add > Umax) {
+                    if (cnt == 0) fits = false;  // one stripe's groups exceed the stage
+                    next = st;
+                    break;
+                }
+                corder.push_back(st);
+                taken[st] = 1;
+                cnt++;
+                for (int64_t e = sgb[st]; e < sgb[st + 1]; e++) {
+                    const int64_t gg = sg[e];
+                    if (mark_g[gg] == cid) continue;
+                    mark_g[gg] = cid;
+                    ug.push_back(gg);
+                    for (int64_t f = gsb[gg]; f < gsb[gg + 1]; f++) {
+                        const int64_t t = gs[f];
+                        if (!taken[t] && mark_s[t] != cid) {
+                            mark_s[t] = cid;
+                            queue.push_back(t);
+                        }
+                    }
+                }
+            }
+            std::sort(ug.begin(), ug.end());
+            for (int64_t gg : ug) xrow.push_back((int32_t)gg);
+            xbeg.push_back((int32_t)xrow.size());
+            cbeg.push_back((int64_t)corder.size());
+            seed = next;
+            cid++;
+        }
+        int64_t ttl = 0;
+        for (int64_t t : tl) ttl += t;
+        const double reuse = fits ? (double)ttl / (double)std::max<size_t>(xrow.size(), 1) : 0.0;
+        if (getenv("VBC_VERBOSE"))
+            fprintf(stderr, "[vbc] tiles: staged X %s: %lld clusters of <= %lld stripes, %zu staged groups, %.2f tiles per group\n",
+                    fits ? "fits" : "does not fit", (long long)cid, (long long)Smax, xrow.size(), reuse);
+        if (fits && (h->tile_stage > 0 || reuse >= h->tile_reuse)) {
+            const int64_t nc = cid;
+            // Workgroups of the persistent kernel (spmm_tiles_xp): nwg (a multiple of 8 when >= 8), each taking a
+            // sequence of clusters.  The clusters are cut into 8 contiguous runs (BFS order: neighbours), one per
+            // XCD (xcd_block maps the logical workgroups of XCD x to a contiguous block), and run x's j-th cluster
+            // goes to that XCD's workgroup j mod n_x: at any time an XCD's workgroups hold consecutive clusters.
+            int64_t nwg = std::min<int64_t>(nc, (int64_t)h->cus * std::max(1, h->tile_wgpc));
+            if (nwg >= 8) nwg = nwg / 8 * 8;
+            std::vector<std::vector<int64_t>> wgc(nwg);
+            {
+                const int64_t parts = nwg >= 8 ? 8 : 1;
+                for (int64_t x = 0; x < parts; x++) {
+                    const int64_t c0 = x * nc / parts, c1 = (x + 1) * nc / parts;
+                    const int64_t w0 = x * nwg / parts, nx = (x + 1) * nwg / parts - w0;
+                    for (int64_t c = c0; c < c1; c++) wgc[w0 + (c - c0) % nx].push_back(c);
+                }
+            }
+            // per cluster: streams (LPT), sorted so wave k takes streams 4k .. 4k+3; its segment = the longest of
+            // its four in whole batches (at least one: every wave meets every cluster's END)
+            std::vector<std::array<std::vector<int64_t>, kTileXStreams>> csm(nc);
+            std::vector<std::array<int64_t, 4>> clen(nc);
+            for (int64_t c = 0; c < nc; c++) {
+                std::vector<int64_t> byl(corder.begin() + cbeg[c], corder.begin() + cbeg[c + 1]);
+                std::stable_sort(byl.begin(), byl.end(), [&](int64_t x, int64_t y) { return tl[x] > tl[y]; });
+                std::array<int64_t, kTileXStreams> load{};
+                std::array<std::vector<int64_t>, kTileXStreams> sm;
+                for (int64_t i : byl) {  // longest first to the least loaded stream
+                    const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                    load[k] += tl[i];
+                    sm[k].push_back(i);
+                }
+                std::array<int, kTileXStreams> so;
+                for (int k = 0; k < kTileXStreams; k++) so[k] = k;
+                std::stable_sort(so.begin(), so.end(), [&](int x, int y) { return load[x] > load[y]; });
+                for (int k = 0; k < kTileXStreams; k++) csm[c][k] = std::move(sm[so[k]]);
+                for (int wv = 0; wv < 4; wv++)
+                    clen[c][wv] = std::max<int64_t>(NB, (load[so[4 * wv]] + NB - 1) / NB * NB);
+            }
+            // cinfo in workgroup order; per workgroup and wave one contiguous stream per row (its clusters'
+            // segments back to back), row g at base + g x Ltot
+            std::vector<int32_t> cinfo((size_t)nc * kTileXInfo, 0), out(n), wginfo((size_t)nwg * 2, 0);
+            std::vector<int64_t> lorder(n), cof(nc);  // position -> stripe index; new cluster index -> old
+            int64_t slot_total = 0, most_s = 1, most_u = 0, pos = 0, ci_n = 0;
+            for (int64_t L = 0; L < nwg; L++) {
+                wginfo[2 * L] = (int32_t)ci_n;
+                wginfo[2 * L + 1] = (int32_t)wgc[L].size();
+                std::array<int64_t, 4> base{}, ltot{}, off{};
+                for (int wv = 0; wv < 4; wv++) {
+                    for (int64_t c : wgc[L]) ltot[wv] += clen[c][wv];
+                    base[wv] = slot_total;
+                    slot_total += 4 * ltot[wv];
+                }
+                if (slot_total >= (int64_t(1) << 31) / std::max(1, TV)) return false;
+                for (int64_t c : wgc[L]) {
+                    int32_t *ci = &cinfo[(size_t)ci_n * kTileXInfo];
+                    cof[ci_n++] = c;
+                    ci[0] = (int32_t)pos;
+                    ci[1] = (int32_t)(cbeg[c + 1] - cbeg[c]);
+                    ci[2] = xbeg[c + 1] - xbeg[c];
+                    ci[3] = xbeg[c];
+                    for (int k = 0; k < kTileXStreams; k++) {
+                        ci[8 + k] = (int32_t)(pos - ci[0]);
+                        for (int64_t i : csm[c][k]) lorder[pos++] = i;
+                    }
+                    for (int wv = 0; wv < 4; wv++) {
+                        ci[4 + wv] = (int32_t)ltot[wv];
+                        ci[24 + wv] = (int32_t)(base[wv] + off[wv]);
+                        ci[28 + wv] = (int32_t)clen[c][wv];
+                        off[wv] += clen[c][wv];
+                    }
+                    most_s = std::max<int64_t>(most_s, ci[1]);
+                    most_u = std::max<int64_t>(most_u, ci[2]);
+                }
+            }
+            for (int64_t q = 0; q < n; q++) out[q] = (int32_t)s.col0[stripes[lorder[q]]];
+            const int64_t kpad = (D + 1) * NB + 16, vpad = (int64_t)((D + 1) * NB + 2) * TV + 64;
+            pp = PendingPanel{};
+            pp.tile = true;
+            TileBin &tb = pp.tb;
+            tb.w = w;
+            tb.ub = ub;
+            tb.nbt = NB;
+            tb.staged = 1;
+            if (const char *e = getenv("VBC_TILE_DIAG")) tb.diag = atoi(e);  // (ablations, tools/ab.py)
+            tb.xslots = (int32_t)(most_u + 1);
+            tb.stage_bytes = (int32_t)((most_s * w * 16 * esz + 15) / 16 * 16);
+            tb.nranges = (int32_t)nc;
+            tb.nwg = (int32_t)nwg;
+            tb.out_affine = 0;
+            pp.o_key = ar.reserve((slot_total + kpad) * 4);
+            pp.o_val = ar.reserve((slot_total * TV + vpad) * esz);
+            pp.zoff = (size_t)((slot_total * TV + vpad) * esz - 64) / 16 * 16;
+            pp.o_out = ar.reserve(n * 4);
+            pp.o_rgrp = ar.reserve(cinfo.size() * 4);
+            pp.o_wg = ar.reserve(wginfo.size() * 4);
+            xrow.push_back(0);  // the kernel reads slot U's row (unused): one entry past the last cluster's
+            pp.o_xrow = ar.reserve(xrow.size() * 4);
+            std::memcpy(ar.at<int32_t>(pp.o_out), out.data(), out.size() * 4);
+            std::memcpy(ar.at<int32_t>(pp.o_rgrp), cinfo.data(), cinfo.size() * 4);
+            std::memcpy(ar.at<int32_t>(pp.o_wg), wginfo.data(), wginfo.size() * 4);
+            std::memcpy(ar.at<int32_t>(pp.o_xrow), xrow.data(), xrow.size() * 4);
+            uint32_t *key = ar.at<uint32_t>(pp.o_key);
+            char *vv = ar.at<char>(pp.o_val);
+            std::fill(key, key + slot_total + kpad, 0u);
+            std::memset(vv, 0, (size_t)(slot_total * TV + vpad) * esz);
+            bool masku = false;
+            std::vector<int32_t> gslot(s.m, -1);
+            for (int64_t cn = 0; cn < nc; cn++) {
+                const int32_t *ci = &cinfo[(size_t)cn * kTileXInfo];
+                const int64_t c = cof[cn];
+                const uint32_t U = (uint32_t)ci[2];
+                for (int32_t x = xbeg[c]; x < xbeg[c + 1]; x++) gslot[xrow[x]] = x - xbeg[c];
+                for (int k = 0; k < kTileXStreams; k++) {
+                    const int64_t len = ci[28 + k / 4];
+                    int64_t slot = ci[24 + k / 4] + (int64_t)(k % 4) * ci[4 + k / 4];
+                    const int64_t first = slot;
+                    for (int64_t i : csm[c][k]) {
+                        const int64_t l = stripes[i];
+                        if (s.rbeg[l + 1] == s.rbeg[l]) {  // empty stripe: one zero-slot LAST tile
+                            key[slot++] = kTileLast | U;
+                            continue;
+                        }
+                        int64_t cb = -1;
+                        unsigned seen = 0;
+                        for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
+                            int64_t base;
+                            int u;
+                            group_of(s.rows[q], R, base, u);
+                            const int rr = (int)(s.rows[q] - base);
+                            const unsigned bit = 1u << rr;
+                            if (base != cb || (seen & bit)) {
+                                if (cb >= 0) {
+                                    key[slot] = (uint32_t)gslot[cb] | (seen << kTileMaskShift);
+                                    masku = masku || seen != (1u << ub) - 1;
+                                    slot++;
+                                }
+                                cb = base;
+                                seen = 0;
+                            }
+                            seen |= bit;
+                            std::memcpy(vv + (slot * TV + (int64_t)rr * w) * esz,
+                                        val + (s.voff[l] + (q - s.rbeg[l]) * w) * esz, (size_t)w * esz);
+                        }
+                        key[slot] = (uint32_t)gslot[cb] | (seen << kTileMaskShift) | kTileLast;
+                        masku = masku || seen != (1u << ub) - 1;
+                        slot++;
+                    }
+                    for (; slot < first + len; slot++) key[slot] = U;  // padding: the zero slot
+                    key[first + len - 1] |= kTileXEnd;                 // the segment's last tile
+                }
+            }
+            tb.masku = masku ? 1 : 0;
+            h->bytes_m += slot_total * (4 + (int64_t)TV * esz) + (int64_t)xrow.size() * (4 + slot_b) + nc * kTileXInfo * 4;
+            if (getenv("VBC_VERBOSE"))
+                fprintf(stderr, "[vbc] tiles: staged X, w %d, ub %d: %lld clusters on %lld workgroups, <= %lld stripes and %lld groups each, %lld slots%s\n",
+                        w, ub, (long long)nc, (long long)nwg, (long long)most_s, (long long)most_u, (long long)slot_total,
+                        masku ? ", masked rows" : "");
+            return true;
         }
     }
     // ranges: <= smax stripes (the LDS stage), a whole number of rounds of resident waves, balanced by tiles
@@ -2632,6 +2894,10 @@ static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, P
             t.val = base + pp.o_val;
             t.out = reinterpret_cast<const int32_t *>(base + pp.o_out);
             t.rinfo = reinterpret_cast<const int32_t *>(base + pp.o_rgrp);
+            t.xrow = t.staged ? reinterpret_cast<const int32_t *>(base + pp.o_xrow) : nullptr;
+            t.wginfo = t.staged ? reinterpret_cast<const int32_t *>(base + pp.o_wg) : nullptr;
+            // (a zero 16-B source for the persistent kernel's LDS-DMA staging: the value array's padding)
+            t.zsrc = t.staged ? base + pp.o_val + pp.zoff : nullptr;
             L.tbins.push_back(t);
             continue;
         }
@@ -2994,6 +3260,12 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = getenv("VBC_TILE_X4")) h->tile_x4 = atoi(e) != 0;
         if (const char *e = getenv("VBC_TILE_ORDER")) h->tile_order = atoi(e);
         if (const char *e = getenv("VBC_TILE_BLOB")) h->tile_blob = std::max(1, atoi(e));
+        if (const char *e = getenv("VBC_TILE_STAGE")) h->tile_stage = atoi(e) < 0 ? -1 : atoi(e) != 0;
+        if (const char *e = getenv("VBC_TILE_SMAX")) h->tile_smax = std::max(1, atoi(e));
+        if (const char *e = getenv("VBC_TILE_UMAX")) h->tile_umax = std::max(1, atoi(e));
+        if (const char *e = getenv("VBC_TILE_REUSE")) h->tile_reuse = atof(e);
+        if (const char *e = getenv("VBC_TILE_WGPC")) h->tile_wgpc = std::max(1, atoi(e));
+        if (const char *e = getenv("VBC_TILE_PERSIST")) h->tile_persist = atoi(e) != 0;
         h->occ_tiles = occupancy_tiles(h->esz);
     }
 
@@ -3341,6 +3613,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
                  : h->has_mf ? (int32_t)(h->lmf.bins.size() + h->lmf.qbins.size() + h->lmf.tbins.size()) : 0;
     if ((h->has_m && !h->lm.tbins.empty()) || (h->has_mf && !h->lmf.tbins.empty()))
         info->planar_mask |= 512;  // multi-RHS buckets in the tile-granular layout (spmm_tiles)
+    for (const vbc::PanelLaunch *pl : {h->has_m ? &h->lm : nullptr, h->has_mf ? &h->lmf : nullptr})
+        if (pl)
+            for (const auto &tb : pl->tbins)
+                if (tb.staged) info->planar_mask |= 1024;  // ... in the staged-X form (spmm_tiles_x)
     if ((h->has_m && !h->lm.qbins.empty()) || (h->has_mf && !h->lmf.qbins.empty()))
         info->planar_mask |= 128;  // multi-RHS buckets in the VALU stripe-quad layout (spmm_quads)
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too

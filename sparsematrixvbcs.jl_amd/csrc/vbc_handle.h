@@ -122,6 +122,15 @@ struct vbc_handle {
     int tile_order = 0;           // VBC_TILE_ORDER: 0 natural stripe order, 1 blob order (vbc_device.hip build_tiles;
                                   // c5-mesh 305 -> 310 us dword, 334 -> 370 us 16-B form: not kept)
     int tile_blob = 512;          // VBC_TILE_BLOB: stripes per blob of the blob order
+    int tile_stage = 0;           // VBC_TILE_STAGE: staged-X tile form (spmm_tiles_x / _xp): 0 never (default: c5-mesh
+                                  // 304 us unstaged vs 302-306 staged, 388 persistent), -1 auto (when the
+                                  // clusters reuse each staged group >= tile_reuse times), 1 whenever it fits
+    int tile_smax = -1;           // VBC_TILE_SMAX: stripes per cluster of the staged-X form (auto: 48 persistent, 64)
+    int tile_umax = -1;           // VBC_TILE_UMAX: row groups staged per cluster (LDS: (U + 1) x ub x 16 elements;
+                                  // auto: 160 for the persistent kernel's double-buffered stage, 192)
+    int tile_wgpc = 2;            // VBC_TILE_WGPC: persistent workgroups per CU of the staged-X form
+    int tile_persist = 0;         // VBC_TILE_PERSIST=1: the persistent staged-X kernel (spmm_tiles_xp) when X and Y allow it
+    double tile_reuse = 2.0;      // VBC_TILE_REUSE: auto staged-X form when each staged group serves >= this many tiles
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch

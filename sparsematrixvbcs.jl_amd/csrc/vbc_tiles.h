@@ -41,6 +41,19 @@ constexpr int kTileStageBytes = 8192;        // largest LDS output stage per wav
 constexpr int kTileStripes = 32;             // default stripes per range (c5-mesh 8 / 16 / 32: 338 / 327 / 298 us)
 constexpr int kTileBatch = 8;                // default tiles per stream per pipeline stage (4 or 8: one key load per two)
 
+// Staged-X form (round 5b; TileBin::staged): one workgroup per CLUSTER of stripes that share block rows
+constexpr int kTileXInfo = 32;        // ints per cluster: {first stripe (out index), stripes, U, xrow offset,
+                                      //  4 x row stride of wave k's stream, 16 x first local stripe of stream k,
+                                      //  4 x first tile slot of wave k's segment (row 0), 4 x its length}
+constexpr uint32_t kTileXEnd = 0x40000000u;  // key bit 30: the last tile of a wave's segment of a cluster
+constexpr int kTileXStreams = 16;     // 4 waves x 4 rows of 16 lanes
+constexpr int kTileXBatch = 8;        // tiles per stream per pipeline stage
+constexpr int kTileXDepth = 4;        // stages in flight (keys and values)
+constexpr uint32_t kTileXSlot = 0xFFFFu;  // key bits 0..15: the tile's X slot in the cluster's LDS stage
+constexpr int64_t kTileXLds = 65536;      // LDS per workgroup: X stage + output stage
+constexpr int kTileXPieces = 12;          // 16-B X pieces per thread of the staging (U + 1) x ub x 16 elements
+constexpr int kTileXOutPieces = 4;        // 16-B output pieces per thread of the epilogue (stripes x w x 16 elements)
+
 // One width bucket of the tile layout (one launch per 16 right-hand sides).
 struct TileBin {
     int32_t w;            // stripe width (1..4)
@@ -58,6 +71,14 @@ struct TileBin {
     const void *val;      // per range: 4 streams x len x (ub * w) values (+ padding)
     const int32_t *rinfo; // per range: {first tile slot, len, first stripe, stripes, stream 1..3 first stripe, 0}
     const int32_t *out;   // per stripe: first y column
+    // staged-X form: nranges = clusters (one workgroup each), rinfo = kTileXInfo ints per cluster, key bits
+    // 0..15 an X slot of the cluster (slot U: the zero slot of padding), xrow = every cluster's slot base rows
+    int32_t staged;
+    int32_t xslots;       // largest U + 1 of a cluster (the LDS X stage: xslots x ub x 16 elements)
+    const int32_t *xrow;
+    int32_t nwg;          // persistent kernel (spmm_tiles_xp): workgroups, each a sequence of clusters
+    const int32_t *wginfo;  // per workgroup: {first cluster, clusters}
+    const void *zsrc;     // 16 zero bytes in device memory (the LDS-DMA source of zero pieces)
 };
 
 // v from lane N of each 16-lane row (DPP row_newbcast, gfx90a+)
@@ -544,6 +565,448 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles4(const TileBin b, co
                 if (rd) o = fmadd(beta, *yo, o);
                 *yo = o;
             }
+        }
+    }
+}
+
+// Staged-X form (round 5b, TileBin::staged).  The unit of scheduling is a CLUSTER of stripes that gather the
+// same X block rows (a compact ball of the stripe graph: a 3D operator's neighbouring nodes), one workgroup
+// each.  A node's X block row is used by every stripe coupled to it -- ~16 tiles on the c5-mesh operator --
+// and a cluster of ~50 neighbouring stripes gathers each of its U distinct block rows ~4 times, so:
+//   * phase 1: the workgroup loads the cluster's U block rows (ub x 16 right-hand sides each, slot order =
+//     ascending row) into LDS with full-line 16-B loads, plus one zero slot (U) for padding tiles;
+//   * phase 2: 16 streams (4 waves x 4 rows of 16 lanes; lane j = right-hand side j) walk the cluster's
+//     tiles, each tile's block read with ub ds_read_b32 from its slot (key bits 0..15) instead of ub
+//     global gathers, the values streamed and DPP-broadcast exactly as spmm_tiles (the same fma chain per
+//     column, so every column equals the reference's product bit for bit, multiply_VBC.jl:126-135);
+//     keys and values run kTileXDepth batches ahead (no X registers to hold: the gathers are LDS reads);
+//   * a LAST tile parks the stripe's w x 16 sums in the workgroup's output stage, written after a barrier.
+// X4: 16 contiguous right-hand sides in 16-B aligned rows (16-B staging loads); else element loads.
+template <typename T, int UB, int W, bool MASKU, bool X4>
+__global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, const T *__restrict__ X, int64_t sxr,
+                                                              int64_t sxc, int64_t xrows, T *__restrict__ Y, int64_t syr,
+                                                              int64_t syc, int nrhs, T alpha, T beta, int rd_i, int fast)
+{
+    constexpr int NB = kTileXBatch, D = kTileXDepth;
+    constexpr int TV = UB * W;
+    constexpr int EPL = 16 / (int)sizeof(T);  // elements per 16-B piece
+    constexpr int PER = 16 * EPL;             // elements per value load of a 16-lane row
+    constexpr int NV = (NB * TV + PER - 1) / PER;
+    constexpr int PPR = 16 / EPL;             // 16-B pieces per X row of 16 right-hand sides
+    typedef T tv __attribute__((ext_vector_type(EPL)));
+    extern __shared__ __attribute__((aligned(16))) char tile_stage[];
+    const int cl = xcd_block(blockIdx.x, gridDim.x);
+    if (cl >= b.nranges) return;  // (the whole workgroup)
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, j = lane & 15;
+    // the cluster's info through the scalar cache (constant address space: uniform s_load)
+    typedef __attribute__((address_space(4))) const int32_t *cptr;
+    const cptr ci = (cptr)b.rinfo + (size_t)cl * kTileXInfo;
+    const int s0 = __builtin_amdgcn_readfirstlane(ci[0]), ns = __builtin_amdgcn_readfirstlane(ci[1]);
+    const int U = __builtin_amdgcn_readfirstlane(ci[2]), xo = __builtin_amdgcn_readfirstlane(ci[3]);
+    // the wave's segment of the cluster: its own length (the longest of its 4 rows' streams, whole batches);
+    // the rows of a wave are strided by the wave's whole stream (the persistent layout, spmm_tiles_xp)
+    const int tile0 = __builtin_amdgcn_readfirstlane(ci[24 + wv]), len = __builtin_amdgcn_readfirstlane(ci[28 + wv]);
+    const int rstride = __builtin_amdgcn_readfirstlane(ci[4 + wv]);
+    const int stream = wv * 4 + g;
+    int sidx = G(b.rinfo)[(size_t)cl * kTileXInfo + 8 + stream];  // cluster-local index of this row's first stripe
+                                                                  // (a stream's stripes are consecutive)
+    const int64_t kb = (int64_t)tile0 + (int64_t)g * rstride;
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    T *xl = reinterpret_cast<T *>(tile_stage);
+    T *st = reinterpret_cast<T *>(tile_stage + (size_t)b.xslots * UB * 16 * sizeof(T));
+    const T zero = T(0);
+
+    // keys and values of the first D batches first: their latency overlaps the X stage
+    auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < NB ? j : NB - 1)]; };
+    auto load_vals = [&](int t0, tv (&V)[NV]) {
+        const gptr<const T> p = val + (kb + t0) * TV + j * EPL;
+#pragma unroll
+        for (int v = 0; v < NV; v++) V[v] = __builtin_nontemporal_load((gptr<const tv>)(p + v * PER));
+    };
+    uint32_t K[D];
+    tv V[D][NV];
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        K[d] = load_keys(d * NB);
+        load_vals(d * NB, V[d]);
+    }
+    // the output columns of this thread's output pieces (the epilogue's), loaded now so that no round trip
+    // follows the loop: piece p = tid + k * 256 of the ns x W x PPR pieces belongs to stripe p / (W * PPR)
+    const gptr<const int32_t> outp = G(b.out) + s0;
+    int ocol[kTileXOutPieces];
+#pragma unroll
+    for (int k = 0; k < kTileXOutPieces; k++) ocol[k] = outp[min((tid + k * kBlockThreads) / (W * PPR), max(ns - 1, 0))];
+
+    // phase 1: the cluster's X block rows -> LDS [slot][r][16], slot U (and rows past X) zero.  Every load of
+    // a thread is issued before the first LDS write, with clamped addresses and selects instead of branches
+    // (a load inside a branch makes the compiler wait for every load in flight, the prefetched values
+    // included): one round trip for the slots' rows, one for the stage.  At most kTileXPieces 16-B pieces
+    // per thread (the builder caps U to fit).
+    if (!(b.diag & 1)) {  // (diag 1: no staging -- an ablation, tools/ab.py)
+        constexpr int MP = kTileXPieces;
+        const gptr<const int32_t> xr = G(b.xrow) + xo;  // (xrow carries one entry past the last cluster's)
+        if constexpr (X4) {
+            const int np = (U + 1) * UB * PPR;
+            int row[MP];
+#pragma unroll
+            for (int u = 0; u < MP; u++) {
+                const int p = tid + u * kBlockThreads;
+                const int slot = min(p / (UB * PPR), U);
+                const int rr = (p - slot * (UB * PPR)) / PPR;
+                const int r0 = xr[slot] + rr;
+                row[u] = ((p < np) & (slot < U) & (r0 < xrows)) ? r0 : -1;
+            }
+            tv v[MP];
+#pragma unroll
+            for (int u = 0; u < MP; u++) {
+                const int p = tid + u * kBlockThreads;
+                const tv t = *(gptr<const tv>)(G(X) + (int64_t)max(row[u], 0) * sxr + (p % PPR) * EPL);
+                v[u] = row[u] >= 0 ? t : tv{};
+            }
+#pragma unroll
+            for (int u = 0; u < MP; u++) {
+                const int p = tid + u * kBlockThreads;
+                // piece p of the stage is elements p * EPL .. p * EPL + EPL - 1: (slot, row r, RHS group q)
+                if (p < np) *reinterpret_cast<tv *>(xl + p * EPL) = v[u];
+            }
+        } else {
+            const int ne = (U + 1) * UB * 16;
+            for (int e0 = 0; e0 < ne; e0 += MP * kBlockThreads) {
+                int row[MP];
+#pragma unroll
+                for (int u = 0; u < MP; u++) {
+                    const int e = e0 + tid + u * kBlockThreads;
+                    const int slot = min(e / (UB * 16), U);
+                    const int r0 = xr[slot] + (e >> 4) - slot * UB;
+                    row[u] = ((e < ne) & (slot < U) & (r0 < xrows) & ((e & 15) < nrhs)) ? r0 : -1;
+                }
+                T v[MP];
+#pragma unroll
+                for (int u = 0; u < MP; u++) {
+                    const int jj = (e0 + tid + u * kBlockThreads) & 15;
+                    const T t = G(X)[(int64_t)max(row[u], 0) * sxr + (int64_t)(row[u] >= 0 ? jj : 0) * sxc];
+                    v[u] = row[u] >= 0 ? t : zero;
+                }
+#pragma unroll
+                for (int u = 0; u < MP; u++)
+                    if (e0 + tid + u * kBlockThreads < ne) xl[e0 + tid + u * kBlockThreads] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+
+    T acc[W];
+#pragma unroll
+    for (int c = 0; c < W; c++) acc[c] = zero;
+    // per batch: bit 16 g + s of `lastm` = LAST of step s of row g (lanes s >= NB hold copies, never tested)
+    auto fold = [&](uint32_t Kk, const tv (&Vv)[NV]) {
+        const uint64_t lastm = __builtin_amdgcn_ballot_w64((Kk & kTileLast) != 0);
+        T xs[NB][UB];
+#pragma unroll
+        for (int s = 0; s < NB; s++) {
+            const uint32_t ks = (uint32_t)row_bcast_rt((int)Kk, s);
+            const T *xp = xl + (ks & kTileXSlot) * (UB * 16) + j;
+#pragma unroll
+            for (int r = 0; r < UB; r++) {
+                xs[s][r] = xp[r * 16];
+                // a slot row the tile does not store: x taken as 0 (its values are 0), as in spmm_tiles
+                if constexpr (MASKU) xs[s][r] = ((ks >> (kTileMaskShift + r)) & 1) ? xs[s][r] : zero;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NB; s++) {
+#pragma unroll
+            for (int r = 0; r < UB; r++) {
+#pragma unroll
+                for (int c = 0; c < W; c++) {
+                    const int f = s * TV + r * W + c;
+                    fmac_bcast_rt(acc[c], Vv[f / PER][f % EPL], xs[s][r], (f % PER) / EPL);
+                }
+            }
+            if ((lastm >> s) & 0x0001000100010001ull) {
+                const bool last = ((lastm >> (16 * g + s)) & 1) != 0;
+                if (last) {
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        st[(sidx * W + c) * 16 + j] = acc[c];
+                        acc[c] = zero;
+                    }
+                }
+                sidx += last ? 1 : 0;
+            }
+        }
+    };
+    // phase 2: batch t0 + d NB from ring slot d, refilled with batch t0 + (d + D) NB (streams are padded to
+    // whole batches; the loads past a stream's end read the next stream or the layout's padding, unused)
+    for (int t0 = 0; t0 < len; t0 += D * NB) {
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            // (the refill is unconditional: a load inside the branch would make every later fold wait for
+            // all loads in flight; past the stream's end it reads the next stream or the padding, unused)
+            __builtin_amdgcn_sched_barrier(0);
+            if (t0 + d * NB < len) fold(K[d], V[d]);
+            __builtin_amdgcn_sched_barrier(0);
+            K[d] = load_keys(t0 + (d + D) * NB);
+            load_vals(t0 + (d + D) * NB, V[d]);
+        }
+    }
+    __syncthreads();
+
+    // the cluster's outputs: stripe i (cluster-local) -> columns out[s0 + i] .. + W - 1
+    const bool rd = rd_i != 0;
+    if (b.diag & 2) return;  // (diag 2: no output stores -- an ablation)
+    if (fast) {  // Y row-major with 16 contiguous right-hand sides: a stripe's W x 16 block is contiguous
+        const int np = ns * W * PPR;  // (<= kTileXOutPieces x 256: the builder caps the stripes per cluster)
+#pragma unroll
+        for (int k = 0; k < kTileXOutPieces; k++) {
+            const int p = tid + k * kBlockThreads;
+            if (p >= np) break;
+            const int i = p / (W * PPR), rem = p - i * (W * PPR);
+            gptr<T> yo = G(Y) + (int64_t)((b.diag & 4) ? (s0 + i) * W : ocol[k]) * 16 + rem * EPL;  // (diag 4: contiguous)
+            const tv v = *reinterpret_cast<const tv *>(st + i * W * 16 + rem * EPL);
+            tv o;
+#pragma unroll
+            for (int q = 0; q < EPL; q++) o[q] = alpha * v[q];
+            if (rd) {
+                const tv y0 = *(gptr<const tv>)yo;
+#pragma unroll
+                for (int q = 0; q < EPL; q++) o[q] = fmadd(beta, y0[q], o[q]);
+            }
+            *(gptr<tv>)yo = o;
+        }
+    } else {
+        const int total = ns * W * 16;
+        for (int e = tid; e < total; e += kBlockThreads) {
+            const int i = e / (W * 16), rem = e - i * (W * 16), c = rem >> 4, jj = rem & 15;
+            if (jj >= nrhs) continue;
+            gptr<T> yo = G(Y) + ((int64_t)outp[i] + c) * syr + (int64_t)jj * syc;
+            T o = alpha * st[e];
+            if (rd) o = fmadd(beta, *yo, o);
+            *yo = o;
+        }
+    }
+}
+
+// Persistent staged-X form (round 5b, spmm_tiles_xp; fp32, 16 contiguous right-hand sides in X and Y).  The
+// per-workgroup costs of spmm_tiles_x -- dispatch, the chain cluster info -> row groups -> X -> LDS before the
+// first tile, the output stores draining at the end (c5-mesh ablations: staging 60 us, stores 58 us of 303) --
+// are taken off the compute waves:
+//   * one workgroup per resident slot (TileBin::nwg) walks a sequence of clusters (wginfo); its 4 compute waves
+//     each read ONE continuous stream per row (the clusters' segments back to back), so the keys and values run
+//     kTileXDepth batches ahead across cluster boundaries;
+//   * a stager wave fills the other half of a double-buffered LDS X stage with the next cluster's row groups
+//     (LDS-DMA, global_load_lds_dwordx4: no registers, all pieces in flight at once) while the compute waves
+//     fold the current cluster;
+//   * a writer wave stores the previous cluster's outputs from the other half of a double-buffered output stage;
+//   * the END key bit (the last tile of a wave's segment) closes a cluster: one barrier of all six waves, then
+//     both halves swap.  Every wave passes 1 + K barriers.
+// Each column keeps the reference's fma chain per stripe (the fold is spmm_tiles_x's): bit for bit.
+// A workgroup barrier that orders LDS only: __syncthreads()'s workgroup fence would also wait for every
+// global load in flight (vmcnt(0): the compute waves' value prefetch, drained at each cluster boundary).
+// The LDS-DMA stage is waited for by the stager itself (vmcnt(0)) before it joins the barrier.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+constexpr int kTileXPWaves = 6;                         // 4 compute, 1 stager, 1 writer
+constexpr int64_t kTileXPLds = 160 * 1024 - 1024;       // LDS of the CU shared by the persistent workgroups
+constexpr int kTileXPThreads = kTileXPWaves * 64;
+constexpr int kTileXPLoad = 32;                         // 16-B X pieces per stager lane per cluster (at most)
+constexpr int kTileXPOut = 24;                          // 16-B output pieces per writer lane per cluster
+template <int UB, int W, bool MASKU>
+__global__ __launch_bounds__(kTileXPThreads) void spmm_tiles_xp(const TileBin b, const float *__restrict__ X, int64_t sxr,
+                                                                int64_t xrows, float *__restrict__ Y, float alpha,
+                                                                float beta, int rd_i)
+{
+    typedef float T;
+    constexpr int NB = kTileXBatch, D = kTileXDepth;
+    constexpr int TV = UB * W;
+    constexpr int EPL = 4, PER = 64, PPR = 4;
+    constexpr int NV = (NB * TV + PER - 1) / PER;
+    typedef float tv __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(4))) const int32_t *cptr;
+    extern __shared__ __attribute__((aligned(16))) char tile_stage[];
+    const int xfl = b.xslots * UB * 16;          // floats per X half
+    const int sfl = b.stage_bytes / 4;           // floats per output half
+    T *xbuf = reinterpret_cast<T *>(tile_stage);
+    T *sbuf = xbuf + 2 * xfl;
+    int *sinfo = reinterpret_cast<int *>(sbuf + 2 * sfl);  // [2][16]: first local stripe of each stream
+    const int L = xcd_block(blockIdx.x, gridDim.x);
+    const cptr wg = (cptr)b.wginfo + 2 * L;
+    const int c0 = wg[0], K = wg[1];
+    if (K == 0) return;  // (the whole workgroup)
+    const cptr cinfo = (cptr)b.rinfo;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+
+    if (wv == 4) {  // ---- stager
+        // rows of cluster c's pieces p = i * 64 + lane (-1: a zero piece), loaded one cluster ahead of its DMA
+        auto load_rows = [&](int c, int (&row)[kTileXPLoad]) {
+            const cptr ci = cinfo + (size_t)c * kTileXInfo;
+            const int U = ci[2];
+            const gptr<const int32_t> xr = G(b.xrow) + ci[3];
+#pragma unroll
+            for (int i = 0; i < kTileXPLoad; i++) {
+                const int p = i * 64 + lane;
+                const int slot = min(p / (UB * PPR), U);
+                const int r0 = xr[slot] + (p - slot * (UB * PPR)) / PPR;
+                // (bitwise &, not &&: a short-circuit test becomes a branch, the load is sunk into it and waited
+                // for on the spot, one round trip per piece)
+                const bool ok = (slot < U) & (r0 < xrows);
+                row[i] = ok ? r0 : -1;
+            }
+        };
+        auto dma = [&](int c, int half, const int (&row)[kTileXPLoad]) {
+            const cptr ci = cinfo + (size_t)c * kTileXInfo;
+            const int np = (ci[2] + 1) * UB * PPR;
+            if (lane < kTileXStreams) sinfo[half * kTileXStreams + lane] = G(b.rinfo)[(size_t)c * kTileXInfo + 8 + lane];
+            // LDS byte address of this half (M0 of the DMA: lane l of piece round i lands at M0 + l * 16)
+            const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(xbuf + half * xfl);
+#pragma unroll
+            for (int i = 0; i < kTileXPLoad; i++) {
+                const int p = i * 64 + lane;
+                if (i * 64 < np) {  // (uniform)
+                    const void *src = (row[i] >= 0 && p < np) ? (const void *)(X + (int64_t)row[i] * sxr + (p % PPR) * EPL) : b.zsrc;
+                    // inline asm: the compiler's own LDS-DMA tracking waited for each piece before issuing the
+                    // next (vmcnt(0)); the stager waits once for all of them before the cluster barrier.  Lanes
+                    // past np are exec-masked off (the DMA writes only active lanes' pieces).
+                    if (p < np)
+                        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                                     :: "s"(dst + (uint32_t)i * 1024u), "v"(src) : "memory");
+                }
+            }
+        };
+        int row[kTileXPLoad];
+        load_rows(c0, row);
+        dma(c0, 0, row);
+        if (K > 1) load_rows(c0 + 1, row);
+        __builtin_amdgcn_s_waitcnt(0);
+        lds_barrier();
+        for (int k = 0; k < K; k++) {
+            if (k + 1 < K) {
+                dma(c0 + k + 1, (k + 1) & 1, row);        // (addresses read at issue)
+                if (k + 2 < K) load_rows(c0 + k + 2, row);  // in flight with the DMA: one round trip per cluster
+            }
+            __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA pieces landed)
+            lds_barrier();  // cluster k done; cluster k + 1's stage in place
+        }
+        return;
+    }
+    if (wv == 5) {  // ---- writer
+        const bool rd = rd_i != 0;
+        lds_barrier();
+        for (int k = 0; k < K; k++) {
+            const cptr ci = cinfo + (size_t)(c0 + k) * kTileXInfo;
+            const int s0 = ci[0], ns = ci[1];
+            const int np = ns * W * PPR;
+            const gptr<const int32_t> outp = G(b.out) + s0;
+            int ocol[kTileXPOut];
+#pragma unroll
+            for (int i = 0; i < kTileXPOut; i++) ocol[i] = outp[min((i * 64 + lane) / (W * PPR), max(ns - 1, 0))];
+            lds_barrier();  // cluster k's sums in output half k & 1
+            const T *st = sbuf + (k & 1) * sfl;
+#pragma unroll
+            for (int i = 0; i < kTileXPOut; i++) {
+                const int p = i * 64 + lane;
+                if (i * 64 >= np) break;  // (uniform)
+                if (p < np) {
+                    const int si = p / (W * PPR), rem = p - si * (W * PPR);
+                    gptr<T> yo = G(Y) + (int64_t)ocol[i] * 16 + rem * EPL;
+                    const tv v = *reinterpret_cast<const tv *>(st + si * W * 16 + rem * EPL);
+                    tv o;
+#pragma unroll
+                    for (int q = 0; q < EPL; q++) o[q] = alpha * v[q];
+                    if (rd) {
+                        const tv y0 = *(gptr<const tv>)yo;
+#pragma unroll
+                        for (int q = 0; q < EPL; q++) o[q] = fmadd(beta, y0[q], o[q]);
+                    }
+                    *(gptr<tv>)yo = o;
+                }
+            }
+        }
+        return;
+    }
+    // ---- compute waves
+    const int g = lane >> 4, j = lane & 15, stream = wv * 4 + g;
+    const cptr ci0 = cinfo + (size_t)c0 * kTileXInfo;
+    const int len = ci0[4 + wv];  // the wave's whole stream (its segments of the K clusters)
+    const int64_t kb = (int64_t)ci0[24 + wv] + (int64_t)g * len;
+    const gptr<const uint32_t> key = G(b.key);
+    const gptr<const T> val = G(static_cast<const T *>(b.val));
+    const T zero = T(0);
+    auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < NB ? j : NB - 1)]; };
+    auto load_vals = [&](int t0, tv (&V)[NV]) {
+        const gptr<const T> p = val + (kb + t0) * TV + j * EPL;
+#pragma unroll
+        for (int v = 0; v < NV; v++) V[v] = __builtin_nontemporal_load((gptr<const tv>)(p + v * PER));
+    };
+    uint32_t Kr[D];
+    tv V[D][NV];
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        Kr[d] = load_keys(d * NB);
+        load_vals(d * NB, V[d]);
+    }
+    lds_barrier();  // cluster 0's stage in place
+    int half = 0;
+    int sidx = sinfo[stream];
+    T acc[W];
+#pragma unroll
+    for (int c = 0; c < W; c++) acc[c] = zero;
+    auto fold = [&](uint32_t Kk, const tv (&Vv)[NV]) {
+        const T *xl = xbuf + half * xfl;
+        T *st = sbuf + half * sfl;
+        const uint64_t lastm = __builtin_amdgcn_ballot_w64((Kk & kTileLast) != 0);
+        T xs[NB][UB];
+#pragma unroll
+        for (int s = 0; s < NB; s++) {
+            const uint32_t ks = (uint32_t)row_bcast_rt((int)Kk, s);
+            const T *xp = xl + (ks & kTileXSlot) * (UB * 16) + j;
+#pragma unroll
+            for (int r = 0; r < UB; r++) {
+                xs[s][r] = xp[r * 16];
+                if constexpr (MASKU) xs[s][r] = ((ks >> (kTileMaskShift + r)) & 1) ? xs[s][r] : zero;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NB; s++) {
+#pragma unroll
+            for (int r = 0; r < UB; r++) {
+#pragma unroll
+                for (int c = 0; c < W; c++) {
+                    const int f = s * TV + r * W + c;
+                    fmac_bcast_rt(acc[c], Vv[f / PER][f % EPL], xs[s][r], (f % PER) / EPL);
+                }
+            }
+            if ((lastm >> s) & 0x0001000100010001ull) {
+                const bool last = ((lastm >> (16 * g + s)) & 1) != 0;
+                if (last) {
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        st[(sidx * W + c) * 16 + j] = acc[c];
+                        acc[c] = zero;
+                    }
+                }
+                sidx += last ? 1 : 0;
+            }
+        }
+        // the segment's last batch (every row of every compute wave has END at step NB - 1 of it)
+        const uint32_t ke = (uint32_t)__builtin_amdgcn_readfirstlane(row_bcast_i<NB - 1>((int)Kk));
+        if (ke & kTileXEnd) {
+            lds_barrier();  // every wave done with this cluster; the next one's stage in place
+            half ^= 1;
+            sidx = sinfo[half * kTileXStreams + stream];
+        }
+    };
+    for (int t0 = 0; t0 < len; t0 += D * NB) {
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (t0 + d * NB < len) fold(Kr[d], V[d]);
+            __builtin_amdgcn_sched_barrier(0);
+            Kr[d] = load_keys(t0 + (d + D) * NB);
+            load_vals(t0 + (d + D) * NB, V[d]);
         }
     }
 }

@@ -80,6 +80,73 @@ static void launch_tiles_u(const TileBin &tb, int grid, hipStream_t s, const T *
     }
 }
 
+// the persistent staged-X form (spmm_tiles_xp): nwg workgroups of 6 waves, both LDS stages double-buffered
+static size_t tiles_xp_lds(const TileBin &tb)
+{
+    return 2 * (size_t)tb.xslots * tb.ub * 16 * sizeof(float) + 2 * (size_t)tb.stage_bytes + 2 * kTileXStreams * sizeof(int);
+}
+template <int UB, int W>
+static void launch_tiles_xp_uw(const TileBin &tb, hipStream_t s, const float *xs, int64_t sxr, int64_t xrows, float *ys,
+                               float alpha, float beta, int rd)
+{
+    const size_t lds = tiles_xp_lds(tb);
+    static bool attr[2] = {false, false};  // dynamic LDS above 64 KB: raised once per instantiation
+    if (!attr[tb.masku ? 1 : 0]) {
+        if (tb.masku) (void)hipFuncSetAttribute(reinterpret_cast<const void *>(spmm_tiles_xp<UB, W, true>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTileXPLds);
+        else (void)hipFuncSetAttribute(reinterpret_cast<const void *>(spmm_tiles_xp<UB, W, false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTileXPLds);
+        attr[tb.masku ? 1 : 0] = true;
+    }
+    if (tb.masku)
+        hipLaunchKernelGGL((spmm_tiles_xp<UB, W, true>), dim3(tb.nwg), dim3(kTileXPThreads), lds, s, tb, xs, sxr, xrows, ys,
+                           alpha, beta, rd);
+    else
+        hipLaunchKernelGGL((spmm_tiles_xp<UB, W, false>), dim3(tb.nwg), dim3(kTileXPThreads), lds, s, tb, xs, sxr, xrows, ys,
+                           alpha, beta, rd);
+}
+template <int UB>
+static void launch_tiles_xp_u(const TileBin &tb, hipStream_t s, const float *xs, int64_t sxr, int64_t xrows, float *ys,
+                              float alpha, float beta, int rd)
+{
+    switch (tb.w) {
+    case 1: launch_tiles_xp_uw<UB, 1>(tb, s, xs, sxr, xrows, ys, alpha, beta, rd); break;
+    case 2: launch_tiles_xp_uw<UB, 2>(tb, s, xs, sxr, xrows, ys, alpha, beta, rd); break;
+    case 3: launch_tiles_xp_uw<UB, 3>(tb, s, xs, sxr, xrows, ys, alpha, beta, rd); break;
+    default: launch_tiles_xp_uw<UB, 4>(tb, s, xs, sxr, xrows, ys, alpha, beta, rd); break;
+    }
+}
+
+// the staged-X form (spmm_tiles_x): one workgroup per cluster, LDS = X stage + output stage
+template <typename T, int UB, int W>
+static void launch_tiles_x_uw(const TileBin &tb, hipStream_t s, const T *xs, int64_t sxr, int64_t sxc, int64_t xrows,
+                              bool x4, T *ys, int64_t syr, int64_t syc, int nr, T alpha, T beta, int rd, int fast)
+{
+    const size_t lds = (size_t)tb.xslots * UB * 16 * sizeof(T) + (size_t)tb.stage_bytes;
+#define VBC_TILESX(MASKU, X4)                                                                                      \
+    hipLaunchKernelGGL((spmm_tiles_x<T, UB, W, MASKU, X4>), dim3(tb.nranges), dim3(kBlockThreads), lds, s, tb, xs, \
+                       sxr, sxc, xrows, ys, syr, syc, nr, alpha, beta, rd, fast)
+    if (tb.masku) {
+        if (x4) VBC_TILESX(true, true);
+        else VBC_TILESX(true, false);
+    } else {
+        if (x4) VBC_TILESX(false, true);
+        else VBC_TILESX(false, false);
+    }
+#undef VBC_TILESX
+}
+template <typename T, int UB>
+static void launch_tiles_x_u(const TileBin &tb, hipStream_t s, const T *xs, int64_t sxr, int64_t sxc, int64_t xrows,
+                             bool x4, T *ys, int64_t syr, int64_t syc, int nr, T alpha, T beta, int rd, int fast)
+{
+    switch (tb.w) {
+    case 1: launch_tiles_x_uw<T, UB, 1>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, alpha, beta, rd, fast); break;
+    case 2: launch_tiles_x_uw<T, UB, 2>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, alpha, beta, rd, fast); break;
+    case 3: launch_tiles_x_uw<T, UB, 3>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, alpha, beta, rd, fast); break;
+    default: launch_tiles_x_uw<T, UB, 4>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, alpha, beta, rd, fast); break;
+    }
+}
+
 // Y = alpha op(B) X + beta Y for the tile buckets of L (the other buckets are the panel kernel's): per
 // 16 right-hand sides one launch per bucket.  xrows: rows of X (m for B'X, n for B·X on Bᵀ's layout).
 template <typename T>
@@ -104,6 +171,33 @@ static int mulmat_tiles(const vbc_handle *h, const PanelLaunch &L, int64_t nrhs,
         const uint32_t xb = (uint32_t)std::min<int64_t>(span, lim - 1);
         for (const TileBin &tb : L.tbins) {
             if (tb.nranges == 0) continue;
+            if (tb.staged) {
+                const bool x4 = nr == 16 && sxc == 1 && (sxr * (int64_t)sizeof(T)) % 16 == 0 &&
+                                reinterpret_cast<uintptr_t>(xs) % 16 == 0;
+                const int fastx = nr == 16 && syc == 1 && syr == 16 && reinterpret_cast<uintptr_t>(ys) % 16 == 0;
+                if constexpr (sizeof(T) == 4) {
+                    if (h->tile_persist && x4 && fastx && tb.nwg > 0 && tiles_xp_lds(tb) <= (size_t)kTileXPLds) {
+                        const float *xf = reinterpret_cast<const float *>(xs);
+                        float *yf = reinterpret_cast<float *>(ys);
+                        switch (tb.ub) {
+                        case 1: launch_tiles_xp_u<1>(tb, s, xf, sxr, xrows, yf, (float)alpha, (float)beta, rd); break;
+                        case 2: launch_tiles_xp_u<2>(tb, s, xf, sxr, xrows, yf, (float)alpha, (float)beta, rd); break;
+                        case 3: launch_tiles_xp_u<3>(tb, s, xf, sxr, xrows, yf, (float)alpha, (float)beta, rd); break;
+                        default: launch_tiles_xp_u<4>(tb, s, xf, sxr, xrows, yf, (float)alpha, (float)beta, rd); break;
+                        }
+                        VBC_HIP(hipGetLastError());
+                        continue;
+                    }
+                }
+                switch (tb.ub) {
+                case 1: launch_tiles_x_u<T, 1>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fastx); break;
+                case 2: launch_tiles_x_u<T, 2>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fastx); break;
+                case 3: launch_tiles_x_u<T, 3>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fastx); break;
+                default: launch_tiles_x_u<T, 4>(tb, s, xs, sxr, sxc, xrows, x4, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fastx); break;
+                }
+                VBC_HIP(hipGetLastError());
+                continue;
+            }
             // one contiguous run of Y per range: affine map of stride w, 16 contiguous right-hand sides
             const int fast = tb.out_affine && tb.out_stride == tb.w && nr == 16 && syc == 1 && syr == 16 &&
                              reinterpret_cast<uintptr_t>(ys) % 16 == 0;

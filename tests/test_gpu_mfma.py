@@ -18,16 +18,21 @@ DEV = "cuda:0"
 TOL64, TOL32 = 1e-12, 1e-5
 
 
-@pytest.fixture(autouse=True, params=["tiles", "8", "0"], ids=["tiles", "quads", "panels"])
+@pytest.fixture(autouse=True, params=["staged", "tiles", "8", "0"], ids=["staged", "tiles", "quads", "panels"])
 def multi_layout(request, monkeypatch):
     """Every test on the three multi-RHS layouts: every width on the MFMA panels (VBC_PANEL_QUADS=0,
     VBC_PANEL_TILES=0); stripes of width <= 8 in the VALU stripe-quad layout (VBC_PANEL_QUADS=8; spmm_quads,
     measured slower on both C5 inputs, kept as the A/B alternative); and (round 5) every bucket of width <= 4
     whose tiles are <= 4 rows in the tile-granular layout (VBC_PANEL_TILES=1, spmm_tiles -- the default
-    for such buckets when their rows come in tiles)."""
-    if request.param == "tiles":
+    for such buckets when their rows come in tiles); and (round 5b) the same buckets in the staged-X form
+    (VBC_TILE_STAGE=1, spmm_tiles_x: clusters of stripes sharing row groups, the groups staged in LDS -- the
+    default when the clusters reuse each staged group >= 2 times)."""
+    if request.param in ("tiles", "staged"):
         monkeypatch.setenv("VBC_PANEL_TILES", "1")
         monkeypatch.setenv("VBC_PANEL_QUADS", "0")
+        monkeypatch.setenv("VBC_TILE_STAGE", "1" if request.param == "staged" else "0")
+        # (staged: fp32 products with 16 contiguous right-hand sides run the persistent kernel spmm_tiles_xp)
+        monkeypatch.setenv("VBC_TILE_PERSIST", "1" if request.param == "staged" else "0")
     else:
         monkeypatch.setenv("VBC_PANEL_TILES", "0")
         monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
@@ -260,9 +265,10 @@ def test_tiles_mixed_heights_widths_every_column(dtype, multi_layout):
     tol = TOL64 if dtype == np.float64 else TOL32
     B = _vbc2d_mixed_heights(rng, 300, 400, 1200, (3, 1, 4, 2, 3), (1, 3, 2, 4, 3), dtype)
     assert (np.diff(B.pos) == 0).any()
-    if multi_layout == "tiles":
+    if multi_layout in ("tiles", "staged"):
         assert B.info(multi=True)["planar_mask"] & 512
         assert B.info(trans=False, multi=True)["planar_mask"] & 512
+        assert bool(B.info(multi=True)["planar_mask"] & 1024) == (multi_layout == "staged")
     R = ref_2d(B)
     for nrhs in (5, 16, 21):
         for layout in ("R", "C"):
@@ -304,7 +310,7 @@ def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
     val = np.zeros(nv + 8)
     val[:nv] = rng.integers(-8, 9, nv)
     B = V.SparseMatrix1DVBC(8, 3 * N, int(spl[-1] - 1), V.SplitPartition(spl), pos, np.concatenate(rows) + 1, ofs, val)
-    if multi_layout == "tiles":
+    if multi_layout in ("tiles", "staged"):
         assert B.info(multi=True)["planar_mask"] & 512
     R = ref_1d(B)
     X = rng.integers(-8, 9, (B.m, 16)).astype(np.float64)
@@ -321,3 +327,43 @@ def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
     assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isinf(got), np.isinf(ref))
     fin = np.isfinite(ref)
     assert np.array_equal(got[fin], ref[fin])
+
+
+@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("smax,umax", [(3, 40), (7, 64), (64, 192)])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, persist, multi_layout, monkeypatch):
+    """Staged-X tile form (spmm_tiles_x; with persist "1" and fp32 the persistent spmm_tiles_xp: workgroups walking
+    sequences of clusters, stager / writer waves, double-buffered LDS) on the structured C5 input at small scale:
+    clusters cut by the stripe cap or by the LDS stage (VBC_TILE_SMAX / VBC_TILE_UMAX), 16 row-major right-hand
+    sides, both directions
+    (B·X on Bᵀ's tiles): integer data, so every column equals the oracle bit for bit (each column is the
+    reference's fma chain, multiply_VBC.jl:126-135); then random data with alpha / beta, 7 right-hand sides,
+    column-major operands (the element staging path)."""
+    if multi_layout != "staged":
+        pytest.skip("staged-X form only")
+    monkeypatch.setenv("VBC_TILE_SMAX", str(smax))
+    monkeypatch.setenv("VBC_TILE_UMAX", str(umax))
+    monkeypatch.setenv("VBC_TILE_PERSIST", persist)  # fp32 x 16 row-major RHS: the persistent kernel when "1"
+    import bench
+    B = bench.build_matrix("c5-mesh", dtype, 0.002)
+    B.val[:] = np.random.default_rng(3).integers(-8, 9, B.val.shape)
+    assert B.info(multi=True)["planar_mask"] & 1024 and B.info(trans=False, multi=True)["planar_mask"] & 1024
+    Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    rng = np.random.default_rng(smax)
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        X = rng.integers(-8, 9, (nx, 16)).astype(dtype)
+        Y = torch.full((ny, 16), float("nan"), dtype=torch.float32 if dtype == np.float32 else torch.float64, device=DEV)
+        V.mul_(Y, B.T if trans else B, torch.from_numpy(X).to(DEV), engine="mfma")
+        want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64), np.zeros(ny), trans=trans)
+                         for j in range(16)], axis=1)
+        assert np.array_equal(Y.cpu().numpy(), want.astype(dtype)), trans
+        X = rng.uniform(-1, 1, (nx, 7)).astype(dtype)
+        Y0 = rng.uniform(-1, 1, (ny, 7)).astype(dtype)
+        Yd = as_dev(Y0, "C")
+        V.mul_(Yd, B.T if trans else B, as_dev(X, "C"), 0.5, -1.25, engine="mfma")
+        want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64),
+                               np.ascontiguousarray(Y0[:, j], dtype=np.float64), 0.5, -1.25, trans=trans,
+                               ref_semantics=False) for j in range(7)], axis=1)
+        assert rel(Yd.cpu().numpy(), want) <= (TOL64 if dtype == np.float64 else TOL32), trans
