@@ -2205,19 +2205,24 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
     // Auto (tile_stage < 0): only when the clusters gather each staged group >= tile_reuse times.
     if (h->tile_stage != 0) {
         constexpr int NB = kTileXBatch, D = kTileXDepth;
-        // fp32: the persistent kernel (spmm_tiles_xp) double-buffers both LDS stages, so its clusters are smaller
+        // fp32: the persistent kernel (spmm_tiles_xp) double-buffers both LDS stages, so its clusters are smaller;
+        // else (spmm_tiles_x) fp32 clusters are run by 8 compute waves (two 80 KB workgroups per CU), fp64 by 4
         const bool persist = h->tile_persist && esz == 4;
+        const int NWv = persist || esz != 4 ? 4 : std::max(4, std::min(kTileXMaxWaves, h->tile_waves)) / 4 * 4;
+        const int NS = 4 * NWv, NT = 64 * NWv;
+        const int64_t ldscap = NWv == 8 ? kTileXLds8 : kTileXLds;
         // stripes per cluster: the kernels' epilogues hold kTileXOutPieces 16-B output pieces per thread (the
         // persistent writer wave kTileXPOut per lane)
-        int64_t Smax = h->tile_smax > 0 ? h->tile_smax : (persist ? 48 : 64);
-        Smax = std::min<int64_t>(Smax, (int64_t)kTileXOutPieces * kBlockThreads * 16 / ((int64_t)w * 16 * esz));
+        int64_t Smax = h->tile_smax > 0 ? h->tile_smax : (persist ? 48 : NWv == 8 ? 128 : 64);
+        Smax = std::min<int64_t>(Smax, (int64_t)kTileXOutPieces * NT * 16 / ((int64_t)w * 16 * esz));
         if (persist) Smax = std::min<int64_t>(Smax, (int64_t)kTileXPOut * 64 * 16 / ((int64_t)w * 16 * esz));
         Smax = std::max<int64_t>(1, Smax);
         const int64_t stage = (Smax * w * 16 * esz + 15) / 16 * 16;
         const int64_t slot_b = (int64_t)ub * 16 * esz;
         // the LDS stage, and the kernels' staging pieces per thread (16-B pieces: (U + 1) x ub x 16 elements)
-        int64_t Umax = h->tile_umax > 0 ? h->tile_umax : (persist ? 160 : 192);
-        Umax = std::min<int64_t>({Umax, (kTileXLds - stage) / slot_b - 1, (int64_t)kTileXPieces * kBlockThreads * 16 / slot_b - 1});
+        int64_t Umax = h->tile_umax > 0 ? h->tile_umax : (persist ? 160 : NWv == 8 ? 256 : 192);
+        Umax = std::min<int64_t>({Umax, (ldscap - stage) / slot_b - 1, (int64_t)tile_x_pieces(NWv) * NT * 16 / slot_b - 1,
+                                  (int64_t)kTileXSlot - 1});
         if (persist)  // both stages double-buffered in the CU's LDS share of one of tile_wgpc workgroups
             Umax = std::min<int64_t>({Umax, (kTileXPLds / std::max(1, h->tile_wgpc) - 2 * stage - 128) / (2 * slot_b) - 1,
                                       (int64_t)kTileXPLoad * 64 * 16 / slot_b - 1});
@@ -2315,23 +2320,23 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
             }
             // per cluster: streams (LPT), sorted so wave k takes streams 4k .. 4k+3; its segment = the longest of
             // its four in whole batches (at least one: every wave meets every cluster's END)
-            std::vector<std::array<std::vector<int64_t>, kTileXStreams>> csm(nc);
-            std::vector<std::array<int64_t, 4>> clen(nc);
+            std::vector<std::array<std::vector<int64_t>, kTileXMaxStreams>> csm(nc);
+            std::vector<std::array<int64_t, kTileXMaxWaves>> clen(nc);
             for (int64_t c = 0; c < nc; c++) {
                 std::vector<int64_t> byl(corder.begin() + cbeg[c], corder.begin() + cbeg[c + 1]);
                 std::stable_sort(byl.begin(), byl.end(), [&](int64_t x, int64_t y) { return tl[x] > tl[y]; });
-                std::array<int64_t, kTileXStreams> load{};
-                std::array<std::vector<int64_t>, kTileXStreams> sm;
+                std::vector<int64_t> load(NS, 0);
+                std::vector<std::vector<int64_t>> sm(NS);
                 for (int64_t i : byl) {  // longest first to the least loaded stream
                     const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
                     load[k] += tl[i];
                     sm[k].push_back(i);
                 }
-                std::array<int, kTileXStreams> so;
-                for (int k = 0; k < kTileXStreams; k++) so[k] = k;
+                std::vector<int> so(NS);
+                for (int k = 0; k < NS; k++) so[k] = k;
                 std::stable_sort(so.begin(), so.end(), [&](int x, int y) { return load[x] > load[y]; });
-                for (int k = 0; k < kTileXStreams; k++) csm[c][k] = std::move(sm[so[k]]);
-                for (int wv = 0; wv < 4; wv++)
+                for (int k = 0; k < NS; k++) csm[c][k] = std::move(sm[so[k]]);
+                for (int wv = 0; wv < NWv; wv++)
                     clen[c][wv] = std::max<int64_t>(NB, (load[so[4 * wv]] + NB - 1) / NB * NB);
             }
             // cinfo in workgroup order; per workgroup and wave one contiguous stream per row (its clusters'
@@ -2342,8 +2347,8 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
             for (int64_t L = 0; L < nwg; L++) {
                 wginfo[2 * L] = (int32_t)ci_n;
                 wginfo[2 * L + 1] = (int32_t)wgc[L].size();
-                std::array<int64_t, 4> base{}, ltot{}, off{};
-                for (int wv = 0; wv < 4; wv++) {
+                std::array<int64_t, kTileXMaxWaves> base{}, ltot{}, off{};
+                for (int wv = 0; wv < NWv; wv++) {
                     for (int64_t c : wgc[L]) ltot[wv] += clen[c][wv];
                     base[wv] = slot_total;
                     slot_total += 4 * ltot[wv];
@@ -2356,14 +2361,14 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
                     ci[1] = (int32_t)(cbeg[c + 1] - cbeg[c]);
                     ci[2] = xbeg[c + 1] - xbeg[c];
                     ci[3] = xbeg[c];
-                    for (int k = 0; k < kTileXStreams; k++) {
-                        ci[8 + k] = (int32_t)(pos - ci[0]);
+                    for (int k = 0; k < NS; k++) {
+                        ci[kXiSidx + k] = (int32_t)(pos - ci[0]);
                         for (int64_t i : csm[c][k]) lorder[pos++] = i;
                     }
-                    for (int wv = 0; wv < 4; wv++) {
-                        ci[4 + wv] = (int32_t)ltot[wv];
-                        ci[24 + wv] = (int32_t)(base[wv] + off[wv]);
-                        ci[28 + wv] = (int32_t)clen[c][wv];
+                    for (int wv = 0; wv < NWv; wv++) {
+                        ci[kXiStride + wv] = (int32_t)ltot[wv];
+                        ci[kXiSeg + wv] = (int32_t)(base[wv] + off[wv]);
+                        ci[kXiLen + wv] = (int32_t)clen[c][wv];
                         off[wv] += clen[c][wv];
                     }
                     most_s = std::max<int64_t>(most_s, ci[1]);
@@ -2383,7 +2388,8 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
             tb.xslots = (int32_t)(most_u + 1);
             tb.stage_bytes = (int32_t)((most_s * w * 16 * esz + 15) / 16 * 16);
             tb.nranges = (int32_t)nc;
-            tb.nwg = (int32_t)nwg;
+            tb.nwg = persist ? (int32_t)nwg : 0;
+            tb.nwaves = NWv;
             tb.out_affine = 0;
             pp.o_key = ar.reserve((slot_total + kpad) * 4);
             pp.o_val = ar.reserve((slot_total * TV + vpad) * esz);
@@ -2408,9 +2414,9 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
                 const int64_t c = cof[cn];
                 const uint32_t U = (uint32_t)ci[2];
                 for (int32_t x = xbeg[c]; x < xbeg[c + 1]; x++) gslot[xrow[x]] = x - xbeg[c];
-                for (int k = 0; k < kTileXStreams; k++) {
-                    const int64_t len = ci[28 + k / 4];
-                    int64_t slot = ci[24 + k / 4] + (int64_t)(k % 4) * ci[4 + k / 4];
+                for (int k = 0; k < NS; k++) {
+                    const int64_t len = ci[kXiLen + k / 4];
+                    int64_t slot = ci[kXiSeg + k / 4] + (int64_t)(k % 4) * ci[kXiStride + k / 4];
                     const int64_t first = slot;
                     for (int64_t i : csm[c][k]) {
                         const int64_t l = stripes[i];
@@ -3266,6 +3272,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = getenv("VBC_TILE_REUSE")) h->tile_reuse = atof(e);
         if (const char *e = getenv("VBC_TILE_WGPC")) h->tile_wgpc = std::max(1, atoi(e));
         if (const char *e = getenv("VBC_TILE_PERSIST")) h->tile_persist = atoi(e) != 0;
+        if (const char *e = getenv("VBC_TILE_WAVES")) h->tile_waves = atoi(e);
         h->occ_tiles = occupancy_tiles(h->esz);
     }
 

@@ -128,6 +128,8 @@ struct vbc_handle {
     int tile_smax = -1;           // VBC_TILE_SMAX: stripes per cluster of the staged-X form (auto: 48 persistent, 64)
     int tile_umax = -1;           // VBC_TILE_UMAX: row groups staged per cluster (LDS: (U + 1) x ub x 16 elements;
                                   // auto: 160 for the persistent kernel's double-buffered stage, 192)
+    int tile_waves = 4;           // VBC_TILE_WAVES: compute waves per cluster workgroup of spmm_tiles_x (fp32: 4 or 8;
+                                  // 8 = two 80 KB workgroups per CU: c5-mesh 356 us against 307 us with 4)
     int tile_wgpc = 2;            // VBC_TILE_WGPC: persistent workgroups per CU of the staged-X form
     int tile_persist = 0;         // VBC_TILE_PERSIST=1: the persistent staged-X kernel (spmm_tiles_xp) when X and Y allow it
     double tile_reuse = 2.0;      // VBC_TILE_REUSE: auto staged-X form when each staged group serves >= this many tiles

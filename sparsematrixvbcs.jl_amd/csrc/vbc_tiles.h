@@ -42,16 +42,22 @@ constexpr int kTileStripes = 32;             // default stripes per range (c5-me
 constexpr int kTileBatch = 8;                // default tiles per stream per pipeline stage (4 or 8: one key load per two)
 
 // Staged-X form (round 5b; TileBin::staged): one workgroup per CLUSTER of stripes that share block rows
-constexpr int kTileXInfo = 32;        // ints per cluster: {first stripe (out index), stripes, U, xrow offset,
-                                      //  4 x row stride of wave k's stream, 16 x first local stripe of stream k,
-                                      //  4 x first tile slot of wave k's segment (row 0), 4 x its length}
+constexpr int kTileXMaxWaves = 8;     // compute waves per cluster workgroup (4 or 8; the persistent kernel: 4)
+constexpr int kTileXMaxStreams = 4 * kTileXMaxWaves;
+// ints per cluster: {first stripe (out index), stripes, U, xrow offset, 8 x row stride of wave k's stream,
+// 32 x first local stripe of stream k, 8 x first tile slot of wave k's segment (row 0), 8 x its length}
+constexpr int kXiStride = 4, kXiSidx = kXiStride + kTileXMaxWaves, kXiSeg = kXiSidx + kTileXMaxStreams,
+              kXiLen = kXiSeg + kTileXMaxWaves;
+constexpr int kTileXInfo = 64;
 constexpr uint32_t kTileXEnd = 0x40000000u;  // key bit 30: the last tile of a wave's segment of a cluster
-constexpr int kTileXStreams = 16;     // 4 waves x 4 rows of 16 lanes
+constexpr int kTileXStreams = 16;     // 4 waves x 4 rows of 16 lanes (the persistent kernel's compute waves)
 constexpr int kTileXBatch = 8;        // tiles per stream per pipeline stage
 constexpr int kTileXDepth = 4;        // stages in flight (keys and values)
 constexpr uint32_t kTileXSlot = 0xFFFFu;  // key bits 0..15: the tile's X slot in the cluster's LDS stage
-constexpr int64_t kTileXLds = 65536;      // LDS per workgroup: X stage + output stage
+constexpr int64_t kTileXLds = 65536;      // LDS per workgroup: X stage + output stage (4 compute waves)
+constexpr int64_t kTileXLds8 = 80 * 1024; // ... 8 compute waves: two workgroups per CU
 constexpr int kTileXPieces = 12;          // 16-B X pieces per thread of the staging (U + 1) x ub x 16 elements
+constexpr int tile_x_pieces(int nw) { return nw == 8 ? 8 : kTileXPieces; }  // (8 waves: registers for 4 waves / SIMD)
 constexpr int kTileXOutPieces = 4;        // 16-B output pieces per thread of the epilogue (stripes x w x 16 elements)
 
 // One width bucket of the tile layout (one launch per 16 right-hand sides).
@@ -76,6 +82,7 @@ struct TileBin {
     int32_t staged;
     int32_t xslots;       // largest U + 1 of a cluster (the LDS X stage: xslots x ub x 16 elements)
     const int32_t *xrow;
+    int32_t nwaves;       // compute waves per cluster (spmm_tiles_x: 4 or 8; 4 streams each)
     int32_t nwg;          // persistent kernel (spmm_tiles_xp): workgroups, each a sequence of clusters
     const int32_t *wginfo;  // per workgroup: {first cluster, clusters}
     const void *zsrc;     // 16 zero bytes in device memory (the LDS-DMA source of zero pieces)
@@ -582,8 +589,8 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles4(const TileBin b, co
 //     keys and values run kTileXDepth batches ahead (no X registers to hold: the gathers are LDS reads);
 //   * a LAST tile parks the stripe's w x 16 sums in the workgroup's output stage, written after a barrier.
 // X4: 16 contiguous right-hand sides in 16-B aligned rows (16-B staging loads); else element loads.
-template <typename T, int UB, int W, bool MASKU, bool X4>
-__global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, const T *__restrict__ X, int64_t sxr,
+template <typename T, int UB, int W, bool MASKU, bool X4, int NW>
+__global__ __launch_bounds__(NW * 64) void spmm_tiles_x(const TileBin b, const T *__restrict__ X, int64_t sxr,
                                                               int64_t sxc, int64_t xrows, T *__restrict__ Y, int64_t syr,
                                                               int64_t syc, int nrhs, T alpha, T beta, int rd_i, int fast)
 {
@@ -605,10 +612,10 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
     const int U = __builtin_amdgcn_readfirstlane(ci[2]), xo = __builtin_amdgcn_readfirstlane(ci[3]);
     // the wave's segment of the cluster: its own length (the longest of its 4 rows' streams, whole batches);
     // the rows of a wave are strided by the wave's whole stream (the persistent layout, spmm_tiles_xp)
-    const int tile0 = __builtin_amdgcn_readfirstlane(ci[24 + wv]), len = __builtin_amdgcn_readfirstlane(ci[28 + wv]);
-    const int rstride = __builtin_amdgcn_readfirstlane(ci[4 + wv]);
+    const int tile0 = __builtin_amdgcn_readfirstlane(ci[kXiSeg + wv]), len = __builtin_amdgcn_readfirstlane(ci[kXiLen + wv]);
+    const int rstride = __builtin_amdgcn_readfirstlane(ci[kXiStride + wv]);
     const int stream = wv * 4 + g;
-    int sidx = G(b.rinfo)[(size_t)cl * kTileXInfo + 8 + stream];  // cluster-local index of this row's first stripe
+    int sidx = G(b.rinfo)[(size_t)cl * kTileXInfo + kXiSidx + stream];  // cluster-local index of this row's first stripe
                                                                   // (a stream's stripes are consecutive)
     const int64_t kb = (int64_t)tile0 + (int64_t)g * rstride;
     const gptr<const uint32_t> key = G(b.key);
@@ -636,7 +643,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
     const gptr<const int32_t> outp = G(b.out) + s0;
     int ocol[kTileXOutPieces];
 #pragma unroll
-    for (int k = 0; k < kTileXOutPieces; k++) ocol[k] = outp[min((tid + k * kBlockThreads) / (W * PPR), max(ns - 1, 0))];
+    for (int k = 0; k < kTileXOutPieces; k++) ocol[k] = outp[min((tid + k * (NW * 64)) / (W * PPR), max(ns - 1, 0))];
 
     // phase 1: the cluster's X block rows -> LDS [slot][r][16], slot U (and rows past X) zero.  Every load of
     // a thread is issued before the first LDS write, with clamped addresses and selects instead of branches
@@ -644,14 +651,14 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
     // included): one round trip for the slots' rows, one for the stage.  At most kTileXPieces 16-B pieces
     // per thread (the builder caps U to fit).
     if (!(b.diag & 1)) {  // (diag 1: no staging -- an ablation, tools/ab.py)
-        constexpr int MP = kTileXPieces;
+        constexpr int MP = tile_x_pieces(NW);
         const gptr<const int32_t> xr = G(b.xrow) + xo;  // (xrow carries one entry past the last cluster's)
         if constexpr (X4) {
             const int np = (U + 1) * UB * PPR;
             int row[MP];
 #pragma unroll
             for (int u = 0; u < MP; u++) {
-                const int p = tid + u * kBlockThreads;
+                const int p = tid + u * (NW * 64);
                 const int slot = min(p / (UB * PPR), U);
                 const int rr = (p - slot * (UB * PPR)) / PPR;
                 const int r0 = xr[slot] + rr;
@@ -660,23 +667,23 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
             tv v[MP];
 #pragma unroll
             for (int u = 0; u < MP; u++) {
-                const int p = tid + u * kBlockThreads;
+                const int p = tid + u * (NW * 64);
                 const tv t = *(gptr<const tv>)(G(X) + (int64_t)max(row[u], 0) * sxr + (p % PPR) * EPL);
                 v[u] = row[u] >= 0 ? t : tv{};
             }
 #pragma unroll
             for (int u = 0; u < MP; u++) {
-                const int p = tid + u * kBlockThreads;
+                const int p = tid + u * (NW * 64);
                 // piece p of the stage is elements p * EPL .. p * EPL + EPL - 1: (slot, row r, RHS group q)
                 if (p < np) *reinterpret_cast<tv *>(xl + p * EPL) = v[u];
             }
         } else {
             const int ne = (U + 1) * UB * 16;
-            for (int e0 = 0; e0 < ne; e0 += MP * kBlockThreads) {
+            for (int e0 = 0; e0 < ne; e0 += MP * (NW * 64)) {
                 int row[MP];
 #pragma unroll
                 for (int u = 0; u < MP; u++) {
-                    const int e = e0 + tid + u * kBlockThreads;
+                    const int e = e0 + tid + u * (NW * 64);
                     const int slot = min(e / (UB * 16), U);
                     const int r0 = xr[slot] + (e >> 4) - slot * UB;
                     row[u] = ((e < ne) & (slot < U) & (r0 < xrows) & ((e & 15) < nrhs)) ? r0 : -1;
@@ -684,13 +691,13 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
                 T v[MP];
 #pragma unroll
                 for (int u = 0; u < MP; u++) {
-                    const int jj = (e0 + tid + u * kBlockThreads) & 15;
+                    const int jj = (e0 + tid + u * (NW * 64)) & 15;
                     const T t = G(X)[(int64_t)max(row[u], 0) * sxr + (int64_t)(row[u] >= 0 ? jj : 0) * sxc];
                     v[u] = row[u] >= 0 ? t : zero;
                 }
 #pragma unroll
                 for (int u = 0; u < MP; u++)
-                    if (e0 + tid + u * kBlockThreads < ne) xl[e0 + tid + u * kBlockThreads] = v[u];
+                    if (e0 + tid + u * (NW * 64) < ne) xl[e0 + tid + u * (NW * 64)] = v[u];
             }
         }
     }
@@ -760,7 +767,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
         const int np = ns * W * PPR;  // (<= kTileXOutPieces x 256: the builder caps the stripes per cluster)
 #pragma unroll
         for (int k = 0; k < kTileXOutPieces; k++) {
-            const int p = tid + k * kBlockThreads;
+            const int p = tid + k * (NW * 64);
             if (p >= np) break;
             const int i = p / (W * PPR), rem = p - i * (W * PPR);
             gptr<T> yo = G(Y) + (int64_t)((b.diag & 4) ? (s0 + i) * W : ocol[k]) * 16 + rem * EPL;  // (diag 4: contiguous)
@@ -777,7 +784,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles_x(const TileBin b, c
         }
     } else {
         const int total = ns * W * 16;
-        for (int e = tid; e < total; e += kBlockThreads) {
+        for (int e = tid; e < total; e += (NW * 64)) {
             const int i = e / (W * 16), rem = e - i * (W * 16), c = rem >> 4, jj = rem & 15;
             if (jj >= nrhs) continue;
             gptr<T> yo = G(Y) + ((int64_t)outp[i] + c) * syr + (int64_t)jj * syc;
@@ -859,7 +866,7 @@ __global__ __launch_bounds__(kTileXPThreads) void spmm_tiles_xp(const TileBin b,
         auto dma = [&](int c, int half, const int (&row)[kTileXPLoad]) {
             const cptr ci = cinfo + (size_t)c * kTileXInfo;
             const int np = (ci[2] + 1) * UB * PPR;
-            if (lane < kTileXStreams) sinfo[half * kTileXStreams + lane] = G(b.rinfo)[(size_t)c * kTileXInfo + 8 + lane];
+            if (lane < kTileXStreams) sinfo[half * kTileXStreams + lane] = G(b.rinfo)[(size_t)c * kTileXInfo + kXiSidx + lane];
             // LDS byte address of this half (M0 of the DMA: lane l of piece round i lands at M0 + l * 16)
             const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(xbuf + half * xfl);
 #pragma unroll
@@ -930,8 +937,8 @@ __global__ __launch_bounds__(kTileXPThreads) void spmm_tiles_xp(const TileBin b,
     // ---- compute waves
     const int g = lane >> 4, j = lane & 15, stream = wv * 4 + g;
     const cptr ci0 = cinfo + (size_t)c0 * kTileXInfo;
-    const int len = ci0[4 + wv];  // the wave's whole stream (its segments of the K clusters)
-    const int64_t kb = (int64_t)ci0[24 + wv] + (int64_t)g * len;
+    const int len = ci0[kXiStride + wv];  // the wave's whole stream (its segments of the K clusters)
+    const int64_t kb = (int64_t)ci0[kXiSeg + wv] + (int64_t)g * len;
     const gptr<const uint32_t> key = G(b.key);
     const gptr<const T> val = G(static_cast<const T *>(b.val));
     const T zero = T(0);

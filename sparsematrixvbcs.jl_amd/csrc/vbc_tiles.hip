@@ -118,14 +118,36 @@ static void launch_tiles_xp_u(const TileBin &tb, hipStream_t s, const float *xs,
 }
 
 // the staged-X form (spmm_tiles_x): one workgroup per cluster, LDS = X stage + output stage
+template <typename T, int UB, int W, bool MASKU, bool X4, int NW>
+static void launch_tiles_x_k(const TileBin &tb, hipStream_t s, const T *xs, int64_t sxr, int64_t sxc, int64_t xrows,
+                             T *ys, int64_t syr, int64_t syc, int nr, T alpha, T beta, int rd, int fast)
+{
+    const size_t lds = (size_t)tb.xslots * UB * 16 * sizeof(T) + (size_t)tb.stage_bytes;
+    if (lds > 65536) {  // (above the default dynamic LDS limit: raised once per instantiation)
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(spmm_tiles_x<T, UB, W, MASKU, X4, NW>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTileXLds8);
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL((spmm_tiles_x<T, UB, W, MASKU, X4, NW>), dim3(tb.nranges), dim3(NW * 64), lds, s, tb, xs, sxr, sxc,
+                       xrows, ys, syr, syc, nr, alpha, beta, rd, fast);
+}
 template <typename T, int UB, int W>
 static void launch_tiles_x_uw(const TileBin &tb, hipStream_t s, const T *xs, int64_t sxr, int64_t sxc, int64_t xrows,
                               bool x4, T *ys, int64_t syr, int64_t syc, int nr, T alpha, T beta, int rd, int fast)
 {
-    const size_t lds = (size_t)tb.xslots * UB * 16 * sizeof(T) + (size_t)tb.stage_bytes;
-#define VBC_TILESX(MASKU, X4)                                                                                      \
-    hipLaunchKernelGGL((spmm_tiles_x<T, UB, W, MASKU, X4>), dim3(tb.nranges), dim3(kBlockThreads), lds, s, tb, xs, \
-                       sxr, sxc, xrows, ys, syr, syc, nr, alpha, beta, rd, fast)
+#define VBC_TILESX(MASKU, X4)                                                                                          \
+    do {                                                                                                               \
+        if constexpr (sizeof(T) == 4) {                                                                                \
+            if (tb.nwaves == 8) {                                                                                      \
+                launch_tiles_x_k<T, UB, W, MASKU, X4, 8>(tb, s, xs, sxr, sxc, xrows, ys, syr, syc, nr, alpha, beta, rd, fast); \
+                break;                                                                                                 \
+            }                                                                                                          \
+        }                                                                                                              \
+        launch_tiles_x_k<T, UB, W, MASKU, X4, 4>(tb, s, xs, sxr, sxc, xrows, ys, syr, syc, nr, alpha, beta, rd, fast); \
+    } while (0)
     if (tb.masku) {
         if (x4) VBC_TILESX(true, true);
         else VBC_TILESX(true, false);

@@ -329,11 +329,11 @@ def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
     assert np.array_equal(got[fin], ref[fin])
 
 
-@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("form", ["persist", "waves4", "waves8"])
 @pytest.mark.parametrize("smax,umax", [(3, 40), (7, 64), (64, 192)])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, persist, multi_layout, monkeypatch):
-    """Staged-X tile form (spmm_tiles_x; with persist "1" and fp32 the persistent spmm_tiles_xp: workgroups walking
+def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, form, multi_layout, monkeypatch):
+    """Staged-X tile form (spmm_tiles_x with 4 or 8 compute waves; with form "persist" and fp32 the persistent spmm_tiles_xp: workgroups walking
     sequences of clusters, stager / writer waves, double-buffered LDS) on the structured C5 input at small scale:
     clusters cut by the stripe cap or by the LDS stage (VBC_TILE_SMAX / VBC_TILE_UMAX), 16 row-major right-hand
     sides, both directions
@@ -344,7 +344,10 @@ def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, persist, multi_l
         pytest.skip("staged-X form only")
     monkeypatch.setenv("VBC_TILE_SMAX", str(smax))
     monkeypatch.setenv("VBC_TILE_UMAX", str(umax))
-    monkeypatch.setenv("VBC_TILE_PERSIST", persist)  # fp32 x 16 row-major RHS: the persistent kernel when "1"
+    # fp32 x 16 row-major RHS: the persistent kernel (spmm_tiles_xp); else spmm_tiles_x with 4 or 8 compute waves
+    # per cluster (fp64 always 4)
+    monkeypatch.setenv("VBC_TILE_PERSIST", "1" if form == "persist" else "0")
+    monkeypatch.setenv("VBC_TILE_WAVES", "8" if form == "waves8" else "4")
     import bench
     B = bench.build_matrix("c5-mesh", dtype, 0.002)
     B.val[:] = np.random.default_rng(3).integers(-8, 9, B.val.shape)
