@@ -299,6 +299,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int total = ns * W * 16;
     const bool rd = rd_i != 0;
+    if (b.diag & 8) return;  // (diag 8: no output stores -- an ablation, tools/ab.py)
     if (fast) {
         gptr<T> yb = G(Y) + ((int64_t)b.out_base + (int64_t)s0 * W) * 16;
         for (int e = lane * EPL; e < total; e += 64 * EPL) {
