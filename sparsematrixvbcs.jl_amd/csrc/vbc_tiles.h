@@ -300,7 +300,26 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
     const int total = ns * W * 16;
     const bool rd = rd_i != 0;
     if (b.diag & 8) return;  // (diag 8: no output stores -- an ablation, tools/ab.py)
-    if (fast) {
+    if (fast == 2) {
+        // Y row-major with 16 contiguous right-hand sides, stripes not contiguous (a non-natural stripe order,
+        // e.g. VBC_TILE_ORDER=1): each stripe's W x 16 block is contiguous -- 16-B pieces, not element stores
+        constexpr int PPR = 16 / EPL;
+        const gptr<const int32_t> outp = G(b.out) + s0;
+        for (int p = lane; p < ns * W * PPR; p += 64) {
+            const int i = p / (W * PPR), rem = p - i * (W * PPR);
+            gptr<T> yo = G(Y) + (int64_t)outp[i] * 16 + rem * EPL;
+            const tv v = *reinterpret_cast<const tv *>(st + i * W * 16 + rem * EPL);
+            tv o;
+#pragma unroll
+            for (int q = 0; q < EPL; q++) o[q] = alpha * v[q];
+            if (rd) {
+                const tv yo0 = *(gptr<const tv>)yo;
+#pragma unroll
+                for (int q = 0; q < EPL; q++) o[q] = fmadd(beta, yo0[q], o[q]);
+            }
+            *(gptr<tv>)yo = o;
+        }
+    } else if (fast) {
         gptr<T> yb = G(Y) + ((int64_t)b.out_base + (int64_t)s0 * W) * 16;
         for (int e = lane * EPL; e < total; e += 64 * EPL) {
             tv v = *reinterpret_cast<const tv *>(st + e);

@@ -221,8 +221,10 @@ static int mulmat_tiles(const vbc_handle *h, const PanelLaunch &L, int64_t nrhs,
                 continue;
             }
             // one contiguous run of Y per range: affine map of stride w, 16 contiguous right-hand sides
-            const int fast = tb.out_affine && tb.out_stride == tb.w && nr == 16 && syc == 1 && syr == 16 &&
-                             reinterpret_cast<uintptr_t>(ys) % 16 == 0;
+            const bool rows16 = nr == 16 && syc == 1 && syr == 16 && reinterpret_cast<uintptr_t>(ys) % 16 == 0;
+            int fast = tb.out_affine && tb.out_stride == tb.w && rows16 ? 1 : 0;
+            // (the dword form: stripes in another order still store 16-B pieces of each stripe's block)
+            const int fast_dw = fast ? 1 : (rows16 ? 2 : 0);
             const int grid = (tb.nranges + kWavesPerBlock - 1) / kWavesPerBlock;
             // the 16-B form: fp32, 16 contiguous right-hand sides in 16-B aligned rows (one dwordx4 per tile row)
             if constexpr (sizeof(T) == 4) {
@@ -242,10 +244,10 @@ static int mulmat_tiles(const vbc_handle *h, const PanelLaunch &L, int64_t nrhs,
                 }
             }
             switch (tb.ub) {
-            case 1: launch_tiles_u<T, 1>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast); break;
-            case 2: launch_tiles_u<T, 2>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast); break;
-            case 3: launch_tiles_u<T, 3>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast); break;
-            default: launch_tiles_u<T, 4>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast); break;
+            case 1: launch_tiles_u<T, 1>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast_dw); break;
+            case 2: launch_tiles_u<T, 2>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast_dw); break;
+            case 3: launch_tiles_u<T, 3>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast_dw); break;
+            default: launch_tiles_u<T, 4>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, (T)alpha, (T)beta, rd, fast_dw); break;
             }
             VBC_HIP(hipGetLastError());
         }

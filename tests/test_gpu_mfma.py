@@ -370,3 +370,30 @@ def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, form, multi_layo
                                np.ascontiguousarray(Y0[:, j], dtype=np.float64), 0.5, -1.25, trans=trans,
                                ref_semantics=False) for j in range(7)], axis=1)
         assert rel(Yd.cpu().numpy(), want) <= (TOL64 if dtype == np.float64 else TOL32), trans
+
+
+@pytest.mark.parametrize("blob", ["64", "512"])
+def test_tiles_blob_order_scattered_stripes_bitwise(blob, multi_layout, monkeypatch):
+    """Tile layout in blob order (VBC_TILE_ORDER=1: stripes processed in compact balls of the stripe graph, so a
+    range's stripes are not contiguous columns): 16 row-major right-hand sides take the per-stripe 16-B epilogue
+    (each stripe's w x 16 block of Y), with and without beta -- integer data, every column bit for bit."""
+    if multi_layout != "tiles":
+        pytest.skip("tile layout only")
+    monkeypatch.setenv("VBC_TILE_ORDER", "1")
+    monkeypatch.setenv("VBC_TILE_BLOB", blob)
+    import bench
+    B = bench.build_matrix("c5-mesh", np.float32, 0.002)
+    B.val[:] = np.random.default_rng(5).integers(-8, 9, B.val.shape)
+    Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    rng = np.random.default_rng(int(blob))
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        X = rng.integers(-8, 9, (nx, 16)).astype(np.float32)
+        Y0 = rng.integers(-8, 9, (ny, 16)).astype(np.float32)
+        for alpha, beta in ((1.0, 0.0), (2.0, -1.0)):
+            Yd = torch.from_numpy(Y0.copy()).to(DEV)
+            V.mul_(Yd, B.T if trans else B, torch.from_numpy(X).to(DEV), alpha, beta, engine="mfma")
+            want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64),
+                                   np.ascontiguousarray(Y0[:, j], dtype=np.float64), alpha, beta, trans=trans,
+                                   ref_semantics=False) for j in range(16)], axis=1)
+            assert np.array_equal(Yd.cpu().numpy(), want.astype(np.float32)), (trans, alpha, beta)
