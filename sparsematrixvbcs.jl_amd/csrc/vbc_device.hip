@@ -743,10 +743,14 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     const int64_t real = sbeg[nseg] - sbeg[0];
     std::vector<int32_t> len(nseg);  // runs per stripe (an empty stripe: one zero run)
     for (int64_t q = 0; q < nseg; q++) len[q] = (int32_t)std::max<int64_t>(1, (sbeg[q + 1] - sbeg[q]) / run);
-    const double share = (double)h->target_ranges_l * (double)real / (double)std::max<int64_t>(total_entries, 1);
+    // (sized for half the resident waves -- round 5: fewer, longer tiles near the LDS cap; FE-3D 12,255 tiles of
+    // 272 stripes 218.2 us, 10,163 of 328 213.8 us, profiles/r05zh_lanes_ab.log -- the selection rule above
+    // keeps the full count)
+    const double share = (double)h->target_ranges_l / std::max(1, h->lanes_rdiv) * (double)real /
+                         (double)std::max<int64_t>(total_entries, 1);
     const int64_t nr_target = std::max<int64_t>(1, std::llround(share));
     // one tile per range (a wave) of at most one LDS tile buffer of outputs; S a multiple of 4 stripes,
-    // the ranges a whole number of rounds of the resident waves
+    // the ranges a whole number of rounds of the target
     const int64_t smax = (kLaneTileBytes / (w * esz)) & ~3;
     const int64_t rounds = std::max<int64_t>(1, (nseg + nr_target * smax - 1) / (nr_target * smax));
     int64_t S = (nseg + rounds * nr_target - 1) / (rounds * nr_target);
@@ -3226,6 +3230,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char *e = getenv("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
+    if (const char *e = getenv("VBC_LANES_RDIV")) h->lanes_rdiv = std::max(1, atoi(e));
     if (const char *e = getenv("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
     if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));

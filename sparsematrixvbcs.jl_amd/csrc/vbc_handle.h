@@ -146,6 +146,7 @@ struct vbc_handle {
     size_t carry_mm_bytes = 0;
     int target_ranges_k[2] = {4096, 4096};  // resident waves of the B'x / Bx kernels (one range each)
     int tile_k = vbc::kTileKDefault;  // entries per slot per tile
+    int lanes_rdiv = 2;               // VBC_LANES_RDIV: lane-stream tiles sized for target_ranges_l / this many ranges
     int pipe = vbc::kPipeDefault;     // software-pipeline depth (2 or 3 tiles)
     int diag = 0;                     // ablation variant (VBC_DIAG; tools/ab.py only)
     int target_ranges_s[2] = {4096, 4096};  // resident waves of the slotted kernels
