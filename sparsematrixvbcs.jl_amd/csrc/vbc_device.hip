@@ -3258,11 +3258,11 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     }
     h->slot_u = h->esz == 8 ? 8 : 16;  // rows per step (measured on FE: 4 / 8 rows are 4-8 % slower)
     if (flags & (VBC_CREATE_MULTI | VBC_CREATE_MULTI_FORWARD)) {
-        // at most two ranges per SIMD (round 5): the fp32 panel kernel's occupancy allows four, but half as many
-        // ranges of twice the length run faster -- C5 fp32 B'X 206.5 -> 195.5 us, B·X 205.8 -> 196.1 us
-        // (1536 ranges: 240 us; 3072: 202 us; profiles/r05zk_c5*.log); fp64 already resides two per SIMD
+        // (round 5: half as many ranges measured 195.5 against 206.5 us in tools/ab.py's interleaved graph replays,
+        // but 213-216 against 208-210 us in bench.py's own C5 line, each setting in a fresh process --
+        // profiles/r05zo_c5_ranges_ab.log; the bench decides, the count stays one round of resident waves)
         const int om = occupancy_panel(h->esz);
-        h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 2)) * kWavesPerBlock;
+        h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
         if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
         if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
         if (const char *e = getenv("VBC_PANEL_DIAG")) h->panel_valu |= atoi(e) & ~1;
