@@ -118,9 +118,6 @@ def kernel_name(B, local, k, trans=True):
         if B.info(local, trans, multi=True)["planar_mask"] & 512:
             return ("vbc::spmm_tiles<T, UB, W, NBT, MASKU, BUF> (tile-granular: one key and one UB-row X block per "
                     "u x w tile, 4 streams of stripes per wave, csrc/vbc_tiles.h)")
-        if B.info(local, trans, multi=True)["planar_mask"] & 128:
-            return ("vbc::spmm_quads<T, W, VEC> (VALU stripe quads: 16 stripes x 4 right-hand-side quads per wave, "
-                    "csrc/vbc_panel.h)")
         return "vbc::spmm_panel<T, NB, BUF, FAST> (v_mfma_*_16x16x4)"
     if not trans:
         inf = B.info(local, False)

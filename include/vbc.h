@@ -301,14 +301,13 @@ typedef struct vbc_info {
                                bit 4: the forward bucket in lane streams (node blocks transposed);
                                bit 5: a small matrix's B'x buckets of every width (1..8) laid out planar
                                and split, run by ONE fused launch (planar_split = its P); bit 6: some of
-                               those stripes cut into 2 / 4 lane parts (long stripes); bit 7: the multi-RHS
-                               layout has VALU stripe-quad buckets (widths <= 8, spmm_quads); bit 8: the
+                               those stripes cut into 2 / 4 lane parts (long stripes); bit 7: reserved (0;
+                               round 5's VALU stripe-quad layout); bit 8: the
                                forward product runs on the transposed layout of C = Bᵀ (stripes of several
                                widths: one fused launch instead of one per width); bit 9: the multi-RHS
                                layout has tile-granular buckets (u, w <= 4 tiles: one key and one u-row X
-                               block per tile, spmm_tiles); bit 10: some of those buckets in the staged-X
-                               form (clusters of stripes sharing row groups, the groups staged in LDS,
-                               spmm_tiles_x) */
+                               block per tile, spmm_tiles); bit 10: reserved (0; round 5's staged-X tile
+                               form) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

@@ -119,7 +119,7 @@ static int build_bucket(vbc_handle *h, int kind, int w, const std::vector<Entry>
     pb.b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
     for (size_t q = 1; q < out.size() && pb.b.out_affine; q++)
         pb.b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * pb.b.out_stride;
-    if (getenv("VBC_NO_AFFINE")) pb.b.out_affine = 0;  // A/B knob
+    if (ablation_knob("VBC_NO_AFFINE")) pb.b.out_affine = 0;  // (the VBC_ABLATION build only)
     range0 += (int)nr;
     const int64_t Rp = ntiles * tile_rows;
     pb.o_key = ar.reserve(Rp * 4);
@@ -536,7 +536,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     }
     rrow.push_back((int32_t)rows);
     nr = (int64_t)rchunk.size();
-    if (getenv("VBC_VERBOSE"))
+    if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] slot bin kind %d w %d planar %d pair %d run %d split %d chunks %lld rows %lld ranges %lld "
                 "(target share %.0f)\n", kind, w, (int)planar, (int)pair, run, split, (long long)nch, (long long)rows,
                 (long long)nr, share);
@@ -584,7 +584,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.out_stride = out.size() > 1 ? out[1] - out[0] : 0;
     for (size_t q = 1; q < out.size() && b.out_affine; q++)
         b.out_affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * b.out_stride;
-    if (getenv("VBC_NO_AFFINE")) b.out_affine = 0;  // A/B knob
+    if (ablation_knob("VBC_NO_AFFINE")) b.out_affine = 0;  // (the VBC_ABLATION build only)
     {
         const int V = w <= 8 ? vec_elems(esz, w) : 1;
         const bool full = b.spl > 1 || planar || (RPI * (w / V) == 64 && V * esz <= 16);
@@ -810,7 +810,7 @@ static int build_lanes(vbc_handle *h, int w, const std::vector<Entry> &ents, con
     const std::vector<int32_t> &rrow = trow;  // one tile per range
     std::vector<int32_t> rchunk(nr + 1);
     for (int64_t r = 0; r <= nr; r++) rchunk[r] = (int32_t)r;
-    if (getenv("VBC_VERBOSE"))
+    if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] lanes bin w %d run %d pair %d stripes %lld ranges %lld x %lld stripes (target %d), rows "
                 "%lld (live %.3f)\n", w, run, (int)pair, (long long)nseg, (long long)nr, (long long)S, h->target_ranges_l,
                 (long long)rows, (double)real / (double)std::max<int64_t>(1, rows * NS * (run / rows_per_step)));
@@ -1109,7 +1109,7 @@ static int padded_width(const vbc_handle *h, int w)
     static const int def64[9] = {0, 1, 2, 4, 4, 5, 6, 8, 8};
     static const int def32[9] = {0, 1, 2, 4, 4, 5, 8, 8, 8};
     int wp = w <= 8 ? (h->esz == 8 ? def64[w] : def32[w]) : w;
-    if (const char *e = getenv("VBC_PAD")) {
+    if (const char *e = tuning_knob("VBC_PAD")) {
         wp = w;
         for (const char *p = e; *p;) {
             int a = 0, b = 0, n = 0;
@@ -1172,7 +1172,7 @@ static void hole_runs(const vbc_handle *h, const Stripes &s, const std::vector<i
             }
             hsbeg.push_back((int64_t)hents.size());
         }
-        if (getenv("VBC_VERBOSE"))
+        if (layout_knob("VBC_VERBOSE"))
             fprintf(stderr, "[vbc] runs with holes: w %d R %d rows %lld -> %lld\n", w, R, (long long)real,
                     (long long)expanded);
         return;
@@ -1215,7 +1215,7 @@ static int build_ksplit(vbc_handle *h, int w, int ks, const std::vector<Entry> &
                 const int64_t t = c * m + i;
                 order[c * 64 + p * m + i] = (t < n ? byl[t] : t) * ks + p;
             }
-    if (getenv("VBC_VERBOSE"))
+    if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] long stripes: w %d, %lld stripes cut into %d parts (runs of %d), %lld chunks\n", w,
                 (long long)n, ks, R, (long long)nchk);
     return build_slots(h, 0, w, w, ents, sx, ox, total, val, ar, range0, ps, order, false, ks);
@@ -1266,7 +1266,7 @@ static bool column_pieces(const vbc_handle *h, const Stripes &s, Stripes &c)
         }
     }
     c.L = (int64_t)c.w.size();
-    if (getenv("VBC_VERBOSE"))
+    if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] column pieces: %lld stripes -> %lld (dominant width %d)\n", (long long)s.L,
                 (long long)c.L, wd);
     return true;
@@ -1412,7 +1412,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
             kst.clear();
             h->fuse_w = 0;
         }
-        if (getenv("VBC_VERBOSE"))
+        if (layout_knob("VBC_VERBOSE"))
             fprintf(stderr, "[vbc] small fused split: %d of %d buckets (width mask 0x%x), %lld chunks, %.1f rows per "
                     "chunk -> P = %d%s\n", nf, (int)buckets.size(), h->fuse_w, (long long)nch, avg, h->small_split,
                     kst.empty() ? "" : ", long stripes cut");
@@ -1461,7 +1461,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
         const int wp = padded_width(h, w);
         // the slotted kernel has no scan to feed: fp64 w = 3 runs unpadded (8-B lanes), measured
         // 117 -> 106 us on the ldoor stand-in (fp32 keeps 3 -> 4: 73 vs 84 us unpadded)
-        const int wps = slot_planar(h, 0, w) ? w : (h->esz == 8 && w == 3 && !getenv("VBC_PAD")) ? 3 : wp;
+        const int wps = slot_planar(h, 0, w) ? w : (h->esz == 8 && w == 3 && !tuning_knob("VBC_PAD")) ? 3 : wp;
         std::vector<int64_t> sbeg{0}, order;
         for (int64_t l : kv.second) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
         bool mask = false;
@@ -1561,7 +1561,7 @@ static int build_transposed(vbc_handle *h, const Stripes &s0, const char *val, A
     L.sweep_tiles = tile0;
     L.fuse_p = h->small_split;  // (the handle's field is rebuilt by the next build_transposed call)
     L.sweep_tile_bytes = h->sweep_tile;
-    if (const char *e = getenv("VBC_SWEEP_DIAG")) L.sweep_diag = atoi(e);
+    if (const char *e = ablation_knob("VBC_SWEEP_DIAG")) L.sweep_diag = atoi(e);
     h->bytes_t += (s.m + s.n) * h->esz;  // x read once, y written once
     return VBC_OK;
 }
@@ -1663,7 +1663,7 @@ static bool build_fwd_runs(vbc_handle *h, int w, int R, const std::vector<Entry>
         }
     }
     rrow.push_back((int32_t)rows);
-    if (getenv("VBC_VERBOSE"))
+    if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] forward runs bin w %d R %d segments %lld chunks %lld rows %lld (real %lld) mask %d sorted %d "
                 "split %d ranges %zu\n", w, R, (long long)nseg, (long long)nch, (long long)rows, (long long)real, (int)mask,
                 (int)(!order.empty() && !mask), split, rchunk.size());
@@ -1852,7 +1852,7 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
                 Ls.emplace_back();
                 Ls.back().sweep_tiles = tile0;
                 Ls.back().sweep_tile_bytes = h->sweep_tile;
-                if (const char *e = getenv("VBC_SWEEP_DIAG")) Ls.back().sweep_diag = atoi(e);
+                if (const char *e = ablation_knob("VBC_SWEEP_DIAG")) Ls.back().sweep_diag = atoi(e);
                 pbs.push_back({});
                 pss.push_back({});
                 pws.push_back({pw});
@@ -1939,87 +1939,10 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
 
 struct PendingPanel {
     PanelBin b;
-    QuadBin qb;  // quad: a stripe-quad bucket (o_rgrp = its chunk rows)
-    bool quad;
     TileBin tb;  // tile: a small-tile bucket (vbc_tiles.h; o_rgrp = its range table)
     bool tile = false;
     size_t o_key, o_val, o_out, o_rgrp, o_rseg;
-    size_t o_xrow = 0;  // staged tile bucket: the clusters' row groups
-    size_t o_wg = 0;    // staged tile bucket: per persistent workgroup {first cluster, clusters}
-    size_t zoff = 0;    // staged tile bucket: byte offset of >= 16 zero bytes in the value array (its padding)
 };
-
-// Stripe-quad bucket (vbc_panel.h spmm_quads): chunks of 16 stripes of width w <= 8, chunk rows = its
-// longest stripe's, rows x 16 keys (x row or kPanelSentinel) and rows x 16 x w values.  Natural stripe
-// order when the chunks pad <= slots_pad, else by decreasing length inside windows of 32 chunks.
-// pcs: the bucket's pieces (stripe, first column of the piece inside it).
-static void build_quads(vbc_handle *h, const Stripes &s, const std::vector<std::pair<int64_t, int>> &pcs, int w,
-                        const char *val, Arena &ar, PendingPanel &pp)
-{
-    std::vector<int64_t> stripes;
-    for (const auto &pc : pcs) stripes.push_back(pc.first);
-    const int esz = h->esz;
-    const int64_t n = (int64_t)stripes.size();
-    std::vector<int64_t> sbeg{0};
-    for (int64_t l : stripes) sbeg.push_back(sbeg.back() + s.rbeg[l + 1] - s.rbeg[l]);
-    std::vector<int64_t> order;
-    auto padded = [&](const std::vector<int64_t> &sb) {
-        int64_t rows = 0;
-        for (int32_t c : chunk_rows(sb, 16)) rows += c;
-        return rows * 16;
-    };
-    if ((double)padded(sbeg) > h->slots_pad * (double)std::max<int64_t>(sbeg[n], 1)) order = sorted_order(sbeg, 16);
-    std::vector<int64_t> ord(n);
-    for (int64_t i = 0; i < n; i++) ord[i] = order.empty() ? i : order[i];
-    const int64_t nch = (n + 15) / 16;
-    std::vector<int32_t> crow{0}, out(n);
-    for (int64_t c = 0; c < nch; c++) {
-        int64_t len = 0;
-        for (int64_t i = c * 16; i < std::min(n, c * 16 + 16); i++) {
-            const int64_t l = stripes[ord[i]];
-            len = std::max<int64_t>(len, s.rbeg[l + 1] - s.rbeg[l]);
-        }
-        crow.push_back((int32_t)(crow.back() + len));
-    }
-    for (int64_t i = 0; i < n; i++) out[i] = (int32_t)(s.col0[stripes[ord[i]]] + pcs[ord[i]].second);
-    const int64_t rows = crow.back();
-    pp = PendingPanel{};
-    pp.quad = true;
-    QuadBin &b = pp.qb;
-    b.w = w;
-    b.nchunks = (int32_t)nch;
-    b.nseg = (int32_t)n;
-    b.out_affine = 1;
-    b.out_base = n > 0 ? out[0] : 0;
-    b.out_stride = n > 1 ? out[1] - out[0] : 0;
-    for (int64_t i = 1; i < n && b.out_affine; i++) b.out_affine = (int64_t)out[i] == (int64_t)out[0] + i * b.out_stride;
-    pp.o_key = ar.reserve(std::max<int64_t>(rows, 1) * 16 * 4);
-    pp.o_val = ar.reserve(std::max<int64_t>(rows, 1) * 16 * w * esz);
-    pp.o_out = ar.reserve(std::max<int64_t>(n, 1) * 4);
-    pp.o_rgrp = ar.reserve(crow.size() * 4);
-    std::memcpy(ar.at<int32_t>(pp.o_out), out.data(), out.size() * 4);
-    std::memcpy(ar.at<int32_t>(pp.o_rgrp), crow.data(), crow.size() * 4);
-    uint32_t *key = ar.at<uint32_t>(pp.o_key);
-    char *vv = ar.at<char>(pp.o_val);
-    for (int64_t c = 0; c < nch; c++)
-        for (int64_t r = crow[c]; r < crow[c + 1]; r++)
-            for (int sl = 0; sl < 16; sl++) {
-                const int64_t i = c * 16 + sl, e = r * 16 + sl, k = r - crow[c];
-                const int64_t l = i < n ? stripes[ord[i]] : -1;
-                if (l >= 0 && s.rbeg[l] + k < s.rbeg[l + 1]) {
-                    key[e] = (uint32_t)s.rows[s.rbeg[l] + k];
-                    std::memcpy(vv + e * w * esz, val + (s.voff[l] + k * s.w[l] + pcs[ord[i]].second) * esz,
-                                (size_t)w * esz);
-                } else {
-                    key[e] = kPanelSentinel;
-                    std::memset(vv + e * w * esz, 0, (size_t)w * esz);
-                }
-            }
-    h->bytes_m += rows * 16 * (4 + (int64_t)w * esz) + n * 4;
-    if (getenv("VBC_VERBOSE"))
-        fprintf(stderr, "[vbc] stripe quads: w %d, %lld stripes, %lld chunks, %lld rows (%s order, %lld real)\n", w,
-                (long long)n, (long long)nch, (long long)rows, order.empty() ? "natural" : "sorted", (long long)sbeg[n]);
-}
 
 // Tile layout (vbc_tiles.h) of one width bucket (w <= 4, whole stripes) of the multi-RHS product: each
 // stripe's stored rows grouped into tiles of consecutive rows of one row group -- Π's block rows (tgrp:
@@ -2035,7 +1958,7 @@ constexpr double kTilePad = 1.25;
 static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64_t> &stripes_in, int w,
                         const std::vector<int64_t> *tgrp, const char *val, Arena &ar, PendingPanel &pp)
 {
-    std::vector<int64_t> stripes = stripes_in;  // (processing order: natural, or blob order below)
+    const std::vector<int64_t> &stripes = stripes_in;  // (natural order)
     if (h->panel_tiles == 0 || w < 1 || w > 4 || stripes.empty() || s.m >= (int64_t)kTileRow) return false;
     for (int64_t l : stripes)
         if (s.w[l] != w || s.vstride(l) != w) return false;
@@ -2108,78 +2031,6 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
     if (h->panel_tiles < 0 && (double)rows < 1.5 * (double)std::max<int64_t>(tiles, 1)) return false;
     const int TV = ub * w;
     const int64_t n = (int64_t)stripes.size();
-    // Blob order (VBC_TILE_ORDER=1): the stripes are processed in compact blobs of the stripe graph
-    // (two stripes adjacent when they store tiles of one row group, i.e. gather the same X rows): each
-    // blob a BFS ball of tile_blob stripes from a seed on the previous blob's frontier.  A 3D mesh's
-    // natural order reuses an X row across +-g^2 stripes (three planes), beyond what an XCD's L2 holds
-    // while the front of concurrent stripes sweeps on; compact blobs keep a stripe's X rows within a
-    // few consecutive blobs.  Outputs are unaffected (each stripe writes its own columns).
-    if (h->tile_order == 1 && n > h->tile_blob) {
-        std::vector<int64_t> sgb(n + 1, 0), sg;  // per stripe: its groups (base rows)
-        for (int64_t i = 0; i < n; i++) {
-            const int64_t l = stripes[i];
-            int64_t cb = -1;
-            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
-                int64_t base;
-                int u;
-                group_of(s.rows[q], R, base, u);
-                if (base != cb) sg.push_back(base);
-                cb = base;
-            }
-            sgb[i + 1] = (int64_t)sg.size();
-        }
-        std::vector<int64_t> gsb(s.m + 1, 0), gs(sg.size());  // per group (base row): its stripes
-        for (int64_t g : sg) gsb[g + 1]++;
-        for (int64_t r = 0; r < s.m; r++) gsb[r + 1] += gsb[r];
-        {
-            std::vector<int64_t> at(gsb.begin(), gsb.end() - 1);
-            for (int64_t i = 0; i < n; i++)
-                for (int64_t e = sgb[i]; e < sgb[i + 1]; e++) gs[at[sg[e]]++] = i;
-        }
-        std::vector<char> taken(n, 0);
-        std::vector<int64_t> mark_s(n, -1), mark_g(s.m, -1), order, queue;
-        order.reserve(n);
-        int64_t scan = 0, seed = -1, blob = 0;
-        const int64_t C = h->tile_blob;
-        while ((int64_t)order.size() < n) {
-            if (seed < 0 || taken[seed]) {
-                while (taken[scan]) scan++;
-                seed = scan;
-            }
-            queue.assign(1, seed);
-            mark_s[seed] = blob;
-            int64_t cnt = 0, next = -1;
-            for (size_t hd = 0; hd < queue.size(); hd++) {
-                const int64_t st = queue[hd];
-                if (cnt == C) {  // the ball is full: the first frontier stripe seeds the next blob
-                    next = st;
-                    break;
-                }
-                order.push_back(st);
-                taken[st] = 1;
-                cnt++;
-                for (int64_t e = sgb[st]; e < sgb[st + 1]; e++) {
-                    const int64_t g = sg[e];
-                    if (mark_g[g] == blob) continue;
-                    mark_g[g] = blob;
-                    for (int64_t f = gsb[g]; f < gsb[g + 1]; f++) {
-                        const int64_t t = gs[f];
-                        if (!taken[t] && mark_s[t] != blob) {
-                            mark_s[t] = blob;
-                            queue.push_back(t);
-                        }
-                    }
-                }
-            }
-            seed = next;
-            blob++;
-        }
-        std::vector<int64_t> re(n);
-        for (int64_t i = 0; i < n; i++) re[i] = stripes[order[i]];
-        stripes.swap(re);
-        if (getenv("VBC_VERBOSE"))
-            fprintf(stderr, "[vbc] tiles: blob order, %lld blobs of <= %lld stripes\n", (long long)blob, (long long)C);
-    }
     std::vector<int64_t> tl(n);  // tiles per stripe (an empty stripe: one invalid LAST tile)
     {
         for (int64_t i = 0; i < n; i++) {
@@ -2201,279 +2052,8 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
             tl[i] = std::max<int64_t>(t, 1);
         }
     }
-    // Staged-X form (round 5b, vbc_tiles.h spmm_tiles_x): clusters of stripes that gather the same row groups,
-    // one workgroup each, the cluster's distinct row groups staged in LDS once per product.  A cluster is a
-    // BFS ball of the stripe graph (two stripes adjacent when they store tiles of one row group), grown from
-    // a seed on the previous cluster's frontier (consecutive clusters -- one XCD's run of workgroups -- share
-    // their border groups in L2) until it holds tile_smax stripes or its groups would pass the LDS stage.
-    // Auto (tile_stage < 0): only when the clusters gather each staged group >= tile_reuse times.
-    if (h->tile_stage != 0) {
-        constexpr int NB = kTileXBatch, D = kTileXDepth;
-        // fp32: the persistent kernel (spmm_tiles_xp) double-buffers both LDS stages, so its clusters are smaller;
-        // else (spmm_tiles_x) fp32 clusters are run by 8 compute waves (two 80 KB workgroups per CU), fp64 by 4
-        const bool persist = h->tile_persist && esz == 4;
-        const int NWv = persist || esz != 4 ? 4 : std::max(4, std::min(kTileXMaxWaves, h->tile_waves)) / 4 * 4;
-        const int NS = 4 * NWv, NT = 64 * NWv;
-        const int64_t ldscap = NWv == 8 ? kTileXLds8 : kTileXLds;
-        // stripes per cluster: the kernels' epilogues hold kTileXOutPieces 16-B output pieces per thread (the
-        // persistent writer wave kTileXPOut per lane)
-        int64_t Smax = h->tile_smax > 0 ? h->tile_smax : (persist ? 48 : NWv == 8 ? 128 : 64);
-        Smax = std::min<int64_t>(Smax, (int64_t)kTileXOutPieces * NT * 16 / ((int64_t)w * 16 * esz));
-        if (persist) Smax = std::min<int64_t>(Smax, (int64_t)kTileXPOut * 64 * 16 / ((int64_t)w * 16 * esz));
-        Smax = std::max<int64_t>(1, Smax);
-        const int64_t stage = (Smax * w * 16 * esz + 15) / 16 * 16;
-        const int64_t slot_b = (int64_t)ub * 16 * esz;
-        // the LDS stage, and the kernels' staging pieces per thread (16-B pieces: (U + 1) x ub x 16 elements)
-        int64_t Umax = h->tile_umax > 0 ? h->tile_umax : (persist ? 160 : NWv == 8 ? 256 : 192);
-        Umax = std::min<int64_t>({Umax, (ldscap - stage) / slot_b - 1, (int64_t)tile_x_pieces(NWv) * NT * 16 / slot_b - 1,
-                                  (int64_t)kTileXSlot - 1});
-        if (persist)  // both stages double-buffered in the CU's LDS share of one of tile_wgpc workgroups
-            Umax = std::min<int64_t>({Umax, (kTileXPLds / std::max(1, h->tile_wgpc) - 2 * stage - 128) / (2 * slot_b) - 1,
-                                      (int64_t)kTileXPLoad * 64 * 16 / slot_b - 1});
-        std::vector<int64_t> sgb(n + 1, 0), sg;  // per stripe: its row groups (base rows), stored order
-        for (int64_t i = 0; i < n; i++) {
-            const int64_t l = stripes[i];
-            int64_t cb = -1;
-            for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
-                int64_t base;
-                int u;
-                group_of(s.rows[q], R, base, u);
-                if (base != cb) sg.push_back(base);
-                cb = base;
-            }
-            sgb[i + 1] = (int64_t)sg.size();
-        }
-        std::vector<int64_t> gsb(s.m + 1, 0), gs(sg.size());  // per group: its stripes
-        for (int64_t g : sg) gsb[g + 1]++;
-        for (int64_t r = 0; r < s.m; r++) gsb[r + 1] += gsb[r];
-        {
-            std::vector<int64_t> at(gsb.begin(), gsb.end() - 1);
-            for (int64_t i = 0; i < n; i++)
-                for (int64_t e = sgb[i]; e < sgb[i + 1]; e++) gs[at[sg[e]]++] = i;
-        }
-        std::vector<char> taken(n, 0);
-        std::vector<int64_t> mark_s(n, -1), mark_g(s.m, -1), corder, cbeg{0}, queue, ug;
-        std::vector<int32_t> xrow, xbeg{0};
-        corder.reserve(n);
-        int64_t scan = 0, seed = -1, cid = 0;
-        bool fits = Umax >= 1;
-        while (fits && (int64_t)corder.size() < n) {
-            if (seed < 0 || taken[seed]) {
-                while (taken[scan]) scan++;
-                seed = scan;
-            }
-            queue.assign(1, seed);
-            mark_s[seed] = cid;
-            ug.clear();
-            int64_t cnt = 0, next = -1;
-            for (size_t hd = 0; hd < queue.size(); hd++) {
-                const int64_t st = queue[hd];
-                int64_t add = 0;
-                for (int64_t e = sgb[st]; e < sgb[st + 1]; e++) add += mark_g[sg[e]] != cid;
-                if (cnt == Smax || (int64_t)ug.size() + add > Umax) {
-                    if (cnt == 0) fits = false;  // one stripe's groups exceed the stage
-                    next = st;
-                    break;
-                }
-                corder.push_back(st);
-                taken[st] = 1;
-                cnt++;
-                for (int64_t e = sgb[st]; e < sgb[st + 1]; e++) {
-                    const int64_t gg = sg[e];
-                    if (mark_g[gg] == cid) continue;
-                    mark_g[gg] = cid;
-                    ug.push_back(gg);
-                    for (int64_t f = gsb[gg]; f < gsb[gg + 1]; f++) {
-                        const int64_t t = gs[f];
-                        if (!taken[t] && mark_s[t] != cid) {
-                            mark_s[t] = cid;
-                            queue.push_back(t);
-                        }
-                    }
-                }
-            }
-            std::sort(ug.begin(), ug.end());
-            for (int64_t gg : ug) xrow.push_back((int32_t)gg);
-            xbeg.push_back((int32_t)xrow.size());
-            cbeg.push_back((int64_t)corder.size());
-            seed = next;
-            cid++;
-        }
-        int64_t ttl = 0;
-        for (int64_t t : tl) ttl += t;
-        const double reuse = fits ? (double)ttl / (double)std::max<size_t>(xrow.size(), 1) : 0.0;
-        if (getenv("VBC_VERBOSE"))
-            fprintf(stderr, "[vbc] tiles: staged X %s: %lld clusters of <= %lld stripes, %zu staged groups, %.2f tiles per group\n",
-                    fits ? "fits" : "does not fit", (long long)cid, (long long)Smax, xrow.size(), reuse);
-        if (fits && (h->tile_stage > 0 || reuse >= h->tile_reuse)) {
-            const int64_t nc = cid;
-            // Workgroups of the persistent kernel (spmm_tiles_xp): nwg (a multiple of 8 when >= 8), each taking a
-            // sequence of clusters.  The clusters are cut into 8 contiguous runs (BFS order: neighbours), one per
-            // XCD (xcd_block maps the logical workgroups of XCD x to a contiguous block), and run x's j-th cluster
-            // goes to that XCD's workgroup j mod n_x: at any time an XCD's workgroups hold consecutive clusters.
-            int64_t nwg = std::min<int64_t>(nc, (int64_t)h->cus * std::max(1, h->tile_wgpc));
-            if (nwg >= 8) nwg = nwg / 8 * 8;
-            std::vector<std::vector<int64_t>> wgc(nwg);
-            {
-                const int64_t parts = nwg >= 8 ? 8 : 1;
-                for (int64_t x = 0; x < parts; x++) {
-                    const int64_t c0 = x * nc / parts, c1 = (x + 1) * nc / parts;
-                    const int64_t w0 = x * nwg / parts, nx = (x + 1) * nwg / parts - w0;
-                    for (int64_t c = c0; c < c1; c++) wgc[w0 + (c - c0) % nx].push_back(c);
-                }
-            }
-            // per cluster: streams (LPT), sorted so wave k takes streams 4k .. 4k+3; its segment = the longest of
-            // its four in whole batches (at least one: every wave meets every cluster's END)
-            std::vector<std::array<std::vector<int64_t>, kTileXMaxStreams>> csm(nc);
-            std::vector<std::array<int64_t, kTileXMaxWaves>> clen(nc);
-            for (int64_t c = 0; c < nc; c++) {
-                std::vector<int64_t> byl(corder.begin() + cbeg[c], corder.begin() + cbeg[c + 1]);
-                std::stable_sort(byl.begin(), byl.end(), [&](int64_t x, int64_t y) { return tl[x] > tl[y]; });
-                std::vector<int64_t> load(NS, 0);
-                std::vector<std::vector<int64_t>> sm(NS);
-                for (int64_t i : byl) {  // longest first to the least loaded stream
-                    const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-                    load[k] += tl[i];
-                    sm[k].push_back(i);
-                }
-                std::vector<int> so(NS);
-                for (int k = 0; k < NS; k++) so[k] = k;
-                std::stable_sort(so.begin(), so.end(), [&](int x, int y) { return load[x] > load[y]; });
-                for (int k = 0; k < NS; k++) csm[c][k] = std::move(sm[so[k]]);
-                for (int wv = 0; wv < NWv; wv++)
-                    clen[c][wv] = std::max<int64_t>(NB, (load[so[4 * wv]] + NB - 1) / NB * NB);
-            }
-            // cinfo in workgroup order; per workgroup and wave one contiguous stream per row (its clusters'
-            // segments back to back), row g at base + g x Ltot
-            std::vector<int32_t> cinfo((size_t)nc * kTileXInfo, 0), out(n), wginfo((size_t)nwg * 2, 0);
-            std::vector<int64_t> lorder(n), cof(nc);  // position -> stripe index; new cluster index -> old
-            int64_t slot_total = 0, most_s = 1, most_u = 0, pos = 0, ci_n = 0;
-            for (int64_t L = 0; L < nwg; L++) {
-                wginfo[2 * L] = (int32_t)ci_n;
-                wginfo[2 * L + 1] = (int32_t)wgc[L].size();
-                std::array<int64_t, kTileXMaxWaves> base{}, ltot{}, off{};
-                for (int wv = 0; wv < NWv; wv++) {
-                    for (int64_t c : wgc[L]) ltot[wv] += clen[c][wv];
-                    base[wv] = slot_total;
-                    slot_total += 4 * ltot[wv];
-                }
-                if (slot_total >= (int64_t(1) << 31) / std::max(1, TV)) return false;
-                for (int64_t c : wgc[L]) {
-                    int32_t *ci = &cinfo[(size_t)ci_n * kTileXInfo];
-                    cof[ci_n++] = c;
-                    ci[0] = (int32_t)pos;
-                    ci[1] = (int32_t)(cbeg[c + 1] - cbeg[c]);
-                    ci[2] = xbeg[c + 1] - xbeg[c];
-                    ci[3] = xbeg[c];
-                    for (int k = 0; k < NS; k++) {
-                        ci[kXiSidx + k] = (int32_t)(pos - ci[0]);
-                        for (int64_t i : csm[c][k]) lorder[pos++] = i;
-                    }
-                    for (int wv = 0; wv < NWv; wv++) {
-                        ci[kXiStride + wv] = (int32_t)ltot[wv];
-                        ci[kXiSeg + wv] = (int32_t)(base[wv] + off[wv]);
-                        ci[kXiLen + wv] = (int32_t)clen[c][wv];
-                        off[wv] += clen[c][wv];
-                    }
-                    most_s = std::max<int64_t>(most_s, ci[1]);
-                    most_u = std::max<int64_t>(most_u, ci[2]);
-                }
-            }
-            for (int64_t q = 0; q < n; q++) out[q] = (int32_t)s.col0[stripes[lorder[q]]];
-            const int64_t kpad = (D + 1) * NB + 16, vpad = (int64_t)((D + 1) * NB + 2) * TV + 64;
-            pp = PendingPanel{};
-            pp.tile = true;
-            TileBin &tb = pp.tb;
-            tb.w = w;
-            tb.ub = ub;
-            tb.nbt = NB;
-            tb.staged = 1;
-            if (const char *e = getenv("VBC_TILE_DIAG")) tb.diag = atoi(e);  // (ablations, tools/ab.py)
-            tb.xslots = (int32_t)(most_u + 1);
-            tb.stage_bytes = (int32_t)((most_s * w * 16 * esz + 15) / 16 * 16);
-            tb.nranges = (int32_t)nc;
-            tb.nwg = persist ? (int32_t)nwg : 0;
-            tb.nwaves = NWv;
-            tb.out_affine = 0;
-            pp.o_key = ar.reserve((slot_total + kpad) * 4);
-            pp.o_val = ar.reserve((slot_total * TV + vpad) * esz);
-            pp.zoff = (size_t)((slot_total * TV + vpad) * esz - 64) / 16 * 16;
-            pp.o_out = ar.reserve(n * 4);
-            pp.o_rgrp = ar.reserve(cinfo.size() * 4);
-            pp.o_wg = ar.reserve(wginfo.size() * 4);
-            xrow.push_back(0);  // the kernel reads slot U's row (unused): one entry past the last cluster's
-            pp.o_xrow = ar.reserve(xrow.size() * 4);
-            std::memcpy(ar.at<int32_t>(pp.o_out), out.data(), out.size() * 4);
-            std::memcpy(ar.at<int32_t>(pp.o_rgrp), cinfo.data(), cinfo.size() * 4);
-            std::memcpy(ar.at<int32_t>(pp.o_wg), wginfo.data(), wginfo.size() * 4);
-            std::memcpy(ar.at<int32_t>(pp.o_xrow), xrow.data(), xrow.size() * 4);
-            uint32_t *key = ar.at<uint32_t>(pp.o_key);
-            char *vv = ar.at<char>(pp.o_val);
-            std::fill(key, key + slot_total + kpad, 0u);
-            std::memset(vv, 0, (size_t)(slot_total * TV + vpad) * esz);
-            bool masku = false;
-            std::vector<int32_t> gslot(s.m, -1);
-            for (int64_t cn = 0; cn < nc; cn++) {
-                const int32_t *ci = &cinfo[(size_t)cn * kTileXInfo];
-                const int64_t c = cof[cn];
-                const uint32_t U = (uint32_t)ci[2];
-                for (int32_t x = xbeg[c]; x < xbeg[c + 1]; x++) gslot[xrow[x]] = x - xbeg[c];
-                for (int k = 0; k < NS; k++) {
-                    const int64_t len = ci[kXiLen + k / 4];
-                    int64_t slot = ci[kXiSeg + k / 4] + (int64_t)(k % 4) * ci[kXiStride + k / 4];
-                    const int64_t first = slot;
-                    for (int64_t i : csm[c][k]) {
-                        const int64_t l = stripes[i];
-                        if (s.rbeg[l + 1] == s.rbeg[l]) {  // empty stripe: one zero-slot LAST tile
-                            key[slot++] = kTileLast | U;
-                            continue;
-                        }
-                        int64_t cb = -1;
-                        unsigned seen = 0;
-                        for (int64_t q = s.rbeg[l]; q < s.rbeg[l + 1]; q++) {
-                            int64_t base;
-                            int u;
-                            group_of(s.rows[q], R, base, u);
-                            const int rr = (int)(s.rows[q] - base);
-                            const unsigned bit = 1u << rr;
-                            if (base != cb || (seen & bit)) {
-                                if (cb >= 0) {
-                                    key[slot] = (uint32_t)gslot[cb] | (seen << kTileMaskShift);
-                                    masku = masku || seen != (1u << ub) - 1;
-                                    slot++;
-                                }
-                                cb = base;
-                                seen = 0;
-                            }
-                            seen |= bit;
-                            std::memcpy(vv + (slot * TV + (int64_t)rr * w) * esz,
-                                        val + (s.voff[l] + (q - s.rbeg[l]) * w) * esz, (size_t)w * esz);
-                        }
-                        key[slot] = (uint32_t)gslot[cb] | (seen << kTileMaskShift) | kTileLast;
-                        masku = masku || seen != (1u << ub) - 1;
-                        slot++;
-                    }
-                    for (; slot < first + len; slot++) key[slot] = U;  // padding: the zero slot
-                    key[first + len - 1] |= kTileXEnd;                 // the segment's last tile
-                }
-            }
-            tb.masku = masku ? 1 : 0;
-            h->bytes_m += slot_total * (4 + (int64_t)TV * esz) + (int64_t)xrow.size() * (4 + slot_b) + nc * kTileXInfo * 4;
-            if (getenv("VBC_VERBOSE"))
-                fprintf(stderr, "[vbc] tiles: staged X, w %d, ub %d: %lld clusters on %lld workgroups, <= %lld stripes and %lld groups each, %lld slots%s\n",
-                        w, ub, (long long)nc, (long long)nwg, (long long)most_s, (long long)most_u, (long long)slot_total,
-                        masku ? ", masked rows" : "");
-            return true;
-        }
-    }
     // ranges: <= smax stripes (the LDS stage), a whole number of rounds of resident waves, balanced by tiles
-    // (the 16-B fp32 form stages every slot row's partial sums: ub x the outputs of a stripe)
-#ifdef VBC_TILE_REDUCE_DPP
-    const int stage_rows = 1;
-#else
-    const int stage_rows = esz == 4 && h->tile_x4 ? ub : 1;
-#endif
-    const int64_t smax = std::max<int64_t>(1, kTileStageBytes / (w * 16 * esz * stage_rows));
+    const int64_t smax = std::max<int64_t>(1, kTileStageBytes / (w * 16 * esz));
     const int64_t slots = (int64_t)h->cus * std::max(1, h->occ_tiles);
     int64_t total = 0;
     for (int64_t t : tl) total += t;
@@ -2491,7 +2071,7 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
         nr = std::min<int64_t>(nr_cap, (nr + slots - 1) / slots * slots);
     }
     nr = std::min<int64_t>(n, nr);
-    if (const char *e = getenv("VBC_TILE_RANGES")) nr = std::min<int64_t>(n, std::max<int64_t>(1, atoll(e)));
+    if (const char *e = tuning_knob("VBC_TILE_RANGES")) nr = std::min<int64_t>(n, std::max<int64_t>(1, atoll(e)));
     std::vector<int64_t> rb{0};  // range starts (stripe index)
     {
         int64_t cum = 0;
@@ -2544,12 +2124,11 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
     tb.w = w;
     tb.ub = ub;
     tb.nbt = nbt;
-    if (const char *e = getenv("VBC_TILE_DIAG")) tb.diag = atoi(e);
+    if (const char *e = ablation_knob("VBC_TILE_DIAG")) tb.diag = atoi(e);
     {
         int64_t most = 1;
         for (size_t r = 0; r + 1 < rb.size(); r++) most = std::max<int64_t>(most, rb[r + 1] - rb[r]);
-        // (the 16-B fp32 form stages every slot row's partial sums: ub x the outputs)
-        tb.stage_bytes = (int32_t)((most * w * 16 * esz * (stage_rows > 1 ? ub : 1) + 15) / 16 * 16);
+        tb.stage_bytes = (int32_t)((most * w * 16 * esz + 15) / 16 * 16);
     }
     tb.nranges = (int32_t)nrg;
     std::vector<int32_t> out(n);
@@ -2610,7 +2189,7 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
     }
     tb.masku = masku ? 1 : 0;
     h->bytes_m += slot_total * (4 + (int64_t)TV * esz) + nrg * 32;
-    if (getenv("VBC_VERBOSE"))
+    if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] tiles: w %d, %lld stripes, %lld rows -> %lld tiles of <= %d rows (%s), %lld ranges, %lld slots%s\n",
                 w, (long long)n, (long long)rows, (long long)total, ub, R == 0 ? "block rows" : "row runs", (long long)nrg,
                 (long long)slot_total, masku ? ", masked rows" : "");
@@ -2655,9 +2234,7 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     // groups of every bucket first: ranges are spread over the launch in proportion to them
     std::map<int, std::vector<int64_t>> pgroups;  // w -> groups per panel
     int64_t total_groups = 0;
-    auto quads = [&](int w) { return w <= h->panel_quads && w <= 8; };  // VALU stripe quads (spmm_quads)
     for (auto &kv : buckets) {
-        if (quads(kv.first)) continue;
         const int S = 16 / kv.first;
         auto &pg = pgroups[kv.first];
         for (size_t p0 = 0; p0 < kv.second.size(); p0 += S) {
@@ -2671,14 +2248,6 @@ static int build_panel(vbc_handle *h, const Stripes &s, const char *val, Arena &
     if (total_groups >= (int64_t(1) << 31)) return fail(VBC_INVALID_ARG, "matrix too large for the panel layout");
     int range0 = 0;
     for (auto &kv : buckets) {
-        if (quads(kv.first)) {  // w <= 8: whole stripes, or the last piece of a stripe wider than 16
-            std::vector<std::pair<int64_t, int>> st;
-            for (const Piece &pc : kv.second) st.emplace_back(pc.l, pc.c0);
-            PendingPanel pp;
-            build_quads(h, s, st, kv.first, val, ar, pp);
-            pps.push_back(pp);
-            continue;
-        }
         const int w = kv.first, S = 16 / w;
         const std::vector<Piece> &pcs = kv.second;
         const std::vector<int64_t> &pg = pgroups[w];
@@ -2894,7 +2463,6 @@ static int build_forward_panel(vbc_handle *h, const Stripes &s, const char *val,
 static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, PanelLaunch &L)
 {
     L.bins.clear();
-    L.qbins.clear();
     L.tbins.clear();
     char *base = static_cast<char *>(h->d_arena);
     for (const PendingPanel &pp : pps) {
@@ -2904,20 +2472,7 @@ static int finalize_panel(vbc_handle *h, const std::vector<PendingPanel> &pps, P
             t.val = base + pp.o_val;
             t.out = reinterpret_cast<const int32_t *>(base + pp.o_out);
             t.rinfo = reinterpret_cast<const int32_t *>(base + pp.o_rgrp);
-            t.xrow = t.staged ? reinterpret_cast<const int32_t *>(base + pp.o_xrow) : nullptr;
-            t.wginfo = t.staged ? reinterpret_cast<const int32_t *>(base + pp.o_wg) : nullptr;
-            // (a zero 16-B source for the persistent kernel's LDS-DMA staging: the value array's padding)
-            t.zsrc = t.staged ? base + pp.o_val + pp.zoff : nullptr;
             L.tbins.push_back(t);
-            continue;
-        }
-        if (pp.quad) {
-            QuadBin q = pp.qb;
-            q.key = reinterpret_cast<const uint32_t *>(base + pp.o_key);
-            q.val = base + pp.o_val;
-            q.out = reinterpret_cast<const int32_t *>(base + pp.o_out);
-            q.crow = reinterpret_cast<const int32_t *>(base + pp.o_rgrp);
-            L.qbins.push_back(q);
             continue;
         }
         PanelBin b = pp.b;
@@ -3172,52 +2727,52 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { release(h); return fail(VBC_HIP_ERROR, "hipGetDeviceProperties failed"); }
     h->tile_k = dtype == VBC_F64 ? 4 : 8;  // measured best (tools/ab.py, FE workload)
-    if (const char *e = getenv("VBC_TILE_K")) {
+    if (const char *e = tuning_knob("VBC_TILE_K")) {
         const int k = atoi(e);
         h->tile_k = (k == 4 || k == 8) ? k : h->tile_k;
     }
-    if (const char *e = getenv("VBC_PIPE")) h->pipe = atoi(e) == 3 ? 3 : 2;
-    if (const char *e = getenv("VBC_DIAG")) h->diag = atoi(e);
+    if (const char *e = tuning_knob("VBC_PIPE")) h->pipe = atoi(e) == 3 ? 3 : 2;
+    if (const char *e = ablation_knob("VBC_DIAG")) h->diag = atoi(e);
     // one range per resident wave: occupancy of the kernel variant this handle will launch
     int occ[2] = {0, 0};
     occupancy_ranges(h->esz, h->tile_k, h->pipe, occ);
     for (int kd = 0; kd < 2; kd++)
         h->target_ranges_k[kd] = prop.multiProcessorCount * std::max(1, std::min(occ[kd], 8)) * kWavesPerBlock;
-    if (const char *e = getenv("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
+    if (const char *e = tuning_knob("VBC_TARGET_RANGES")) h->target_ranges_k[0] = h->target_ranges_k[1] = std::max(1, atoi(e));
     for (int kd = 0; kd < 2; kd++) {
         h->occ_s[kd] = std::max(1, std::min(occupancy_slots(h->esz, kd), 8));
         h->target_ranges_s[kd] = prop.multiProcessorCount * h->occ_s[kd] * kWavesPerBlock;
     }
-    if (const char *e = getenv("VBC_TARGET_RANGES_S")) {  // an explicit range count is taken as is
+    if (const char *e = tuning_knob("VBC_TARGET_RANGES_S")) {  // an explicit range count is taken as is
         h->target_ranges_s[0] = h->target_ranges_s[1] = std::max(1, atoi(e));
         h->occ_s[0] = h->occ_s[1] = 1;
     }
-    if (const char *e = getenv("VBC_RANGE_KB")) h->range_bytes = (int64_t)std::max(0, atoi(e)) << 10;
-    if (const char *e = getenv("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
-    if (const char *e = getenv("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
-    if (const char *e = getenv("VBC_SLOTS_SORT")) h->slots_sort = atoi(e);
-    if (const char *e = getenv("VBC_SLOT_NARROW")) h->slot_narrow = atoi(e) != 0;
-    if (const char *e = getenv("VBC_XCD")) h->xcd = atoi(e) != 0;
-    if (const char *e = getenv("VBC_XCD_P")) h->xcd_p = atoi(e) != 0;
-    if (const char *e = getenv("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
-    if (const char *e = getenv("VBC_SLOT_DEDUP")) h->slot_dedup = atoi(e) != 0;
-    if (const char *e = getenv("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = layout_knob("VBC_RANGE_KB")) h->range_bytes = (int64_t)std::max(0, atoi(e)) << 10;
+    if (const char *e = layout_knob("VBC_SLOTS")) h->slots_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = layout_knob("VBC_SLOTS_PAD")) h->slots_pad = atof(e);
+    if (const char *e = layout_knob("VBC_SLOTS_SORT")) h->slots_sort = atoi(e);
+    if (const char *e = tuning_knob("VBC_SLOT_NARROW")) h->slot_narrow = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_XCD")) h->xcd = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_XCD_P")) h->xcd_p = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
+    if (const char *e = layout_knob("VBC_SLOT_DEDUP")) h->slot_dedup = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     h->sweep_tile = (h->esz == 8 ? 4 : 2) * kSweepTileBytes;  // measured on NS: fp64 32 KB 473 us (16 KB 508), fp32 16 KB 313 us (32 KB 353)
     // packed swept keys: NS fp64 464.5 -> 456.2 us, mixed widths 553 -> 539 us; fp32 311 -> 316 us, so
     // fp64 only (profiles/r03_sweeppack_*.log)
     h->sweep_pack = h->esz == 8;
-    if (const char *e = getenv("VBC_FORK")) h->fork = atoi(e) != 0;
-    if (const char *e = getenv("VBC_FORK_SIDE_KB")) h->fork_side_bytes = atof(e) * 1024.0;
-    if (const char *e = getenv("VBC_SWEEP_PACK")) h->sweep_pack = atoi(e) != 0;
-    if (const char *e = getenv("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
-    if (const char *e = getenv("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
-    if (const char *e = getenv("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
-    if (const char *e = getenv("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
-    if (const char *e = getenv("VBC_PLANAR_PAIR")) h->planar_pair = atoi(e) == 0 ? 0 : atoi(e) == 2 ? 2 : 1;  // 2: always
-    if (const char *e = getenv("VBC_PLANAR_MASK")) h->planar_mask = atoi(e) != 0;
-    if (const char *e = getenv("VBC_PLANAR_MASK_PAIR")) h->planar_mask_pair = atoi(e) != 0;
-    if (const char *e = getenv("VBC_MASK_WINDOW")) h->mask_window = std::max(1, std::min(64, atoi(e)));
-    if (const char *e = getenv("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
+    if (const char *e = layout_knob("VBC_FORK")) h->fork = atoi(e) != 0;
+    if (const char *e = tuning_knob("VBC_FORK_SIDE_KB")) h->fork_side_bytes = atof(e) * 1024.0;
+    if (const char *e = layout_knob("VBC_SWEEP_PACK")) h->sweep_pack = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_SWEEP_TILE")) h->sweep_tile = atoi(e) >= 32 ? 4 * kSweepTileBytes : atoi(e) >= 16 ? 2 * kSweepTileBytes : kSweepTileBytes;
+    if (const char *e = layout_knob("VBC_SLOT_STAGE")) h->slot_stage = (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : 0;
+    if (const char *e = layout_knob("VBC_SLOT_PLANAR")) h->slot_planar = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = layout_knob("VBC_SLOT_RUNS")) h->slot_runs = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_PLANAR_PAIR")) h->planar_pair = atoi(e) == 0 ? 0 : atoi(e) == 2 ? 2 : 1;  // 2: always
+    if (const char *e = layout_knob("VBC_PLANAR_MASK")) h->planar_mask = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_PLANAR_MASK_PAIR")) h->planar_mask_pair = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_MASK_WINDOW")) h->mask_window = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = layout_knob("VBC_PLANAR_SPLIT")) {  // 0 never, 1 auto, 2 / 4 / 8 forced
         const int v = atoi(e);
         h->planar_split = v == 0 ? 0 : (v == 2 || v == 4 || v == 8) ? v : -1;
     }
@@ -3227,32 +2782,32 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     }
     h->occ_p = std::max(1, std::min(occupancy_planar(h->esz), 8));
     h->target_ranges_l = prop.multiProcessorCount * std::max(1, std::min(occupancy_lanes(h->esz), 8)) * kWavesPerBlock;
-    if (const char *e = getenv("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
-    if (const char *e = getenv("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
-    if (const char *e = getenv("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
-    if (const char *e = getenv("VBC_LANES_RDIV")) h->lanes_rdiv = std::max(1, atoi(e));
-    if (const char *e = getenv("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
-    if (const char *e = getenv("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
-    if (const char *e = getenv("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
-    if (const char *e = getenv("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
-    if (const char *e = getenv("VBC_SIDE_FUSE")) h->side_fuse = atoi(e) < 0 ? -1 : atoi(e) != 0;
-    if (const char *e = getenv("VBC_COLSPLIT")) h->colsplit = atoi(e) != 0;
-    if (const char *e = getenv("VBC_FUSE_PMAX")) h->fuse_pmax = atoi(e) >= 8 ? 8 : atoi(e) >= 4 ? 4 : 2;
-    if (const char *e = getenv("VBC_COLSPLIT_W")) h->colsplit_w = std::max(0, atoi(e));
-    if (const char *e = getenv("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
-    if (const char *e = getenv("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
-    if (const char *e = getenv("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
-    if (const char *e = getenv("VBC_FWD_T")) h->fwd_t = atoi(e);
-    if (const char *e = getenv("VBC_SPLIT_DEEP")) h->split_deep = std::max(0.0, atof(e));
-    if (const char *e = getenv("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
-    if (const char *e = getenv("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
-    if (const char *e = getenv("VBC_PLANAR_WPS")) h->planar_wps = h->planar_wps_pair = std::max(0, atoi(e));
-    if (const char *e = getenv("VBC_PLANAR_WPS_PAIR")) h->planar_wps_pair = std::max(0, atoi(e));
-    if (const char *e = getenv("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_PLANAR_LANES")) h->planar_lanes = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char *e = layout_knob("VBC_TARGET_RANGES_L")) h->target_ranges_l = std::max(1, atoi(e));
+    if (const char *e = tuning_knob("VBC_LANES_DEEP")) h->lanes_deep = atoi(e) != 0;
+    if (const char *e = tuning_knob("VBC_LANES_RDIV")) h->lanes_rdiv = std::max(1, atoi(e));
+    if (const char *e = layout_knob("VBC_LANES_PAIR")) h->lanes_pair = atoi(e) != 0;
+    if (const char *e = tuning_knob("VBC_SPLIT_KC")) h->split_kc = atoi(e) != 0;
+    if (const char *e = tuning_knob("VBC_SPLIT_ROWS")) h->split_rows = std::max(1, atoi(e));
+    if (const char *e = layout_knob("VBC_SMALL_FUSE")) h->small_fuse = atoi(e);
+    if (const char *e = layout_knob("VBC_SIDE_FUSE")) h->side_fuse = atoi(e) < 0 ? -1 : atoi(e) != 0;
+    if (const char *e = layout_knob("VBC_COLSPLIT")) h->colsplit = atoi(e) != 0;
+    if (const char *e = tuning_knob("VBC_FUSE_PMAX")) h->fuse_pmax = atoi(e) >= 8 ? 8 : atoi(e) >= 4 ? 4 : 2;
+    if (const char *e = tuning_knob("VBC_COLSPLIT_W")) h->colsplit_w = std::max(0, atoi(e));
+    if (const char *e = tuning_knob("VBC_SPLIT_PIPE")) h->split_pipe = atoi(e);
+    if (const char *e = tuning_knob("VBC_SMALL_ROWS")) h->small_rows = std::max(1, atoi(e));
+    if (const char *e = layout_knob("VBC_KSPLIT")) h->ksplit = std::max(0.0, atof(e));
+    if (const char *e = layout_knob("VBC_FWD_T")) h->fwd_t = atoi(e);
+    if (const char *e = tuning_knob("VBC_SPLIT_DEEP")) h->split_deep = std::max(0.0, atof(e));
+    if (const char *e = tuning_knob("VBC_SPLIT_NT_MB")) h->split_nt_bytes = (int64_t)(atof(e) * (1 << 20));
+    if (const char *e = tuning_knob("VBC_FWD_MIN_ROWS")) h->fwd_min_rows = std::max(1, atoi(e));
+    if (const char *e = tuning_knob("VBC_PLANAR_WPS")) h->planar_wps = h->planar_wps_pair = std::max(0, atoi(e));
+    if (const char *e = tuning_knob("VBC_PLANAR_WPS_PAIR")) h->planar_wps_pair = std::max(0, atoi(e));
+    if (const char *e = tuning_knob("VBC_SLOT_WONLY")) h->slot_wonly = atoi(e) != 0;
     h->target_ranges_p = prop.multiProcessorCount * h->occ_p * kWavesPerBlock;
     h->cus = std::max(1, prop.multiProcessorCount);
     for (int lp = 1; lp <= 3; lp++) h->occ_multi[lp] = occupancy_split_multi(h->esz, 1 << lp);
-    if (const char *e = getenv("VBC_TARGET_RANGES_P")) {
+    if (const char *e = tuning_knob("VBC_TARGET_RANGES_P")) {
         h->target_ranges_p = std::max(1, atoi(e));
         h->occ_p = 1;
     }
@@ -3263,24 +2818,13 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         // profiles/r05zo_c5_ranges_ab.log; the bench decides, the count stays one round of resident waves)
         const int om = occupancy_panel(h->esz);
         h->target_ranges_m = prop.multiProcessorCount * std::max(1, std::min(om, 8)) * kWavesPerBlock;
-        if (const char *e = getenv("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
-        if (const char *e = getenv("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
-        if (const char *e = getenv("VBC_PANEL_DIAG")) h->panel_valu |= atoi(e) & ~1;
-        if (const char *e = getenv("VBC_PANEL_NOBUF")) h->panel_nobuf = atoi(e) != 0;
-        if (const char *e = getenv("VBC_PANEL_QUADS")) h->panel_quads = atoi(e);
-        if (const char *e = getenv("VBC_PANEL_TILES")) h->panel_tiles = atoi(e) < 0 ? -1 : atoi(e) != 0;
-        if (const char *e = getenv("VBC_TILE_NBT")) h->tile_nbt = atoi(e) >= 8 ? 8 : 4;
-        if (const char *e = getenv("VBC_TILE_SPR")) h->tile_spr = std::max(1, atoi(e));
-        if (const char *e = getenv("VBC_TILE_X4")) h->tile_x4 = atoi(e) != 0;
-        if (const char *e = getenv("VBC_TILE_ORDER")) h->tile_order = atoi(e);
-        if (const char *e = getenv("VBC_TILE_BLOB")) h->tile_blob = std::max(1, atoi(e));
-        if (const char *e = getenv("VBC_TILE_STAGE")) h->tile_stage = atoi(e) < 0 ? -1 : atoi(e) != 0;
-        if (const char *e = getenv("VBC_TILE_SMAX")) h->tile_smax = std::max(1, atoi(e));
-        if (const char *e = getenv("VBC_TILE_UMAX")) h->tile_umax = std::max(1, atoi(e));
-        if (const char *e = getenv("VBC_TILE_REUSE")) h->tile_reuse = atof(e);
-        if (const char *e = getenv("VBC_TILE_WGPC")) h->tile_wgpc = std::max(1, atoi(e));
-        if (const char *e = getenv("VBC_TILE_PERSIST")) h->tile_persist = atoi(e) != 0;
-        if (const char *e = getenv("VBC_TILE_WAVES")) h->tile_waves = atoi(e);
+        if (const char *e = tuning_knob("VBC_TARGET_RANGES_M")) h->target_ranges_m = std::max(1, atoi(e));
+        if (const char *e = ablation_knob("VBC_PANEL_VALU")) h->panel_valu = atoi(e) != 0;
+        if (const char *e = ablation_knob("VBC_PANEL_DIAG")) h->panel_valu |= atoi(e) & ~1;
+        if (const char *e = tuning_knob("VBC_PANEL_NOBUF")) h->panel_nobuf = atoi(e) != 0;
+        if (const char *e = layout_knob("VBC_PANEL_TILES")) h->panel_tiles = atoi(e) < 0 ? -1 : atoi(e) != 0;
+        if (const char *e = tuning_knob("VBC_TILE_NBT")) h->tile_nbt = atoi(e) >= 8 ? 8 : 4;
+        if (const char *e = tuning_knob("VBC_TILE_SPR")) h->tile_spr = std::max(1, atoi(e));
         h->occ_tiles = occupancy_tiles(h->esz);
     }
 
@@ -3548,7 +3092,7 @@ int vbc_csc_create(vbc_handle **out, int64_t m, int64_t n, const int64_t *colptr
     // kernels (planar with row runs for 3-dof operators).  Each output y[j] still sums its column in
     // stored row order (TrSpMV.jl:10-16), so the result is that of the unit-width layout, bit for bit.
     // VBC_CSC_BLOCK=0 keeps unit stripes.
-    const char *eb = getenv("VBC_CSC_BLOCK");
+    const char *eb = layout_knob("VBC_CSC_BLOCK");
     if (!(eb && atoi(eb) == 0) && n > 1 && (dtype == VBC_F64 || dtype == VBC_F32 || dtype == VBC_I64)) {
         std::vector<int64_t> g0;  // first column of each group
         for (int64_t j = 0; j < n;) {
@@ -3624,16 +3168,10 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
     info->device_bytes = (int64_t)h->arena_bytes;
     info->bytes_t = h->bytes_t;
     info->bytes_f = h->bytes_f;
-    info->bins_m = h->has_m ? (int32_t)(h->lm.bins.size() + h->lm.qbins.size() + h->lm.tbins.size())
-                 : h->has_mf ? (int32_t)(h->lmf.bins.size() + h->lmf.qbins.size() + h->lmf.tbins.size()) : 0;
+    info->bins_m = h->has_m ? (int32_t)(h->lm.bins.size() + h->lm.tbins.size())
+                 : h->has_mf ? (int32_t)(h->lmf.bins.size() + h->lmf.tbins.size()) : 0;
     if ((h->has_m && !h->lm.tbins.empty()) || (h->has_mf && !h->lmf.tbins.empty()))
         info->planar_mask |= 512;  // multi-RHS buckets in the tile-granular layout (spmm_tiles)
-    for (const vbc::PanelLaunch *pl : {h->has_m ? &h->lm : nullptr, h->has_mf ? &h->lmf : nullptr})
-        if (pl)
-            for (const auto &tb : pl->tbins)
-                if (tb.staged) info->planar_mask |= 1024;  // ... in the staged-X form (spmm_tiles_x)
-    if ((h->has_m && !h->lm.qbins.empty()) || (h->has_mf && !h->lmf.qbins.empty()))
-        info->planar_mask |= 128;  // multi-RHS buckets in the VALU stripe-quad layout (spmm_quads)
     int32_t sl = h->has_t ? (int32_t)(h->lt.sbins.size() + h->lt.pbins.size()) : 0;  // planar bins are slotted too
     for (auto &l : h->lf) sl += h->has_f ? (int32_t)(l.sbins.size() + l.pbins.size()) : 0;  // + planar forward
     if (h->has_ft) sl += (int32_t)(h->lft.sbins.size() + h->lft.pbins.size());  // forward on C = Bᵀ's layout

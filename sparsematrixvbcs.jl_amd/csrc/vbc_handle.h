@@ -60,7 +60,6 @@ struct Launch {
 struct PanelLaunch {
     std::vector<PanelBin> bins;
     PanelBin *d_bins = nullptr;
-    std::vector<QuadBin> qbins;  // stripe-quad buckets (VALU, w <= 8): one launch each
     std::vector<TileBin> tbins;  // small-tile buckets (vbc_tiles.h, u, w <= 4): one launch each
     int total_ranges = 0;
     int nfill = 0;
@@ -109,30 +108,14 @@ struct vbc_handle {
     int64_t bytes_mf = 0;         // matrix bytes one forward panel product streams
     int32_t mf_group = 0;         // forward panel: widest output row group
     int target_ranges_m = 4096;
-    int panel_valu = 0;           // VBC_PANEL_VALU=1: VALU instead of MFMA; VBC_PANEL_DIAG: ablation bits
+    int panel_valu = 0;           // ablation bits of the panel kernel (VBC_PANEL_VALU / VBC_PANEL_DIAG, the VBC_ABLATION
+                                  // build only; 0 in the product library)
     int panel_nobuf = 0;          // VBC_PANEL_NOBUF=1: 64-bit addressing variant (tests / A/B)
-    int panel_quads = 0;          // VBC_PANEL_QUADS: widest stripe of the VALU stripe-quad layout (0: MFMA panels only)
     int panel_tiles = -1;         // VBC_PANEL_TILES: small-tile buckets tile-granular (vbc_tiles.h): -1 auto, 0 never,
                                   // 1 whenever representable (any fill)
     int occ_tiles = 24;           // resident waves per CU of the tile kernel (the layout's range count)
     int tile_nbt = vbc::kTileBatch;  // VBC_TILE_NBT: tiles per stream per pipeline stage of the tile kernel (4 / 8)
     int tile_spr = vbc::kTileStripes;  // VBC_TILE_SPR: stripes per range (wave) of the tile layout
-    int tile_x4 = 0;              // VBC_TILE_X4=1: the 16-B fp32 form of the tile kernel (spmm_tiles4; c5-mesh 308-333 us
-                                  // against 298-305 us for the dword form, profiles/r05_tiles_ab.log)
-    int tile_order = 0;           // VBC_TILE_ORDER: 0 natural stripe order, 1 blob order (vbc_device.hip build_tiles;
-                                  // c5-mesh 305 -> 310 us dword, 334 -> 370 us 16-B form: not kept)
-    int tile_blob = 512;          // VBC_TILE_BLOB: stripes per blob of the blob order
-    int tile_stage = 0;           // VBC_TILE_STAGE: staged-X tile form (spmm_tiles_x / _xp): 0 never (default: c5-mesh
-                                  // 304 us unstaged vs 302-306 staged, 388 persistent), -1 auto (when the
-                                  // clusters reuse each staged group >= tile_reuse times), 1 whenever it fits
-    int tile_smax = -1;           // VBC_TILE_SMAX: stripes per cluster of the staged-X form (auto: 48 persistent, 64)
-    int tile_umax = -1;           // VBC_TILE_UMAX: row groups staged per cluster (LDS: (U + 1) x ub x 16 elements;
-                                  // auto: 160 for the persistent kernel's double-buffered stage, 192)
-    int tile_waves = 4;           // VBC_TILE_WAVES: compute waves per cluster workgroup of spmm_tiles_x (fp32: 4 or 8;
-                                  // 8 = two 80 KB workgroups per CU: c5-mesh 356 us against 307 us with 4)
-    int tile_wgpc = 2;            // VBC_TILE_WGPC: persistent workgroups per CU of the staged-X form
-    int tile_persist = 0;         // VBC_TILE_PERSIST=1: the persistent staged-X kernel (spmm_tiles_xp) when X and Y allow it
-    double tile_reuse = 2.0;      // VBC_TILE_REUSE: auto staged-X form when each staged group serves >= this many tiles
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products
     vbc::Launch lt;               // transposed product: all buckets in one launch

@@ -3,6 +3,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "vbc.h"
 
@@ -16,6 +17,27 @@ inline int fail(int status, const char *what)
     set_error("%s", what);
     return status;
 }
+
+// Environment knobs read at create time.
+//  * layout_knob: a layout choice.  Every value selects a layout that the -m gpu
+//    parity tests hold to the oracle; none changes what a product computes beyond the rounding that
+//    vbc.h states for the split layouts (VBC_CREATE_SERIAL forbids those).
+//  * tuning_knob: a launch / layout tuning constant (range counts, pipeline depths, thresholds) that the
+//    product library keeps at its measured default; the VBC_ABLATION build reads it for tools/ab.py sweeps.
+//  * ablation_knob / VBC_ABL: ablation variants that time a kernel with part of its work removed (x
+//    taken as 1, gathers confined to a few lines, stores dropped): wrong products by design.  Only the
+//    -DVBC_ABLATION build reads them and instantiates those kernels (`make ablation` ->
+//    tools/exp/libs/libvbc_ablation.so, for tools/ab.py); the product libvbc.so does neither.
+inline const char *layout_knob(const char *name) { return std::getenv(name); }
+#ifdef VBC_ABLATION
+#define VBC_ABL(expr) (expr)
+inline const char *ablation_knob(const char *name) { return std::getenv(name); }
+inline const char *tuning_knob(const char *name) { return std::getenv(name); }
+#else
+#define VBC_ABL(expr) 0
+inline const char *ablation_knob(const char *) { return nullptr; }
+inline const char *tuning_knob(const char *) { return nullptr; }
+#endif
 
 inline int elem_size(int dtype)
 {

@@ -23,6 +23,8 @@
 
 #include <cstdint>
 
+#include "vbc_internal.h"  // VBC_ABL
+
 namespace vbc {
 
 constexpr int kBlockThreads = 256;

@@ -45,7 +45,7 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
             faste = faste && sb.out_affine;
             contig = contig && sb.contig;
         }
-        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
+        if (ablation_knob("VBC_NO_FASTE")) faste = false;  // (the VBC_ABLATION build only)
         // auto (-1): B'x stages 8 chunks per write, Bx writes directly -- measured on FE with every
         // variant built twice (tools/ab.py --copies 2): fp64 B'x 192/177 -> 184/172 us staged,
         // fp64 Bx 186 -> 198 and fp32 Bx 142 -> 157 us staged
@@ -83,7 +83,7 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
         const SlotBin &pb = L.pbins[i];
         if (L.fuse_split && pb.fused) continue;
         if (!mine(true)) continue;
-        const bool faste = !rd && pb.out_affine && !getenv("VBC_NO_FASTE");
+        const bool faste = !rd && pb.out_affine && !ablation_knob("VBC_NO_FASTE");
         const bool staged = faste && pb.contig && slot_stage != 0;
         const hipError_t e = (hipError_t)launch_planar((int)sizeof(T), pb, L.d_pbins + i, faste, staged, x, y, alpha,
                                                        beta, rd, stream);
@@ -99,7 +99,7 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
         // load-free owner writes when every bucket maps segments affinely and beta = 0
         bool faste = !rd;
         for (const Bin &bb : L.bins) faste = faste && bb.out_affine;
-        if (getenv("VBC_NO_FASTE")) faste = false;  // A/B knob
+        if (ablation_knob("VBC_NO_FASTE")) faste = false;  // (the VBC_ABLATION build only)
 #define VBC_LAUNCH(KIND, KK, PP)                                                                         \
     do {                                                                                                 \
         if (faste)                                                                                       \
@@ -110,6 +110,7 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
                                L.d_bins, (int)L.bins.size(), L.total_ranges, xs, ys, (T)alpha, (T)beta, (int)rd); \
     } while (0)
         const int P = L.bins.empty() ? kPipeDefault : L.bins[0].pipe;
+#ifdef VBC_ABLATION
         const int D = L.bins.empty() ? 0 : L.bins[0].diag;
         if constexpr (std::is_same<T, double>::value) {
             if (kind == 0 && K == 4 && P == 2 && D == 1) {
@@ -123,6 +124,7 @@ static int launch_group(const Launch &L, int kind, const void *x, void *y, doubl
                 return VBC_OK;
             }
         }
+#endif
         if (kind == 0) {
             if (P == 2) { if (K == 4) VBC_LAUNCH(0, 4, 2); else VBC_LAUNCH(0, 8, 2); }
             else { if (K == 4) VBC_LAUNCH(0, 4, 3); else VBC_LAUNCH(0, 8, 3); }

@@ -116,7 +116,8 @@ __device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
 }
 
-// diag (ablation, VBC_PANEL_DIAG): 1 VALU path, 2 no Y stores, 4 X gathers hit cache, 8 val hits cache.
+// diag (ablation, VBC_PANEL_DIAG; read by the VBC_ABLATION build only, 0 in the product library): 1 VALU path,
+// 2 no Y stores, 4 X gathers hit cache, 8 val hits cache.
 // BUF: X and the bins' val are addressed by 32-bit offsets through buffer descriptors (the host picks
 // it when both, plus the column offsets, stay below 2 GiB); otherwise 64-bit global addresses.
 // FAST (with BUF; beta = 0, affine stripe -> column map, Y below 2 GiB): a full panel is written by
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) {
                     const int jj = nb * 16 + j;
-                    if (jj < nrhs && !(diag & 2)) {
+                    if (jj < nrhs && !VBC_ABL(diag & 2)) {
                         gptr<T> yo = yg + o * syr + (int64_t)jj * syc;
                         T v = alpha * acc[nb][q];
                         if (rd_i) v = fmadd(beta, *yo, v);
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
     auto flush_full = [&]() {
         if constexpr (FAST) {
             const uint32_t pb = (uint32_t)((int64_t)(b.out_base + (int64_t)seg_base * ostr) * syr * esz);
-            if (!(diag & 2)) {
+            if (!VBC_ABL(diag & 2)) {
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) {
                     if (nb * 16 < nrhs) {
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
             fmask = __ballot(head && rs == 0 && gseg > 0);
             const bool ok = (kv & ~kHead) != kPanelSentinel;
             uint32_t xo = ok ? (kv & ~kHead) * sxr_b : xbytes;  // past X: the buffer load returns 0
-            if (diag & 4) xo = ok ? (uint32_t)(lane & 3) * sxr_b : xbytes;  // ablation: X gathers hit cache
+            if (VBC_ABL(diag & 4)) xo = ok ? (uint32_t)(lane & 3) * sxr_b : xbytes;  // ablation: X gathers hit cache
             xch[wv][lane][0] = xo;
             xch[wv][lane][1] = (uint32_t)rs;
         }
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
             rsv[q] = xch[wv][4 * q + kr][1];
             if constexpr (BUF) {
                 const uint32_t vo = (!kOobMask || (int)rsv[q] == sa) ? voff_lane + (uint32_t)(q * 4 * w * esz) : kOobOff;
-                av[q] = buf_load<T, VBC_PANEL_VAL_AUX>(vrs, vo, (diag & 8) ? 0u : (uint32_t)((size_t)gb * 4 * w * esz));
+                av[q] = buf_load<T, VBC_PANEL_VAL_AUX>(vrs, vo, VBC_ABL(diag & 8) ? 0u : (uint32_t)((size_t)gb * 4 * w * esz));
 #pragma unroll
                 for (int nb = 0; nb < NB; nb++) xv[q][nb] = buf_load<T>(xrs, xo + jofs[nb], 0u);
             } else {
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
 #pragma unroll
             for (int nb = 0; nb < NB; nb++) chk = fmadd(xv[q][nb], zero, chk);
         }
-        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(chk != chk) != 0 || (diag & 1) ? 1 : 0);
+        const int any_bad = __builtin_amdgcn_readfirstlane(__ballot(chk != chk) != 0 || VBC_ABL(diag & 1) ? 1 : 0);
         if (!any_bad) {
 #pragma unroll
             for (int q = 0; q < kPanelBatch; q++) {
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
             }
         } else {
             // VALU, one row at a time from memory: row k only feeds the accumulator rows of its own
-            // stripe (rare: only batches whose X holds an Inf / NaN, or VBC_PANEL_VALU)
+            // stripe (rare: only batches whose X holds an Inf / NaN)
             for (int q = 0; q < ng; q++) {
                 if ((fmask >> (4 * q)) & 1) flush_full();
                 for (int k = 0; k < 4; k++) {
@@ -341,163 +342,6 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_panel(const PanelBin *__re
         }
     }
     flush_general(segc - ((segc - 1) / S) * S);  // the last panel (the bin's last may hold < S stripes)
-}
-
-// Stripe-quad layout (round 4; VALU multi-RHS product for stripes of width w <= 8).  An f32 MFMA has no
-// throughput edge over the f32 VALU on gfx950 (both 64 flop / clk / SIMD), and the panel's 16 x 16 x 4
-// MFMA puts only w of its 16 M rows to use (w = 3 node tiles: 19 %), so narrow stripes run on the VALU:
-// a wave owns a chunk of 16 stripes, lane 4 s + q holds stripe s's output columns for right-hand sides
-// 4 q .. 4 q + 3 (w x 4 accumulators), and steps through the chunk's rows in stored order -- per row one
-// key (its x row), the w values (lane q loads component q (and q + 4); a DPP quad broadcast hands each
-// component to the stripe's 4 lanes) and one 16-B gather of the quad's 4 right-hand sides, folded by
-// w x 4 fmas.  Rows of a chunk: its longest stripe's; shorter stripes pad with the sentinel key (x read
-// as 0 past the buffer, zero values).  Each column is one fma chain over the stripe's rows in stored
-// order (the reference's multiply_VBC.jl:93-147 order per column), deterministic, and a non-finite x
-// reaches only the stripes that store its row.
-struct QuadBin {
-    int32_t w;            // stripe width (1..8)
-    int32_t nchunks;      // chunks of 16 stripes
-    int32_t nseg;         // stripes
-    int32_t out_affine;   // out[s] == out_base + s * out_stride
-    int32_t out_base;
-    int32_t out_stride;
-    const int32_t *crow;  // nchunks + 1: first row of each chunk
-    const uint32_t *key;  // rows x 16: x row, or kPanelSentinel
-    const void *val;      // rows x 16 x w values
-    const int32_t *out;   // per stripe: first y column
-};
-
-// v from lane (lane & ~3) | C of its quad (DPP quad_perm [C, C, C, C])
-template <int C, typename T>
-__device__ __forceinline__ T quad_bcast(T v)
-{
-    constexpr int ctrl = C | (C << 2) | (C << 4) | (C << 6);
-    if constexpr (sizeof(T) == 4) {
-        return __builtin_bit_cast(T, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false));
-    } else {
-        const uint64_t u = __builtin_bit_cast(uint64_t, v);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, ctrl, 0xF, 0xF, false);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), ctrl, 0xF, 0xF, false);
-        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
-    }
-}
-template <typename T>
-__device__ __forceinline__ T quad_bcast_rt(T v, int c)
-{
-    switch (c & 3) {
-    case 0: return quad_bcast<0>(v);
-    case 1: return quad_bcast<1>(v);
-    case 2: return quad_bcast<2>(v);
-    default: return quad_bcast<3>(v);
-    }
-}
-
-#ifndef VBC_QUAD_BATCH
-#define VBC_QUAD_BATCH 8
-#endif
-
-// VEC: X and Y row-major with contiguous right-hand sides (column stride 1), 16-B aligned rows, nrhs a
-// multiple of 4, X below 2 GiB: 16-B buffer gathers (past X for padding rows: zeros) and 16-B stores;
-// otherwise one element at a time through 64-bit addresses.
-template <typename T, int W, bool VEC>
-__global__ __launch_bounds__(kBlockThreads) void spmm_quads(const QuadBin b, const T *__restrict__ X, int64_t sxr,
-                                                            int64_t sxc, uint32_t xbytes, T *__restrict__ Y, int64_t syr,
-                                                            int64_t syc, int nrhs, T alpha, T beta, int rd_i, int diag)
-{
-    const int c = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
-    if (c >= b.nchunks) return;
-    const int lane = threadIdx.x & 63, s = lane >> 2, q = lane & 3;
-    const int r0 = __builtin_amdgcn_readfirstlane(G(b.crow)[c]), r1 = __builtin_amdgcn_readfirstlane(G(b.crow)[c + 1]);
-    constexpr int esz = (int)sizeof(T);
-    constexpr int NV = (W + 3) / 4;  // value components per lane per row
-    constexpr int NB = sizeof(T) == 4 ? VBC_QUAD_BATCH : (VBC_QUAD_BATCH + 1) / 2;
-    const bool qlive = 4 * q < nrhs;
-    const gptr<const uint32_t> key = G(b.key);
-    const gptr<const T> val = G(static_cast<const T *>(b.val));
-    const gptr<const T> xg = G(X);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(X), 0, (int)xbytes, 0x00020000);
-    const uint32_t sxr_b = (uint32_t)(sxr * esz), qoff = (uint32_t)(4 * q * esz);
-    // accumulators of stripe column k, right-hand sides 4 q + 2 h, 4 q + 2 h + 1 (fp32: packed fmas)
-    typedef T t2 __attribute__((ext_vector_type(2)));
-    t2 acc[W][2];
-#pragma unroll
-    for (int k = 0; k < W; k++) acc[k][0] = acc[k][1] = t2{T(0), T(0)};
-    // the keys of batch i + 1 are loaded with batch i's values and gathers: one round trip per batch
-    uint32_t kn[NB];
-#pragma unroll
-    for (int j = 0; j < NB; j++) kn[j] = r0 < r1 ? key[(size_t)min(r0 + j, r1 - 1) * 16 + s] : kPanelSentinel;
-    for (int r = r0; r < r1; r += NB) {
-        uint32_t kk[NB];
-        T v[NB][NV];
-        t2 xv[NB][2];
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            kk[j] = kn[j];
-            const size_t rr = (size_t)min(r + j, r1 - 1) * 16 + s;
-#pragma unroll
-            for (int u = 0; u < NV; u++) v[j][u] = val[rr * W + min(4 * u + q, W - 1)];
-        }
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            const bool ok = r + j < r1 && kk[j] != kPanelSentinel && qlive;
-            const uint32_t xr = (diag & 16) ? (kk[j] & 3u) : kk[j];  // ablation: gathers confined to 4 rows
-            if constexpr (VEC) {
-                const uint32_t xo = ok ? xr * sxr_b + qoff : xbytes;  // past X: zeros
-                if constexpr (sizeof(T) == 4) {
-                    typedef float f4 __attribute__((ext_vector_type(4)));
-                    const f4 t4 = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
-                    xv[j][0] = t2{t4[0], t4[1]};
-                    xv[j][1] = t2{t4[2], t4[3]};
-                } else {
-                    xv[j][0] = __builtin_bit_cast(t2, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0));
-                    xv[j][1] = __builtin_bit_cast(t2, __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xo + 16 : xbytes, 0, 0));
-                }
-            } else {
-                T e[4];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const int col = 4 * q + t;
-                    e[t] = (ok && col < nrhs) ? xg[(int64_t)xr * sxr + (int64_t)col * sxc] : T(0);
-                }
-                xv[j][0] = t2{e[0], e[1]};
-                xv[j][1] = t2{e[2], e[3]};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NB; j++) kn[j] = key[(size_t)min(r + NB + j, r1 - 1) * 16 + s];
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-            // rows past the chunk (the batch's clamped tail): zero values times zero x, no-ops
-            const bool live = r + j < r1;
-#pragma unroll
-            for (int u = 0; u < NV; u++) v[j][u] = live ? v[j][u] : T(0);
-#pragma unroll
-            for (int k = 0; k < W; k++) {
-                const T vk = quad_bcast_rt(v[j][k >> 2], k);
-                const t2 vv = t2{vk, vk};
-                acc[k][0] = __builtin_elementwise_fma(vv, xv[j][0], acc[k][0]);
-                acc[k][1] = __builtin_elementwise_fma(vv, xv[j][1], acc[k][1]);
-            }
-        }
-    }
-    const int seg = c * 16 + s;
-    if (seg >= b.nseg || !qlive || (diag & 2)) return;
-    const int64_t o = b.out_affine ? (int64_t)b.out_base + (int64_t)seg * b.out_stride : (int64_t)G(b.out)[seg];
-#pragma unroll
-    for (int k = 0; k < W; k++) {
-        gptr<T> yo = G(Y) + (o + k) * syr;
-        const T a4[4] = {acc[k][0][0], acc[k][0][1], acc[k][1][0], acc[k][1][1]};
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int col = 4 * q + t;
-            if (VEC || col < nrhs) {
-                const int64_t yi = VEC ? (int64_t)col : (int64_t)col * syc;
-                T ov = alpha * a4[t];
-                if (rd_i) ov = fmadd(beta, yo[yi], ov);
-                yo[yi] = ov;
-            }
-        }
-    }
 }
 
 // Y rows of the stripes that store no row (and belong to no panel): beta * Y or 0.

@@ -20,43 +20,6 @@ static int mulmat_panel(const vbc_handle *h, int trans, int64_t nrhs, const char
     const bool rd = beta != 0.0;
     // small-tile buckets (vbc_tiles.h): their own launches, disjoint columns of Y
     if (int st = mulmat_tiles_any(h, trans, nrhs, X, sxr, sxc, Y, syr, syc, alpha, beta, s)) return st;
-    // stripe-quad buckets (VALU, vbc_panel.h spmm_quads): 16 right-hand sides per launch, one launch per bucket
-    for (int64_t c0 = 0; c0 < nrhs && !L.qbins.empty(); c0 += 16) {
-        const int nr = (int)std::min<int64_t>(16, nrhs - c0);
-        const T *xs = reinterpret_cast<const T *>(X) + c0 * sxc;
-        T *ys = reinterpret_cast<T *>(Y) + c0 * syc;
-        const int64_t span = ((xrows - 1) * sxr + (int64_t)(nr - 1) * sxc + 1) * (int64_t)sizeof(T);
-        const int64_t lim = int64_t(1) << 31;
-        const bool vec = sxc == 1 && syc == 1 && nr % 4 == 0 && (sxr * (int64_t)sizeof(T)) % 16 == 0 &&
-                         (syr * (int64_t)sizeof(T)) % 16 == 0 && reinterpret_cast<uintptr_t>(xs) % 16 == 0 &&
-                         reinterpret_cast<uintptr_t>(ys) % 16 == 0 && span + 16 < lim && !h->panel_nobuf;
-        const uint32_t xb = (uint32_t)std::min<int64_t>(span, lim - 1);
-        for (const QuadBin &qb : L.qbins) {
-            if (qb.nchunks == 0) continue;
-            const int grid = (qb.nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
-#define VBC_QUADS(W)                                                                                          \
-    do {                                                                                                      \
-        if (vec)                                                                                              \
-            hipLaunchKernelGGL((spmm_quads<T, W, true>), dim3(grid), dim3(kBlockThreads), 0, s, qb, xs, sxr, sxc, xb, \
-                               ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu);               \
-        else                                                                                                  \
-            hipLaunchKernelGGL((spmm_quads<T, W, false>), dim3(grid), dim3(kBlockThreads), 0, s, qb, xs, sxr, sxc, xb, \
-                               ys, syr, syc, nr, (T)alpha, (T)beta, (int)rd, h->panel_valu);               \
-    } while (0)
-            switch (qb.w) {
-            case 1: VBC_QUADS(1); break;
-            case 2: VBC_QUADS(2); break;
-            case 3: VBC_QUADS(3); break;
-            case 4: VBC_QUADS(4); break;
-            case 5: VBC_QUADS(5); break;
-            case 6: VBC_QUADS(6); break;
-            case 7: VBC_QUADS(7); break;
-            default: VBC_QUADS(8); break;
-            }
-#undef VBC_QUADS
-            VBC_HIP(hipGetLastError());
-        }
-    }
     for (int64_t c0 = 0; c0 < nrhs; c0 += 64) {
         const int nr = (int)std::min<int64_t>(64, nrhs - c0);
         const T *xs = reinterpret_cast<const T *>(X) + c0 * sxc;

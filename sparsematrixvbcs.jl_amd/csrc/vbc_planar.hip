@@ -35,7 +35,8 @@ static void launch_split(const SlotBin &hb, const SlotBin *d_b, const void *x, v
     const T *xs = static_cast<const T *>(x);
     T *ys = static_cast<T *>(y);
     const dim3 grid(hb.nranges);
-    if constexpr (W_ == 3 && RUN == 3 && !KC) {  // ablations (tools/ab.py, VBC_DIAG=1..4)
+#ifdef VBC_ABLATION
+    if constexpr (W_ == 3 && RUN == 3 && !KC) {  // ablations (the VBC_ABLATION build only, VBC_DIAG=1..4)
         if (hb.diag >= 1 && hb.diag <= 4) {
 #define VBC_SPLIT_DIAG(D)                                                                                                     \
     if (hb.diag == D) {                                                                                                       \
@@ -48,6 +49,7 @@ static void launch_split(const SlotBin &hb, const SlotBin *d_b, const void *x, v
 #undef VBC_SPLIT_DIAG
         }
     }
+#endif
     switch (hb.split) {
     case 2: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 2>), grid, dim3(128), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
     case 4: hipLaunchKernelGGL((spmv_planar_split<T, W_, KC, RUN, 4>), grid, dim3(256), 0, s, hb, xs, ys, (T)alpha, (T)beta, (int)rd); break;
@@ -168,11 +170,13 @@ static void launch_lanes_w(const SlotBin &hb, const SlotBin *d_b, const T *xs, T
                            bool rd, hipStream_t s)
 {
     const dim3 grid((hb.nranges + kWavesPerBlock - 1) / kWavesPerBlock), blk(kBlockThreads);
-    if constexpr (W_ == 3 && RUN == 3) {  // ablations (tools/ab.py, VBC_DIAG=1..3)
+#ifdef VBC_ABLATION
+    if constexpr (W_ == 3 && RUN == 3) {  // ablations (the VBC_ABLATION build only, VBC_DIAG=1..3)
         if (hb.diag == 1) { hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false, 1>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta); return; }
         if (hb.diag == 2) { hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false, 2>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta); return; }
         if (hb.diag == 3) { hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false, 3>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta); return; }
     }
+#endif
     if (rd) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, true>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
     else if (hb.deep) hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, true, false>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);
     else hipLaunchKernelGGL((spmv_planar_lanes<T, W_, RUN, false, false>), grid, blk, 0, s, hb, xs, ys, (T)alpha, (T)beta);

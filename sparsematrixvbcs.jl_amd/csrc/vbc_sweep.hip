@@ -210,10 +210,14 @@ template <typename T, int KIND>
 static void launch_any(const SweepBin *d_bins, int nbins, int total_tiles, int tile_bytes, int diag, const void *x,
                        void *y, double alpha, double beta, bool rd, hipStream_t s)
 {
-    if constexpr (sizeof(T) == 8 && KIND == 0) {  // ablations (tools/ab.py only)
+#ifdef VBC_ABLATION
+    if constexpr (sizeof(T) == 8 && KIND == 0) {  // ablations (the VBC_ABLATION build only)
         if (diag == 1 && tile_bytes == 2 * kSweepTileBytes) return launch_t<T, KIND, 2 * kSweepTileBytes, 1>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
         if (diag == 2 && tile_bytes == 2 * kSweepTileBytes) return launch_t<T, KIND, 2 * kSweepTileBytes, 2>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
     }
+#else
+    (void)diag;
+#endif
     if (tile_bytes >= 4 * kSweepTileBytes) launch_t<T, KIND, 4 * kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
     else if (tile_bytes >= 2 * kSweepTileBytes) launch_t<T, KIND, 2 * kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);
     else launch_t<T, KIND, kSweepTileBytes>(d_bins, nbins, total_tiles, x, y, alpha, beta, rd, s);

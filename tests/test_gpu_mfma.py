@@ -18,24 +18,13 @@ DEV = "cuda:0"
 TOL64, TOL32 = 1e-12, 1e-5
 
 
-@pytest.fixture(autouse=True, params=["staged", "tiles", "8", "0"], ids=["staged", "tiles", "quads", "panels"])
+@pytest.fixture(autouse=True, params=["tiles", "0"], ids=["tiles", "panels"])
 def multi_layout(request, monkeypatch):
-    """Every test on the three multi-RHS layouts: every width on the MFMA panels (VBC_PANEL_QUADS=0,
-    VBC_PANEL_TILES=0); stripes of width <= 8 in the VALU stripe-quad layout (VBC_PANEL_QUADS=8; spmm_quads,
-    measured slower on both C5 inputs, kept as the A/B alternative); and (round 5) every bucket of width <= 4
-    whose tiles are <= 4 rows in the tile-granular layout (VBC_PANEL_TILES=1, spmm_tiles -- the default
-    for such buckets when their rows come in tiles); and (round 5b) the same buckets in the staged-X form
-    (VBC_TILE_STAGE=1, spmm_tiles_x: clusters of stripes sharing row groups, the groups staged in LDS -- the
-    default when the clusters reuse each staged group >= 2 times)."""
-    if request.param in ("tiles", "staged"):
-        monkeypatch.setenv("VBC_PANEL_TILES", "1")
-        monkeypatch.setenv("VBC_PANEL_QUADS", "0")
-        monkeypatch.setenv("VBC_TILE_STAGE", "1" if request.param == "staged" else "0")
-        # (staged: fp32 products with 16 contiguous right-hand sides run the persistent kernel spmm_tiles_xp)
-        monkeypatch.setenv("VBC_TILE_PERSIST", "1" if request.param == "staged" else "0")
-    else:
-        monkeypatch.setenv("VBC_PANEL_TILES", "0")
-        monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
+    """Every test on the two multi-RHS layouts: every width on the MFMA panels (VBC_PANEL_TILES=0), and every
+    bucket of width <= 4 whose tiles are <= 4 rows in the tile-granular layout (VBC_PANEL_TILES=1, spmm_tiles --
+    the default for such buckets when their rows come in tiles).  (Round 6: the VALU stripe-quad layout and the
+    staged-X / persistent / 16-B tile forms, which lost their A/B in rounds 4-5, left the library.)"""
+    monkeypatch.setenv("VBC_PANEL_TILES", "1" if request.param == "tiles" else "0")
     return request.param
 
 
@@ -220,13 +209,14 @@ def test_c5_panels_scaled_every_column(workload, scale):
             assert rel(got[:, j], ref) <= TOL32, (trans, j)
 
 
-def test_quads_layout_flag_and_mixed_widths(multi_layout):
-    """vbc_info planar_mask bit 7 reports the VALU stripe-quad buckets (widths <= 8) unless
-    VBC_PANEL_QUADS=0; a matrix with widths 3 and 12 runs both kernels in one product (quads for the
-    3-wide stripes, MFMA panels for the 12-wide ones) and matches the oracle on every column."""
+def test_mixed_widths_tiles_and_panels(multi_layout):
+    """A matrix with widths 3 and 12 runs both multi-RHS kernels in one product (with VBC_PANEL_TILES=1 the
+    tile kernel for the 3-wide stripes, whose rows come in runs; MFMA panels for the 12-wide ones) and matches
+    the oracle on every column; vbc_info planar_mask bits 7 and 10 (the removed stripe-quad and staged-X
+    layouts) stay clear."""
     B = V.synthetic.vbr_1dvbc(700, 80, 900, np.where(np.arange(80) % 2 == 0, 3, 12), W=16, dtype=np.float32, seed=12)
     inf = B.info(multi=True)
-    assert bool(inf["planar_mask"] & 128) == (multi_layout == "8")
+    assert inf["planar_mask"] & (128 | 1024) == 0
     assert inf["bins_m"] == 2
     R = ref_1d(B)
     X = np.random.default_rng(2).uniform(-1, 1, (B.m, 16)).astype(np.float32)
@@ -265,10 +255,9 @@ def test_tiles_mixed_heights_widths_every_column(dtype, multi_layout):
     tol = TOL64 if dtype == np.float64 else TOL32
     B = _vbc2d_mixed_heights(rng, 300, 400, 1200, (3, 1, 4, 2, 3), (1, 3, 2, 4, 3), dtype)
     assert (np.diff(B.pos) == 0).any()
-    if multi_layout in ("tiles", "staged"):
+    if multi_layout == "tiles":
         assert B.info(multi=True)["planar_mask"] & 512
         assert B.info(trans=False, multi=True)["planar_mask"] & 512
-        assert bool(B.info(multi=True)["planar_mask"] & 1024) == (multi_layout == "staged")
     R = ref_2d(B)
     for nrhs in (5, 16, 21):
         for layout in ("R", "C"):
@@ -310,7 +299,7 @@ def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
     val = np.zeros(nv + 8)
     val[:nv] = rng.integers(-8, 9, nv)
     B = V.SparseMatrix1DVBC(8, 3 * N, int(spl[-1] - 1), V.SplitPartition(spl), pos, np.concatenate(rows) + 1, ofs, val)
-    if multi_layout in ("tiles", "staged"):
+    if multi_layout == "tiles":
         assert B.info(multi=True)["planar_mask"] & 512
     R = ref_1d(B)
     X = rng.integers(-8, 9, (B.m, 16)).astype(np.float64)
@@ -329,39 +318,31 @@ def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
     assert np.array_equal(got[fin], ref[fin])
 
 
-@pytest.mark.parametrize("form", ["persist", "waves4", "waves8"])
-@pytest.mark.parametrize("smax,umax", [(3, 40), (7, 64), (64, 192)])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, form, multi_layout, monkeypatch):
-    """Staged-X tile form (spmm_tiles_x with 4 or 8 compute waves; with form "persist" and fp32 the persistent spmm_tiles_xp: workgroups walking
-    sequences of clusters, stager / writer waves, double-buffered LDS) on the structured C5 input at small scale:
-    clusters cut by the stripe cap or by the LDS stage (VBC_TILE_SMAX / VBC_TILE_UMAX), 16 row-major right-hand
-    sides, both directions
-    (B·X on Bᵀ's tiles): integer data, so every column equals the oracle bit for bit (each column is the
+def test_c5_mesh_integer_bitwise(dtype, multi_layout):
+    """The structured C5 input (3 x 3 node tiles) at small scale, 16 row-major right-hand sides, both directions
+    (B·X on Bᵀ's layout): integer data, so every column equals the oracle bit for bit (each column is the
     reference's fma chain, multiply_VBC.jl:126-135); then random data with alpha / beta, 7 right-hand sides,
-    column-major operands (the element staging path)."""
-    if multi_layout != "staged":
-        pytest.skip("staged-X form only")
-    monkeypatch.setenv("VBC_TILE_SMAX", str(smax))
-    monkeypatch.setenv("VBC_TILE_UMAX", str(umax))
-    # fp32 x 16 row-major RHS: the persistent kernel (spmm_tiles_xp); else spmm_tiles_x with 4 or 8 compute waves
-    # per cluster (fp64 always 4)
-    monkeypatch.setenv("VBC_TILE_PERSIST", "1" if form == "persist" else "0")
-    monkeypatch.setenv("VBC_TILE_WAVES", "8" if form == "waves8" else "4")
+    column-major operands (the element path of the epilogue)."""
     import bench
     B = bench.build_matrix("c5-mesh", dtype, 0.002)
     B.val[:] = np.random.default_rng(3).integers(-8, 9, B.val.shape)
-    assert B.info(multi=True)["planar_mask"] & 1024 and B.info(trans=False, multi=True)["planar_mask"] & 1024
+    if multi_layout == "tiles":
+        assert B.info(multi=True)["planar_mask"] & 512 and B.info(trans=False, multi=True)["planar_mask"] & 512
     Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
-    rng = np.random.default_rng(smax)
+    rng = np.random.default_rng(11)
+    tdt = torch.float32 if dtype == np.float32 else torch.float64
     for trans in (True, False):
         nx, ny = (B.m, B.n) if trans else (B.n, B.m)
         X = rng.integers(-8, 9, (nx, 16)).astype(dtype)
-        Y = torch.full((ny, 16), float("nan"), dtype=torch.float32 if dtype == np.float32 else torch.float64, device=DEV)
-        V.mul_(Y, B.T if trans else B, torch.from_numpy(X).to(DEV), engine="mfma")
-        want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64), np.zeros(ny), trans=trans)
-                         for j in range(16)], axis=1)
-        assert np.array_equal(Y.cpu().numpy(), want.astype(dtype)), trans
+        Y0 = rng.integers(-8, 9, (ny, 16)).astype(dtype)
+        for alpha, beta in ((1.0, 0.0), (2.0, -1.0)):
+            Yd = torch.from_numpy(Y0.copy()).to(DEV)
+            V.mul_(Yd, B.T if trans else B, torch.from_numpy(X).to(DEV), alpha, beta, engine="mfma")
+            want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64),
+                                   np.ascontiguousarray(Y0[:, j], dtype=np.float64), alpha, beta, trans=trans,
+                                   ref_semantics=False) for j in range(16)], axis=1)
+            assert Yd.dtype == tdt and np.array_equal(Yd.cpu().numpy(), want.astype(dtype)), (trans, alpha, beta)
         X = rng.uniform(-1, 1, (nx, 7)).astype(dtype)
         Y0 = rng.uniform(-1, 1, (ny, 7)).astype(dtype)
         Yd = as_dev(Y0, "C")
@@ -370,30 +351,3 @@ def test_tiles_staged_cluster_limits_bitwise(dtype, smax, umax, form, multi_layo
                                np.ascontiguousarray(Y0[:, j], dtype=np.float64), 0.5, -1.25, trans=trans,
                                ref_semantics=False) for j in range(7)], axis=1)
         assert rel(Yd.cpu().numpy(), want) <= (TOL64 if dtype == np.float64 else TOL32), trans
-
-
-@pytest.mark.parametrize("blob", ["64", "512"])
-def test_tiles_blob_order_scattered_stripes_bitwise(blob, multi_layout, monkeypatch):
-    """Tile layout in blob order (VBC_TILE_ORDER=1: stripes processed in compact balls of the stripe graph, so a
-    range's stripes are not contiguous columns): 16 row-major right-hand sides take the per-stripe 16-B epilogue
-    (each stripe's w x 16 block of Y), with and without beta -- integer data, every column bit for bit."""
-    if multi_layout != "tiles":
-        pytest.skip("tile layout only")
-    monkeypatch.setenv("VBC_TILE_ORDER", "1")
-    monkeypatch.setenv("VBC_TILE_BLOB", blob)
-    import bench
-    B = bench.build_matrix("c5-mesh", np.float32, 0.002)
-    B.val[:] = np.random.default_rng(5).integers(-8, 9, B.val.shape)
-    Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
-    rng = np.random.default_rng(int(blob))
-    for trans in (True, False):
-        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
-        X = rng.integers(-8, 9, (nx, 16)).astype(np.float32)
-        Y0 = rng.integers(-8, 9, (ny, 16)).astype(np.float32)
-        for alpha, beta in ((1.0, 0.0), (2.0, -1.0)):
-            Yd = torch.from_numpy(Y0.copy()).to(DEV)
-            V.mul_(Yd, B.T if trans else B, torch.from_numpy(X).to(DEV), alpha, beta, engine="mfma")
-            want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64),
-                                   np.ascontiguousarray(Y0[:, j], dtype=np.float64), alpha, beta, trans=trans,
-                                   ref_semantics=False) for j in range(16)], axis=1)
-            assert np.array_equal(Yd.cpu().numpy(), want.astype(np.float32)), (trans, alpha, beta)

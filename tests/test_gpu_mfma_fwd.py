@@ -17,16 +17,11 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(autouse=True, params=["tiles", "8", "0"], ids=["tiles", "quads", "panels"])
+@pytest.fixture(autouse=True, params=["tiles", "0"], ids=["tiles", "panels"])
 def multi_layout(request, monkeypatch):
-    """Every test on the three multi-RHS layouts (test_gpu_mfma.py): MFMA panels, VALU stripe quads, and
-    the tile-granular layout of C = Bᵀ's small tiles (VBC_PANEL_TILES=1)."""
-    if request.param == "tiles":
-        monkeypatch.setenv("VBC_PANEL_TILES", "1")
-        monkeypatch.setenv("VBC_PANEL_QUADS", "0")
-    else:
-        monkeypatch.setenv("VBC_PANEL_TILES", "0")
-        monkeypatch.setenv("VBC_PANEL_QUADS", request.param)
+    """Every test on the two multi-RHS layouts (test_gpu_mfma.py): MFMA panels, and the tile-granular layout
+    of C = Bᵀ's small tiles (VBC_PANEL_TILES=1)."""
+    monkeypatch.setenv("VBC_PANEL_TILES", "1" if request.param == "tiles" else "0")
     return request.param
 
 
