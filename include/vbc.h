@@ -24,7 +24,7 @@
 /* ABI version (major*10000 + minor*100 + patch), returned by vbc_version().  A binding checks the major
  * version at load time: 3.x changed vbc_info (VBC_INFO_SIZE bytes, written whole by vbc_get_info) and
  * added the I64 / I32 / BOOL eltypes, the sharded 2D handle and the *_ex sharded product. */
-#define VBC_VERSION 30000
+#define VBC_VERSION 30100
 #define VBC_INFO_SIZE 152
 
 #ifdef __cplusplus
@@ -223,6 +223,13 @@ VBC_API int vbc_mul_mat_ex(vbc_handle *h, int trans, int64_t nrhs, const void *X
 typedef struct vbc_sharded vbc_sharded; /* opaque */
 #define VBC_SPLIT_STRIPES 0
 #define VBC_SPLIT_ROWS 1
+/* VBC_SPLIT_AUTO: the split with the smaller predicted time of the products `flags` builds (B'x when
+ * VBC_CREATE_TRANSPOSED or no direction flag is given, B x when VBC_CREATE_FORWARD): per product the slowest
+ * shard's kernel (3.1 us + its bytes at 5.7 TB/s, both measured on one MI355X) plus the exchange through
+ * devices[0] (x broadcast + y slices gathered, or x slices + ncclReduce of y) at an ASSUMED ring-collective
+ * rate of 7 xGMI links x 76.8 GB/s x 0.6 with 2 us per ring step.  vbc_sharded_split reports
+ * the choice. */
+#define VBC_SPLIT_AUTO 2
 
 /* Same matrix arguments as vbc1d_create_ex (types: Tv, Ti, compute eltype); `flags` as vbc1d_create
  * (the layouts each shard builds). */
@@ -262,6 +269,8 @@ VBC_API int vbc_sharded_mul_ex(vbc_sharded *s, int trans, const void *x, int x_d
 
 VBC_API int vbc_sharded_destroy(vbc_sharded *s);
 VBC_API int vbc_sharded_count(const vbc_sharded *s, int *ngpus);
+/* The split the handle uses (VBC_SPLIT_STRIPES or VBC_SPLIT_ROWS; what VBC_SPLIT_AUTO chose). */
+VBC_API int vbc_sharded_split(const vbc_sharded *s, int *split);
 /* Shard g: its single-GPU handle (owned by s), its 0-based range [lo, hi) of the split dimension
  * (columns for VBC_SPLIT_STRIPES, rows for VBC_SPLIT_ROWS) and its device. */
 VBC_API int vbc_sharded_shard(const vbc_sharded *s, int g, vbc_handle **h, int64_t *lo, int64_t *hi, int *device);

@@ -22,7 +22,7 @@ VBC_VERSION_MAJOR = 3  # include/vbc.h VBC_VERSION / 10000: the vbc_info layout 
 VBC_INFO_SIZE = 152
 VBC_MUL_REFERENCE_QUIRKS = 0x1
 VBC_MAT_ROWMAJOR = 0x2
-VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = 0, 1
+VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS, VBC_SPLIT_AUTO = 0, 1, 2
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -30,7 +30,7 @@ ABI_SYMBOLS = (
     "vbc1d_create_ex", "vbc2d_create_ex", "vbc_csc_create_ex", "vbc_mul_ex", "vbc_mul_mat_ex",
     "vbc_get_info", "vbc_last_error", "vbc_version",
     "vbc1d_create_sharded", "vbc2d_create_sharded", "vbc_sharded_mul", "vbc_sharded_mul_ex", "vbc_sharded_destroy",
-    "vbc_sharded_count", "vbc_sharded_shard",
+    "vbc_sharded_count", "vbc_sharded_shard", "vbc_sharded_split",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
     "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_partition_block", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
     "vbcx_vbc_fill", "vbcx_transpose_pattern",
@@ -114,6 +114,7 @@ def lib():
         L.vbc_sharded_mul_ex.argtypes = [P, INT, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]
         L.vbc_sharded_destroy.argtypes = [P]
         L.vbc_sharded_count.argtypes = [P, C.POINTER(INT)]
+        L.vbc_sharded_split.argtypes = [P, C.POINTER(INT)]
         L.vbc_sharded_shard.argtypes = [P, INT, C.POINTER(P), C.POINTER(I64), C.POINTER(I64), C.POINTER(INT)]
         L.vbc_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
         L.vbc_mul_mat.argtypes = [P, INT, I64, P, I64, I64, P, I64, I64, D, D, INT, P, U]

@@ -413,6 +413,45 @@ int create_shard(const Fields &f, vbc_handle **out, int64_t m, int64_t n, int64_
     return vbc1d_create_ex(out, m, n, f.W, L, spl, pos, idx, ofs, nv > 0 ? val : nullptr, nv, t64, device, flags);
 }
 
+// VBC_SPLIT_AUTO (vbc.h): the split with the smaller predicted time of the products `flags` builds (B'x for
+// VBC_CREATE_TRANSPOSED or no direction flag, B x for VBC_CREATE_FORWARD).  The model is distributed.py's
+// predict_product_us for this one-process handle's exchange: the slowest shard's kernel -- a
+// measured launch-and-ramp floor plus its bytes (matrix share, x reads, y writes) at the measured streaming
+// rate -- plus the exchange through the root: x broadcast and y slices gathered (disjoint output), or x
+// slices scattered and an ncclReduce of y (partial output), at ASSUMED xGMI rates (7 links of 76.8 GB/s per
+// direction, 60 % reached by a ring collective, 2 us per ring step; no multi-GPU box was available to measure).
+constexpr double kModelT0Us = 3.1, kModelStreamGBs = 5700.0;
+constexpr double kModelCollGBs = 7 * 76.8 * 0.6, kModelStepUs = 2.0;
+
+double predict_us(const Fields &f, int csz, int N, int split, int trans)
+{
+    const int64_t L = f.L;
+    double mat = (double)csz * (double)(f.O[L] - 1) + 4.0 * (double)(f.P[L] - 1) + 4.0 * (3.0 * L + 3.0) +
+                 (f.is2d ? 4.0 * (f.K + 1) : 0.0);
+    mat /= N;
+    if (split == VBC_SPLIT_ROWS && N > 1) mat += 12.0 * (double)L * (N - 1) / N;  // every row shard keeps the headers
+    const double nx = (double)(trans ? f.m : f.n) * csz, ny = (double)(trans ? f.n : f.m) * csz;
+    const bool disj = disjoint_output(split, trans);
+    const double kern = kModelT0Us + (mat + (disj ? nx : nx / N) + (disj ? ny / N : ny)) / (kModelStreamGBs * 1e3);
+    if (N <= 1) return kern;
+    const double part = (double)(N - 1) / N, lat = (N - 1) * kModelStepUs, bw = kModelCollGBs * 1e3;
+    const double coll = disj ? (nx / bw + lat) + (part * ny / bw + lat)     // broadcast x, gather y
+                             : (part * nx / bw + lat) + (part * ny / bw + lat);  // scatter x, reduce y
+    return kern + coll;
+}
+
+int auto_split(const Fields &f, int csz, int N, unsigned flags)
+{
+    const bool t = (flags & VBC_CREATE_TRANSPOSED) || !(flags & VBC_CREATE_FORWARD);
+    const bool fw = (flags & VBC_CREATE_FORWARD) != 0;
+    double cost[2] = {0.0, 0.0};
+    for (int sp = 0; sp < 2; sp++) {
+        if (t) cost[sp] += predict_us(f, csz, N, sp, 1);
+        if (fw) cost[sp] += predict_us(f, csz, N, sp, 0);
+    }
+    return cost[VBC_SPLIT_ROWS] < cost[VBC_SPLIT_STRIPES] * (1 - 1e-9) ? VBC_SPLIT_ROWS : VBC_SPLIT_STRIPES;
+}
+
 int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *types, int ngpus, const int *devices,
                    int split, unsigned flags)
 {
@@ -420,8 +459,8 @@ int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *
     *out = nullptr;
     if (!types) return vbc::fail(VBC_INVALID_ARG, "NULL vbc_types");
     if (ngpus < 1 || !devices) return vbc::fail(VBC_INVALID_ARG, "ngpus must be >= 1 with a device list");
-    if (split != VBC_SPLIT_STRIPES && split != VBC_SPLIT_ROWS)
-        return vbc::fail(VBC_INVALID_ARG, "split must be VBC_SPLIT_STRIPES or VBC_SPLIT_ROWS");
+    if (split != VBC_SPLIT_STRIPES && split != VBC_SPLIT_ROWS && split != VBC_SPLIT_AUTO)
+        return vbc::fail(VBC_INVALID_ARG, "split must be VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS or VBC_SPLIT_AUTO");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) return vbc::fail(VBC_HIP_ERROR, "hipGetDeviceCount failed");
     bool all_same = true, distinct = true;
@@ -439,6 +478,7 @@ int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *
     if (f.vsz == 0) return vbc::fail(VBC_UNSUPPORTED_DTYPE, "unknown val_dtype");
     const int csz = vbc::elem_size(types->compute_dtype);
     if (csz == 0) return vbc::fail(VBC_UNSUPPORTED_DTYPE, "unknown compute_dtype");
+    if (split == VBC_SPLIT_AUTO) split = auto_split(f, csz, ngpus, flags);
     const char *V = f.V;
     const int vsz = f.vsz;
 
@@ -614,6 +654,13 @@ int vbc_sharded_count(const vbc_sharded *s, int *ngpus)
 {
     if (!s || !ngpus) return fail(VBC_INVALID_ARG, "NULL argument");
     *ngpus = s->ngpus;
+    return VBC_OK;
+}
+
+int vbc_sharded_split(const vbc_sharded *s, int *split)
+{
+    if (!s || !split) return fail(VBC_INVALID_ARG, "NULL argument");
+    *split = s->split;
     return VBC_OK;
 }
 

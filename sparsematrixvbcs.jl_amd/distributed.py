@@ -93,13 +93,77 @@ def row_shard(B, r0, r1):
                              val)
 
 
+# --- cost model of a sharded product --------------------------------------------
+# Shard kernel: a fixed launch-and-ramp cost plus its bytes at the streaming rate one MI355X sustains -- both
+# MEASURED on this code (a graph-replayed near-empty product 3.1 us; tools/exp/keep_probe.hip
+# streams 52-110 MB at 5.7-6.4 TB/s).  Collectives: ASSUMED, not measured (no multi-GPU box was ever
+# available to this build): each MI355X has 7 xGMI links of 153.6 GB/s (bidirectional: 76.8 GB/s per
+# direction); a ring collective over the node is taken to reach COLL_EFF of the 7 links' one-way rate, and
+# every ring step costs COLL_STEP_US of latency.  include/vbc.h states the same constants (VBC_SPLIT_AUTO).
+KERNEL_T0_US = 3.1
+KERNEL_GBS = 5700.0
+XGMI_LINKS, XGMI_LINK_GBS, COLL_EFF, COLL_STEP_US = 7, 76.8, 0.6, 2.0
+COLL_GBS = XGMI_LINKS * XGMI_LINK_GBS * COLL_EFF  # ~323 GB/s per GPU (assumption)
+
+
+def collective_us(kind, nbytes, world):
+    """Predicted time of one RCCL collective over `world` GPUs of one node (the assumptions above):
+    ring all-reduce 2(N-1)/N x bytes, all-gather / reduce-scatter / reduce (N-1)/N x bytes of the full
+    vector, broadcast the whole vector once; plus the ring's per-step latency."""
+    if world <= 1 or nbytes <= 0:
+        return 0.0
+    n = world
+    vol, steps = {"allreduce": (2.0 * (n - 1) / n, 2 * (n - 1)), "allgather": ((n - 1) / n, n - 1),
+                  "reduce": ((n - 1) / n, n - 1), "broadcast": (1.0, n - 1)}[kind]
+    return vol * nbytes / (COLL_GBS * 1e3) + steps * COLL_STEP_US
+
+
+def _matrix_bytes(B, ti=4):
+    esz = B.val.dtype.itemsize
+    return esz * int(B.ofs[-1] - 1) + ti * int(B.pos[-1] - 1) + ti * (3 * len(B.Phi) + 3)
+
+
+def predict_product_us(B, world, split, trans, replicate=True):
+    """Predicted wall time of one sharded product mul!(y, op(B), x) (us): the slowest shard's kernel (its
+    matrix bytes, its x reads and y writes) plus the collective its exchange pattern needs --
+    a disjoint output needs none (an all-gather when `replicate` asks for y on every rank), a partial
+    output one all-reduce of y.  Returns (total, kernel, collective)."""
+    esz = B.val.dtype.itemsize
+    nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+    mat = _matrix_bytes(B) / world
+    if split == "rows" and world > 1:
+        mat += 12.0 * len(B.Phi) * (world - 1) / world  # every row shard keeps every stripe's headers
+    disjoint = (split == "stripes") == bool(trans)
+    xb = esz * (nx if disjoint else nx / world)
+    yb = esz * (ny / world if disjoint else ny)
+    kern = KERNEL_T0_US + (mat + xb + yb) / (KERNEL_GBS * 1e3)
+    if disjoint:
+        coll = collective_us("allgather", esz * ny, world) if replicate else 0.0
+    else:
+        coll = collective_us("allreduce", esz * ny, world)
+    return kern + coll, kern, coll
+
+
+def choose_split(B, world, directions="tf", replicate=True):
+    """The split ("stripes" / "rows") with the smaller predicted time summed over the products a caller
+    will run (`directions`: "t" mul!(y, B', x), "f" mul!(y, B, x)); ties go to the stripe split (the
+    reference's own parallel direction, multiply_1DVBC.jl:169-177)."""
+    cost = {}
+    for split in ("stripes", "rows"):
+        cost[split] = sum(predict_product_us(B, world, split, d == "t", replicate)[0] for d in directions)
+    return "rows" if cost["rows"] < cost["stripes"] * (1 - 1e-9) else "stripes"
+
+
 class ShardedSparseMatrix1DVBC:
     """A SparseMatrix1DVBC split across the ranks of `group` (torch.distributed), one libvbc handle
     per rank.  See the module docstring for the two splits and which product needs a collective."""
 
-    def __init__(self, B, rank, world, group=None, local_mul=None, device=None, split="stripes", comm="device"):
+    def __init__(self, B, rank, world, group=None, local_mul=None, device=None, split="stripes", comm="device",
+                 directions="tf"):
+        if split == "auto":  # by the cost model: predicted kernel + collective time of the products to run
+            split = choose_split(B, world, directions)
         if split not in ("stripes", "rows"):
-            raise ValueError("split must be 'stripes' or 'rows'")
+            raise ValueError("split must be 'stripes', 'rows' or 'auto'")
         if comm not in ("device", "cpu"):
             raise ValueError("comm must be 'device' or 'cpu'")
         self.m, self.n, self.W = B.m, B.n, B.W
@@ -221,8 +285,8 @@ class MultiGPUSparseMatrix1DVBC:
     def __init__(self, B, devices=(0,), split="stripes", transposed=True, forward=True, serial=False):
         import ctypes as C
         from . import _lib as _L
-        if split not in ("stripes", "rows"):
-            raise ValueError("split must be 'stripes' or 'rows'")
+        if split not in ("stripes", "rows", "auto"):
+            raise ValueError("split must be 'stripes', 'rows' or 'auto'")
         self.m, self.n, self.W = B.m, B.n, B.W
         self.val = B.val  # eltype queries (mul_ computes in eltype(y))
         self.dtype = B.val.dtype
@@ -234,7 +298,7 @@ class MultiGPUSparseMatrix1DVBC:
         t = _L.vbc_types(_L.dtype_code(B.val.dtype), 64, _L.compute_code(B.val.dtype), 0)
         devs = (C.c_int * len(self.devices))(*self.devices)
         h = C.c_void_p()
-        kind = _L.VBC_SPLIT_STRIPES if split == "stripes" else _L.VBC_SPLIT_ROWS
+        kind = {"stripes": _L.VBC_SPLIT_STRIPES, "rows": _L.VBC_SPLIT_ROWS, "auto": _L.VBC_SPLIT_AUTO}[split]
         if self.is2d:
             _L.check(_L.lib().vbc2d_create_sharded(
                 C.byref(h), B.m, B.n, B.U, B.W, len(B.Pi), B.Pi.spl.ctypes.data, len(B.Phi), B.Phi.spl.ctypes.data,
@@ -247,6 +311,9 @@ class MultiGPUSparseMatrix1DVBC:
                 "create_sharded")
         self._h = h
         self.compute = t.compute_dtype
+        sp = C.c_int()
+        _L.check(_L.lib().vbc_sharded_split(h, C.byref(sp)), "split")
+        self.split = "stripes" if sp.value == _L.VBC_SPLIT_STRIPES else "rows"  # (what VBC_SPLIT_AUTO chose)
 
     @property
     def shape(self):

@@ -28,7 +28,7 @@ const VBC_MEM_DEVICE, VBC_MEM_HOST = Cint(0), Cint(1)
 const VBC_CREATE_TRANSPOSED, VBC_CREATE_FORWARD = Cuint(1), Cuint(2)
 const VBC_CREATE_MULTI, VBC_CREATE_MULTI_FORWARD = Cuint(4), Cuint(16)  # matrix-core panels of B and of Bᵀ
 const VBC_MUL_REFERENCE_QUIRKS = Cuint(1)
-const VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS = Cint(0), Cint(1)
+const VBC_SPLIT_STRIPES, VBC_SPLIT_ROWS, VBC_SPLIT_AUTO = Cint(0), Cint(1), Cint(2)
 
 # the eltypes the reference's tests use (runtests.jl:15-16) and their vbc_dtype codes
 vbc_dtype(::Type{Float64}) = VBC_F64
@@ -234,8 +234,10 @@ const HIPShardedSparseMatrix1DVBC = HIPShardedSparseMatrix  # round-2 name
 
 const VBC_CREATE_SERIAL = Cuint(8)
 
+_split_code(split) = split === :stripes ? VBC_SPLIT_STRIPES : split === :rows ? VBC_SPLIT_ROWS : VBC_SPLIT_AUTO
+
 function _sharded_flags(split, forward, transposed, serial)
-    split in (:stripes, :rows) || throw(ArgumentError("split must be :stripes or :rows"))
+    split in (:stripes, :rows, :auto) || throw(ArgumentError("split must be :stripes, :rows or :auto"))
     return (transposed ? VBC_CREATE_TRANSPOSED : Cuint(0)) | (forward ? VBC_CREATE_FORWARD : Cuint(0)) |
            (serial ? VBC_CREATE_SERIAL : Cuint(0))
 end
@@ -252,7 +254,7 @@ function HIPShardedSparseMatrix(B::SparseMatrix1DVBC{W, Tv, Ti}; devices=0:7, sp
         (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Cvoid}, Int64,
          Ptr{VbcTypes}, Cint, Ptr{Cint}, Cint, Cuint),
         h, B.m, B.n, W, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val), t, length(devs), devs,
-        split === :stripes ? VBC_SPLIT_STRIPES : VBC_SPLIT_ROWS, flags))
+        _split_code(split), flags))
     M = HIPShardedSparseMatrix(B, h[], cdt)
     finalizer(M -> ccall((:vbc_sharded_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle), M)
     return M
@@ -269,13 +271,20 @@ function HIPShardedSparseMatrix(B::SparseMatrixVBC{U, W, Tv, Ti}; devices=0:7, s
         (Ptr{Ptr{Cvoid}}, Int64, Int64, Int64, Int64, Int64, Ptr{Ti}, Int64, Ptr{Ti}, Ptr{Ti}, Ptr{Ti}, Ptr{Ti},
          Ptr{Cvoid}, Int64, Ptr{VbcTypes}, Cint, Ptr{Cint}, Cint, Cuint),
         h, B.m, B.n, U, W, length(B.Π), B.Π.spl, length(B.Φ), B.Φ.spl, B.pos, B.idx, B.ofs, B.val, length(B.val), t,
-        length(devs), devs, split === :stripes ? VBC_SPLIT_STRIPES : VBC_SPLIT_ROWS, flags))
+        length(devs), devs, _split_code(split), flags))
     M = HIPShardedSparseMatrix(B, h[], cdt)
     finalizer(M -> ccall((:vbc_sharded_destroy, libvbc), Cint, (Ptr{Cvoid},), M.handle), M)
     return M
 end
 
 Base.size(A::HIPShardedSparseMatrix) = size(A.host)
+
+"The split a sharded matrix uses (:stripes or :rows; what split = :auto chose by the cost model, DESIGN.md §7)."
+function split_kind(A::HIPShardedSparseMatrix)
+    sp = Ref{Cint}(0)
+    check(ccall((:vbc_sharded_split, libvbc), Cint, (Ptr{Cvoid}, Ptr{Cint}), A.handle, sp))
+    return sp[] == VBC_SPLIT_STRIPES ? :stripes : :rows
+end
 Base.size(A::HIPShardedSparseMatrix, d::Integer) = size(A.host, d)
 Base.eltype(A::HIPShardedSparseMatrix) = eltype(A.host)
 

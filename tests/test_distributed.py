@@ -135,3 +135,30 @@ def test_stripe_split_balance_and_reassembly():
         assert np.array_equal(np.concatenate(vals), B.val[:B.ofs[-1] - 1])
         assert np.array_equal(np.concatenate(idxs), B.idx)
         assert max(share) <= 1.02 * sum(share) / parts + 64 * 40
+
+
+def test_split_cost_model_and_auto_choice():
+    """distributed.predict_product_us / choose_split: a disjoint output needs no collective
+    (an all-gather when y is replicated), a partial output one all-reduce; the automatic split makes the
+    requested direction disjoint (forward only -> rows, transposed only -> stripes), ties go to stripes."""
+    D = V.distributed
+    B = V.synthetic.standin("GHS_psdef/ldoor", scale=0.01).T.tocsc()
+    B = V.SparseMatrix1DVBC[8](B, V.StrictChunker(8))
+    for world in (2, 4, 8):
+        t_s, k_s, c_s = D.predict_product_us(B, world, "stripes", trans=True, replicate=False)
+        t_r, k_r, c_r = D.predict_product_us(B, world, "rows", trans=True, replicate=False)
+        assert c_s == 0.0 and c_r > 0.0 and t_s < t_r
+        f_s = D.predict_product_us(B, world, "stripes", trans=False)
+        f_r = D.predict_product_us(B, world, "rows", trans=False)
+        assert f_s[2] > f_r[2] > 0.0  # all-reduce vs all-gather of the replicated y
+        assert D.choose_split(B, world, "f") == "rows"
+        assert D.choose_split(B, world, "t") == "stripes"
+        assert D.choose_split(B, world, "tf") == "stripes"
+    assert D.predict_product_us(B, 1, "stripes", True)[2] == 0.0
+    # the collective model: all-reduce of 7.6 MB over 8 GPUs, the assumption stated in the module
+    ar = D.collective_us("allreduce", 7_617_624, 8)
+    assert abs(ar - (2 * 7 / 8 * 7_617_624 / (D.COLL_GBS * 1e3) + 14 * D.COLL_STEP_US)) < 1e-9
+    S = D.ShardedSparseMatrix1DVBC(B, 0, 4, split="auto", directions="f", local_mul=lambda *a: None)
+    assert S.split == "rows"
+    S = D.ShardedSparseMatrix1DVBC(B, 0, 4, split="auto", directions="t", local_mul=lambda *a: None)
+    assert S.split == "stripes"

@@ -327,3 +327,24 @@ def test_sharded_serial_flag_forward_rows():
         S.release()
     assert same_family_seen
     B.release()
+
+
+@pytest.mark.parametrize("forward,transposed,want", [(True, False, "rows"), (False, True, "stripes"),
+                                                     (True, True, "stripes")])
+def test_sharded_auto_split(forward, transposed, want):
+    """VBC_SPLIT_AUTO (vbc.h): the split with the smaller predicted kernel + exchange time of the
+    products the handle builds -- forward only: rows (disjoint y, no reduce); B'x: stripes -- reported by
+    vbc_sharded_split, and the products of the chosen split match the oracle."""
+    B = V.synthetic.standin("GHS_psdef/ldoor", scale=0.005).T.tocsc()
+    B = V.SparseMatrix1DVBC[8](B, V.StrictChunker(8))
+    S = D.MultiGPUSparseMatrix1DVBC(B, devices=[0, 0, 0, 0], split="auto", forward=forward, transposed=transposed)
+    assert S.split == want
+    rng = np.random.default_rng(9)
+    R = ref_of(B)
+    for trans in ([True] if transposed else []) + ([False] if forward else []):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        x = rng.uniform(-1, 1, nx)
+        y = dev(np.full(ny, np.nan))
+        V.mul_(y, S.T if trans else S, dev(x))
+        assert rel(y.cpu().numpy(), O.mul(R, x, np.zeros(ny), trans=trans)) <= TOL64, trans
+    S.release()
