@@ -177,6 +177,8 @@ def test_north_star_full_size_vs_oracle(workload):
     V.mul_(y, B.T, dev(xt))
     ref = O.mul(R, xt, np.zeros(B.n), trans=True, nthreads=threads())
     assert rel(y.cpu().numpy(), ref) <= 1e-10
+    if workload == "fe3d":  # the automatic layout choice reaches the lane-stream family (vbc_info planar_mask bit 2)
+        assert B.info(0, True)["planar_mask"] & 4
     B.release()
     yf = torch.empty(B.m, dtype=torch.float64, device=DEV)
     V.mul_(yf, B, dev(xf))
@@ -227,3 +229,27 @@ def test_trspmv_column_blocking(monkeypatch, dtype, ragged):
     yf = torch.zeros(m, dtype=tdt, device=DEV)
     V.mul_(yf, C, dev(xf))
     assert rel(yf.cpu().numpy(), A.astype(np.float64) @ xf.astype(np.float64)) <= tol
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("workload", ["c5", "c5-mesh"])
+def test_c5_full_size_four_columns(workload):
+    """BASELINE C5 at the bench's full size (2D VBC, 1e8 fp32 values, 16 row-major right-hand sides): the
+    multi-RHS product in both directions (B'X on B's layout, B·X on Bᵀ's), 4 of the 16 columns against the
+    oracle's per-column product in fp64 (the reference has no matrix mul!, multiply_VBC.jl:194-197, so its
+    semantics is column by column), normwise 1e-5."""
+    import bench
+    B = bench.build_matrix(workload, np.float32)
+    Rd = O.RefVBC(B.m, B.n, B.U, B.W, B.Pi.spl, B.Phi.spl, B.pos, B.idx, B.ofs, B.val.astype(np.float64))
+    rng = np.random.default_rng(0xC0FFEE)
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        X = rng.uniform(-1, 1, (nx, 16)).astype(np.float32)
+        Y = torch.full((ny, 16), float("nan"), dtype=torch.float32, device=DEV)
+        V.mul_(Y, B.T if trans else B, dev(X))
+        got = Y.cpu().numpy()
+        for j in (0, 5, 10, 15):
+            ref = O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64), np.zeros(ny), trans=trans,
+                        nthreads=threads())
+            assert rel(got[:, j], ref) <= 1e-5, (workload, trans, j)
+        B.release()

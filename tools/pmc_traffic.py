@@ -20,9 +20,9 @@ ROOT = Path(__file__).resolve().parent.parent
 KERNEL = "spmv_ranges"  # --kernel overrides
 
 
-def run_pass(counters, outdir, bench_args, kernel=KERNEL):
+def run_pass(counters, outdir, bench_args, kernel=KERNEL, program="bench.py"):
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", str(outdir),
-           "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), *bench_args]
+           "-o", "pmc", "--", sys.executable, str(ROOT / program), *bench_args]
     print("pass:", " ".join(counters), flush=True)
     subprocess.run(cmd, check=True, cwd=ROOT, timeout=180)
     files = glob.glob(str(outdir / "**" / "*counter_collection.csv"), recursive=True)
@@ -46,18 +46,24 @@ def main():
     ap.add_argument("--counters", default="", help="extra counter passes, ';'-separated groups")
     ap.add_argument("--kernel", default=KERNEL, help="kernel name substring to attribute counters to")
     ap.add_argument("--tag", default="", help="suffix of the output file name (ablation runs)")
+    ap.add_argument("--program", default="", help="run this script with --extra's arguments instead of bench.py "
+                    "(e.g. tools/shard_time.py for one shard of a split)")
     ap.add_argument("--read-factor", type=float, default=2.0,
                     help="FETCH_SIZE correction: 2 for 16-B/lane streaming reads (gfx950 half-count), 1 for "
                          "dword loads and gathers")
     args = ap.parse_args()
     out = ROOT / "gpurun_out" / "pmc"
-    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--no-parity", "--workload", args.workload,
-                  "--dtype", args.dtype] + args.extra.split()
+    if args.program:
+        bench_args = ["--steps", str(args.steps), "--warmup", "2", "--workload", args.workload, "--dtype",
+                      args.dtype] + args.extra.split()
+    else:
+        bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-secondary", "--no-parity",
+                      "--workload", args.workload, "--dtype", args.dtype] + args.extra.split()
     res = {}
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"]] + [g.split(",") for g in args.counters.split(";") if g]
     for i, counters in enumerate(passes):
         try:
-            vals = run_pass(counters, out / f"pass{i}", bench_args, args.kernel)
+            vals = run_pass(counters, out / f"pass{i}", bench_args, args.kernel, args.program or "bench.py")
         except subprocess.SubprocessError as e:  # a counter set the profiler cannot serve
             print("pass failed:", counters, e, flush=True)
             if i < 2:
@@ -69,6 +75,7 @@ def main():
     write_kb = res["WRITE_SIZE"]["mean"]
     summary = {
         "workload": args.workload, "dtype": args.dtype, "kernel": args.kernel,
+        "program": (args.program + " " + args.extra).strip() or None,
         "method": "rocprofv3 --kernel-trace --pmc, FETCH_SIZE and WRITE_SIZE in separate passes; "
                   f"read bytes = {args.read_factor:g} x FETCH_SIZE (gfx950 counts 16-B/lane streaming reads "
                   "at half, MI355X_MICROARCH.md §HBM; dword loads and gathers are counted in full)",

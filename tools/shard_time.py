@@ -1,11 +1,14 @@
-"""Per-shard product times of the N-way stripe split, measured one shard at a time on ONE GPU.
+"""Per-shard product times of the N-way stripe or row split, measured one shard at a time on ONE GPU.
 
 The driver's 8-GPU scaling run is not ours to launch; this predicts it from the single-GPU box:
-every shard of distributed.stripe_split(B, N) gets its own handle and K graph-replayed products
-(bench.timed_products), and the slowest shard bounds the strong-scaling step time of bench.py
---gpus N (the rank's kernel time; B'x on the stripe split has no data-path collective).
+every shard of distributed.stripe_split(B, N) (or row_split with --split rows) gets its own handle and K
+graph-replayed products (bench.timed_products), and the slowest shard bounds the strong-scaling step time
+of bench.py --gpus N (the rank's kernel time).  Stripe split: B'x has disjoint y slices (no data-path
+collective), --forward adds each shard's B x (a partial y -> one all-reduce).  Row split: B x has disjoint
+y slices, B'x a partial y.  Every line also carries the cost model's end-to-end figure per direction
+(distributed.predict_product_us: the MEASURED slowest shard plus the ASSUMED collective).
 
-    python tools/shard_time.py --workload fe --worlds 1,2,4,8 [--dtype f64 --steps 50]
+    python tools/shard_time.py --workload ldoor --worlds 1,2,4,8 [--split rows] [--forward] [--ranks 0]
 """
 import argparse
 import json
@@ -26,7 +29,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--forward", action="store_true", help="also time the forward product B_r x_r of every shard")
+    ap.add_argument("--forward", action="store_true", help="also time the other direction of every shard")
+    ap.add_argument("--split", default="stripes", choices=["stripes", "rows"])
+    ap.add_argument("--ranks", default="", help="time only these shards (comma list; PMC runs of one shard)")
     args = ap.parse_args()
     import torch
 
@@ -38,57 +43,70 @@ def main():
     device = torch.device("cuda", 0)
     B = bench.build_matrix(args.workload, dtype, args.scale)
     total = bench.algorithmic_bytes(B, esz)
-    x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, B.m).astype(dtype)).to(device)
     stream = torch.cuda.Stream(device)
     base = None
     fbase = [None]
+    D = V.distributed
+    rows = args.split == "rows"
+    # the split's main product has disjoint y: B'x for stripes, B x for rows; --forward times the other one
+    main_t = not rows
     for world in (int(w) for w in args.worlds.split(",")):
-        cuts = V.distributed.stripe_split(B, world)
+        cuts = D.row_split(B, world) if rows else D.stripe_split(B, world)
         per = []
-        for r in range(world):
-            S, _ = V.distributed.shard(B, int(cuts[r]), int(cuts[r + 1])) if world > 1 else (B, 0)
-            y = torch.empty(S.n, dtype=x.dtype, device=device)
-            St = S.T
-            with torch.cuda.stream(stream):
-                S.handle(0, True)
-                for _ in range(args.warmup):
-                    V.mul_(y, St, x)
-            torch.cuda.synchronize(device)
-            wall, ev_ms, _ = bench.timed_products(lambda: V.mul_(y, St, x), args.steps, device, stream, 1)
-            rec = {"rank": r, "stripes": int(cuts[r + 1] - cuts[r]), "bytes": bench.algorithmic_bytes(S, esz),
-                   "us_event": round(ev_ms * 1e3, 2), "us_wall": round(wall / args.steps * 1e6, 2),
-                   "kernel": bench.kernel_name(S, 0, 1)}
-            if args.forward:  # C3's forward leg: mul!(y, B_r, x_r) on the shard -> a partial y of length m
-                xf = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, S.n).astype(dtype)).to(device)
-                yf = torch.empty(S.m, dtype=x.dtype, device=device)
+        ranks = [int(r) for r in args.ranks.split(",")] if args.ranks else range(world)
+        for r in ranks:
+            if world == 1:
+                S = B
+            elif rows:
+                S = D.row_shard(B, int(cuts[r]), int(cuts[r + 1]))
+            else:
+                S, _ = D.shard(B, int(cuts[r]), int(cuts[r + 1]))
+
+            def time_dir(trans):
+                nx, ny = (S.m, S.n) if trans else (S.n, S.m)
+                xs = torch.from_numpy(np.random.default_rng(1 if trans else 2).uniform(-1, 1, nx).astype(dtype)).to(device)
+                ys = torch.empty(ny, dtype=xs.dtype, device=device)
+                op = S.T if trans else S
                 with torch.cuda.stream(stream):
-                    S.handle(0, False)
+                    S.handle(0, trans)
                     for _ in range(args.warmup):
-                        V.mul_(yf, S, xf)
+                        V.mul_(ys, op, xs)
                 torch.cuda.synchronize(device)
-                fw, fev, _ = bench.timed_products(lambda: V.mul_(yf, S, xf), args.steps, device, stream, 1)
-                rec.update(fwd_us_event=round(fev * 1e3, 2), fwd_us_wall=round(fw / args.steps * 1e6, 2),
-                           fwd_kernel=bench.kernel_name(S, 0, 1, trans=False),
-                           allreduce_bytes=int(S.m * esz) if world > 1 else 0)
-                del xf, yf
+                wall, ev_ms, _ = bench.timed_products(lambda: V.mul_(ys, op, xs), args.steps, device, stream, 1)
+                return round(ev_ms * 1e3, 2), round(wall / args.steps * 1e6, 2), bench.kernel_name(S, 0, 1, trans=trans)
+
+            ev, wall, kern = time_dir(main_t)
+            rec = {"rank": r, "range": [int(cuts[r]), int(cuts[r + 1])], "bytes": bench.algorithmic_bytes(S, esz),
+                   "us_event": ev, "us_wall": wall, "kernel": kern}
+            if args.forward:  # the other direction: a partial y (length m for stripes' B x, n for rows' B'x)
+                fev, fwall, fkern = time_dir(not main_t)
+                rec.update(fwd_us_event=fev, fwd_us_wall=fwall, fwd_kernel=fkern,
+                           allreduce_bytes=int((S.n if rows else S.m) * esz) if world > 1 else 0)
             per.append(rec)
             if world > 1:
                 S.release()
-            del y
         slow = max(p["us_wall"] for p in per)
         if base is None:
             base = slow
-        line = {"workload": args.workload, "dtype": args.dtype, "world": world,
+        line = {"workload": args.workload, "dtype": args.dtype, "split": args.split, "world": world,
+                "product": "B'x (disjoint y)" if main_t else "B x (disjoint y)",
                 "max_us_wall": slow, "speedup_vs_first": round(base / slow, 3),
                 "value_GBs": round(total / (slow * 1e-6) / 1e9, 1), "shards": per}
+        # cost model end to end: measured slowest shard + assumed collective (y replicated)
+        kind = "allgather"
+        line["model_e2e_us"] = {"main": round(slow + D.collective_us(kind, esz * (B.n if main_t else B.m), world), 2),
+                                "main_sharded_y": slow, "collective": kind + " of y (assumed rates)"}
         if args.forward:
             fslow = max(p["fwd_us_wall"] for p in per)
             if fbase[0] is None:
                 fbase[0] = fslow
-            line.update(fwd_max_us_wall=fslow, fwd_speedup_vs_first=round(fbase[0] / fslow, 3),
+            other = esz * (B.m if main_t else B.n)
+            line.update(other_product="B x (partial y)" if main_t else "B'x (partial y)",
+                        fwd_max_us_wall=fslow, fwd_speedup_vs_first=round(fbase[0] / fslow, 3),
                         fwd_allreduce_bytes=per[0]["allreduce_bytes"],
-                        fwd_note="kernel only: each rank's partial y then goes through one all_reduce(sum) of "
-                                 "allreduce_bytes over RCCL (not timed on one GPU)")
+                        fwd_model_e2e_us=round(fslow + D.collective_us("allreduce", other, world), 2),
+                        fwd_note="kernel only, then one all_reduce(sum) of the partial y over RCCL (model: assumed "
+                                 "rates, distributed.collective_us)")
         print(json.dumps(line), flush=True)
         torch.cuda.empty_cache()
 
