@@ -122,6 +122,9 @@ def kernel_name(B, local, k, trans=True):
     if not trans:
         inf = B.info(local, False)
         pm, R = inf["planar_mask"], inf["fwd_run"]
+        if pm & 2048:
+            return ("vbc::spmv_planar_pair<FASTE, NB, KC, MASK, DOT=true> (forward lane pairs: 3 x 3 node blocks "
+                    "transposed into the B'x lane-pair layout, per-block dot products, csrc/vbc_planar.h)")
         if pm & 256:
             return ("the transposed kernels on C = B^T (forward of a mixed-width matrix: vbc::spmv_split_multi "
                     "fused split over C's row groups, csrc/vbc_planar.h)")

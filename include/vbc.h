@@ -316,7 +316,8 @@ typedef struct vbc_info {
                                widths: one fused launch instead of one per width); bit 9: the multi-RHS
                                layout has tile-granular buckets (u, w <= 4 tiles: one key and one u-row X
                                block per tile, spmm_tiles); bit 10: reserved (0; round 5's staged-X tile
-                               form) */
+                               form); bit 11: the forward product of 3 x 3 fp64 node blocks in the lane-pair
+                               layout of the transposed blocks (spmv_planar_pair DOT, round 6) */
 } vbc_info;
 
 /* Writes VBC_INFO_SIZE bytes: `info` must be a vbc_info of this header's version (vbc_version() /

@@ -416,10 +416,12 @@ static int slot_runs(const vbc_handle *h, const std::vector<Entry> &ents, const 
 
 // Lay out a slotted bucket: chunk rows row-major over the slots, PAD / LAST keys, ranges of whole
 // chunks balanced by rows.  ents[sbeg[q] ...] are segment q's entries (keys = gather index only).
+// pair_only: build nothing and return kBuildDeclined unless the bucket takes the lane-pair layout.
+constexpr int kBuildDeclined = -1;
 static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vector<Entry> &ents,
                        const std::vector<int64_t> &sbeg0, const std::vector<int32_t> &out0, int64_t total_entries,
                        const char *val, Arena &ar, int &range0, PendingSlot &ps,
-                       const std::vector<int64_t> &order = {}, bool mask = false, int ks = 1)
+                       const std::vector<int64_t> &order = {}, bool mask = false, int ks = 1, bool pair_only = false)
 {
     const int esz = h->esz;
     // segment q of the layout is input segment order[q] (natural order when `order` is empty)
@@ -497,6 +499,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
         if (!drop) break;
         pair = false;
     }
+    if (pair_only && !pair) return kBuildDeclined;  // (nothing reserved yet)
     int64_t nr = (int64_t)std::llround(share);
     // one wave per SIMD of the chip for this bucket (the target is CUs x occupancy x waves per workgroup)
     const double quantum = share / std::max(1, planar ? h->occ_p : h->occ_s[kind]);
@@ -1791,6 +1794,50 @@ static int build_fwd_lanes(vbc_handle *h, int w, int R, const std::vector<Entry>
     return build_lanes(h, R, e2, sb, out, w, sb[nseg], tv.data(), ar, ps);
 }
 
+// Forward lane pairs (round 6): fp64 3 x 3 node blocks (w = 3 stripes, output rows in runs of R = 3) in the
+// lane-pair layout of the B'x product (run_pair) with every block TRANSPOSED -- a "stripe" of that layout is
+// an output node run q (rows 3q .. 3q+2), its runs the node's blocks in stripe order, a run's 3 "rows" the
+// block's columns d gathering x[j + d] -- folded in DOT mode (SlotBin::dot: each output row's dot product with
+// the block's x slice added per block, the reference's forward association, multiply_1DVBC.jl:34, :62-71).
+// The forward row-run layout (build_fwd_runs) gathers a 24-B x slice per lane per block in two requests; the
+// lane pair shares one 16-B gather per lane (ldoor stand-in fp64: its B'x in this layout runs 0.81 of the
+// HBM roofline, the forward row runs 0.69).  Returns kBuildDeclined (nothing built) when the bucket would not
+// take the pair layout (too few blocks per node, or a small matrix that takes the split product).
+static int build_fwd_pair(vbc_handle *h, int w, int R, const std::vector<Entry> &ents, const std::vector<int64_t> &sbeg,
+                          int64_t m, int64_t n, const char *val, Arena &ar, PendingSlot &ps)
+{
+    if (h->esz != 8 || w != 3 || R != 3 || h->planar_pair == 0 || h->slot_planar == 0 || h->slot_runs == 0 || m % R)
+        return kBuildDeclined;
+    const int esz = h->esz;
+    const int64_t nseg = m / R;
+    std::vector<int64_t> sb(nseg + 1, 0);
+    for (int64_t q = 0; q < nseg; q++) sb[q + 1] = sb[q] + (sbeg[R * q + 1] - sbeg[R * q]) * w;
+    if (sb[nseg] == 0 || sb[nseg] >= (int64_t(1) << 31)) return kBuildDeclined;
+    std::vector<Entry> e2((size_t)sb[nseg]);
+    std::vector<char> tv((size_t)sb[nseg] * R * esz);  // the blocks transposed: [block][d][r]
+    for (int64_t q = 0; q < nseg; q++) {
+        const int64_t nb = sbeg[R * q + 1] - sbeg[R * q];
+        for (int64_t k = 0; k < nb; k++) {
+            const uint32_t col = ents[sbeg[R * q] + k].key & kSlotIdx;
+            for (int d = 0; d < w; d++) {
+                const int64_t i = sb[q] + k * w + d;
+                e2[i] = {col + (uint32_t)d, i * R};
+                for (int r = 0; r < R; r++)
+                    std::memcpy(tv.data() + (i * R + r) * esz, val + (ents[sbeg[R * q + r] + k].voff + d) * esz, (size_t)esz);
+            }
+        }
+    }
+    std::vector<int32_t> out(nseg);
+    for (int64_t q = 0; q < nseg; q++) out[q] = (int32_t)(R * q);
+    std::vector<int64_t> order;
+    bool mask = false;
+    if (!want_slots(h, 0, w, sb, sb[nseg], n, order, &mask, w)) return kBuildDeclined;
+    int zero = 0;
+    const int st = build_slots(h, 0, w, w, e2, sb, out, sb[nseg], tv.data(), ar, zero, ps, order, mask, 1, true);
+    if (st == VBC_OK) ps.b.dot = 1;
+    return st;
+}
+
 // Forward layout: per width bucket, segments = output rows with entries of that width (ascending),
 // entries = (row, stripe) blocks ordered by stripe within the row.  With a single bucket, a slotted
 // layout takes every row as a segment (affine, no fill list).
@@ -1882,7 +1929,13 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
             if (lanes) {
                 if (int st = build_fwd_lanes(h, w, R, ents, sbeg, s.m, val, ar, ps)) return st;
             }
-            if (lanes || (R > 1 && build_fwd_runs(h, w, R, ents, sbeg, s.m, val, ar, zero, ps))) {
+            bool fpair = false;
+            if (!lanes && R == 3) {
+                const int st = build_fwd_pair(h, w, R, ents, sbeg, s.m, s.n, val, ar, ps);
+                if (st != VBC_OK && st != kBuildDeclined) return st;
+                fpair = st == VBC_OK;
+            }
+            if (lanes || fpair || (R > 1 && build_fwd_runs(h, w, R, ents, sbeg, s.m, val, ar, zero, ps))) {
                 std::vector<PendingSlot> one;
                 one.push_back(std::move(ps));
                 commit_launch_keys(h, one, ar);
@@ -1890,6 +1943,9 @@ static int build_forward(vbc_handle *h, const Stripes &s, const char *val, Arena
                 if (lanes)  // real values, one key per block, nlive per row, the tile tables, y
                     h->bytes_f += p1.real * (int64_t)R * h->esz + p1.key_bytes + p1.rows * 4 +
                                   (int64_t)p1.b.ntiles * (8 + 128) + s.m * h->esz;
+                else if (fpair)  // run-rows of 32 blocks (288 values), one key per block, y
+                    h->bytes_f += p1.rows * 288 * (int64_t)h->esz + p1.key_bytes + (p1.b.mask ? p1.rows * 4 : 0) +
+                                  s.m * h->esz;
                 else
                     h->bytes_f += p1.rows * p1.b.rpi * (int64_t)w * R * h->esz + p1.key_bytes + s.m * h->esz;
                 std::fill(any.begin(), any.end(), 1);
@@ -3203,6 +3259,7 @@ int vbc_get_info(const vbc_handle *h, vbc_info *info)
                 if (b.mask && !b.lanes) info->planar_mask |= 2;
                 if (b.split > 1) info->planar_mask |= 8;
                 if (b.lanes) info->planar_mask |= 16;
+                if (b.dot) info->planar_mask |= 2048;  // forward lane pairs (run_pair DOT)
             }
     if (h->has_ft)  // the forward product on C = Bᵀ: its split bins sum P slices too (bit 3, as a split forward)
         for (const SlotBin &b : h->lft.pbins)

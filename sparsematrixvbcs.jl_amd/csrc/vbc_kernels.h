@@ -124,6 +124,9 @@ struct SlotBin {
     const int32_t *trow;   // ntiles + 1: first row of each tile
     const int32_t *tseg;   // ntiles + 1: first segment of each tile
     const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)
+    int32_t dot;           // pair layout of a forward product (vbc_planar.h run_pair DOT): per block, each output
+                           // row's dot product with the x slice is added to its sum (the reference's forward order)
+    int32_t pad_dot;
 };
 
 // Runs with holes (SlotBin::holes): the run's stored-row mask above the gather index of its first key.

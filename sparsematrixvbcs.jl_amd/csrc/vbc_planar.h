@@ -711,7 +711,13 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_fwd_split(const SlotBin b,
 // second one reads C and its neighbour, its third the even partner's D line: merged requests).
 // MASK (SlotBin::mask): stripe slots >= nlive[run-row] are padding; their lanes read pair 0's keys and
 // values (lane parity kept) and fold nothing.
-template <int NRS, bool FASTE, int NB, bool KC, bool MASK = false>
+// DOT (SlotBin::dot, the forward product mul!(y, B, x) of 3 x 3 node blocks, round 6): the layout is that of
+// the blocks TRANSPOSED -- a "stripe" is an output node run of 3 rows, a run-row one block of it (stripes in
+// order), its "rows" the block's 3 columns gathering x[j .. j+2] -- and each lane adds, per block, the dot
+// product of its output row with the x slice to its accumulator: y[i] += (B[i][j] x[j] + B[i][j+1] x[j+1]) +
+// B[i][j+2] x[j+2], blocks in stripe order -- the association of the reference's serial forward loop
+// (multiply_1DVBC.jl:34, :62-71) and of run_planar_fwd, so the forward product stays bit-identical to it.
+template <int NRS, bool FASTE, int NB, bool KC, bool MASK = false, bool DOT = false>
 __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, const double *__restrict__ x,
                                          double *__restrict__ y, double alpha, double beta, bool rd, char *lds_wave,
                                          int *lds_out)
@@ -844,11 +850,19 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
             if (pad) x0 = x1 = x2 = 0.0;
             // even: v[0] = {r0c0, r0c1}, v[1] = {r1c0, r1c1}, v[2] = {r2c0, r2c1}
             // odd:  v[0] = {r0c2, r1c2}, v[1].x = r2c2
-            const double n0 = odd ? fmadd(v[j][1].x, x2, fmadd(v[j][0].y, x1, fmadd(v[j][0].x, x0, acc0)))
-                                  : fmadd(v[j][2].x, x2, fmadd(v[j][1].x, x1, fmadd(v[j][0].x, x0, acc0)));
-            const double n1 = fmadd(v[j][2].y, x2, fmadd(v[j][1].y, x1, fmadd(v[j][0].y, x0, acc1)));
-            acc0 = live ? n0 : acc0;
-            acc1 = live ? n1 : acc1;
+            if constexpr (DOT) {
+                const double d0 = odd ? fmadd(v[j][1].x, x2, fmadd(v[j][0].y, x1, v[j][0].x * x0))
+                                      : fmadd(v[j][2].x, x2, fmadd(v[j][1].x, x1, v[j][0].x * x0));
+                const double d1 = fmadd(v[j][2].y, x2, fmadd(v[j][1].y, x1, v[j][0].y * x0));
+                acc0 = (live && !pad) ? acc0 + d0 : acc0;
+                acc1 = (live && !pad) ? acc1 + d1 : acc1;
+            } else {
+                const double n0 = odd ? fmadd(v[j][1].x, x2, fmadd(v[j][0].y, x1, fmadd(v[j][0].x, x0, acc0)))
+                                      : fmadd(v[j][2].x, x2, fmadd(v[j][1].x, x1, fmadd(v[j][0].x, x0, acc0)));
+                const double n1 = fmadd(v[j][2].y, x2, fmadd(v[j][1].y, x1, fmadd(v[j][0].y, x0, acc1)));
+                acc0 = live ? n0 : acc0;
+                acc1 = live ? n1 : acc1;
+            }
             const uint32_t lastw = KC ? bs[j] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[j]);
             if (R + j < R1 && (lastw & kLast)) flush();
         }
@@ -871,7 +885,7 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
     }
 }
 
-template <bool FASTE, int NB, bool KC, bool MASK = false>
+template <bool FASTE, int NB, bool KC, bool MASK = false, bool DOT = false>
 __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin b,
                                                                   const double *__restrict__ x, double *__restrict__ y,
                                                                   double alpha, double beta, int rd_i)
@@ -887,7 +901,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmv_planar_pair(const SlotBin 
 #ifndef VBC_PAIR_NRS
 #define VBC_PAIR_NRS 4  // run-rows per pipeline stage (ldoor stand-in: 2 -> 82, 3 -> 80, 4 -> 77 us)
 #endif
-    run_pair<VBC_PAIR_NRS, FASTE, NB, KC, MASK>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
+    run_pair<VBC_PAIR_NRS, FASTE, NB, KC, MASK, DOT>(b, rg, lane, x, y, alpha, beta, rd_i != 0, lds, lds_out);
 }
 
 // Lane-pair streams (SlotBin::lanes with pair: fp64, 3-wide stripes, rows in runs of 3 -- FE-3D): the

@@ -100,7 +100,7 @@ static int launch_t(const SlotBin &hb, const SlotBin *d_b, bool faste, bool stag
     }
 }
 
-template <bool KC>
+template <bool KC, bool DOT>
 static int launch_pair(const SlotBin &hb, const SlotBin *d_b, bool faste, bool staged, const void *x, void *y,
                        double alpha, double beta, bool rd, hipStream_t s)
 {
@@ -108,17 +108,17 @@ static int launch_pair(const SlotBin &hb, const SlotBin *d_b, bool faste, bool s
     const double *xs = static_cast<const double *>(x);
     double *ys = static_cast<double *>(y);
     if (hb.mask)
-        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC, true>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
+        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC, true, DOT>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
                            alpha, beta, (int)rd);
     else if (faste && staged)
-        hipLaunchKernelGGL((spmv_planar_pair<true, 8, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys, alpha,
-                           beta, (int)rd);
+        hipLaunchKernelGGL((spmv_planar_pair<true, 8, KC, false, DOT>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
+                           alpha, beta, (int)rd);
     else if (faste)
-        hipLaunchKernelGGL((spmv_planar_pair<true, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys, alpha,
-                           beta, (int)rd);
+        hipLaunchKernelGGL((spmv_planar_pair<true, 0, KC, false, DOT>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys,
+                           alpha, beta, (int)rd);
     else
-        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs, ys, alpha,
-                           beta, (int)rd);
+        hipLaunchKernelGGL((spmv_planar_pair<false, 0, KC, false, DOT>), dim3(grid), dim3(kBlockThreads), 0, s, hb, xs,
+                           ys, alpha, beta, (int)rd);
     return (int)hipGetLastError();
 }
 
@@ -247,8 +247,11 @@ int launch_planar(int esz, const SlotBin &hb, const SlotBin *d_b, bool faste, bo
     }
     if (hb.pair) {  // fp64, w = 3, runs of 3: lane pairs (vbc_planar.h run_pair)
         if (esz != 8 || hb.wkey != 3 || hb.run != 3) return (int)hipErrorInvalidValue;
-        return hb.kc ? launch_pair<true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
-                     : launch_pair<false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+        if (hb.dot)  // the forward product of 3 x 3 node blocks (SlotBin::dot)
+            return hb.kc ? launch_pair<true, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
+                         : launch_pair<false, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
+        return hb.kc ? launch_pair<true, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)
+                     : launch_pair<false, false>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s);
     }
     if (esz == 8)
         return hb.kc ? launch_t<double, true>(hb, d_b, faste, staged, x, y, alpha, beta, rd, s)

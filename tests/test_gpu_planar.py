@@ -1005,3 +1005,44 @@ def test_ldoor_min_blocks_and_min_memory_partitions():
         y = torch.zeros(B.n, dtype=torch.float64, device=DEV)
         V.mul_(y, B.T, dev(x))
         assert rel(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(B.n), trans=True)) <= TOL64, name
+
+
+@pytest.mark.parametrize("keys16", ["0", "2"])
+@pytest.mark.parametrize("mask", ["0", "1"])
+def test_forward_lane_pairs_bitwise(monkeypatch, keys16, mask):
+    """Forward lane pairs (round 6, vbc_planar.h run_pair DOT, vbc_info planar_mask bit 11): fp64 3 x 3 node
+    blocks (an ldoor-like operator, ~15 blocks per node) laid out as the B'x lane pairs of the transposed
+    blocks, each output row adding its per-block dot product (the reference's forward order,
+    multiply_1DVBC.jl:34, :62-71).  Random x: bit for bit against the oracle and against the forward row-run
+    layout (VBC_PLANAR_PAIR=0); alpha / beta; both key forms; natural and masked chunk order; a node with no
+    block (empty output rows: beta * y)."""
+    monkeypatch.setenv("VBC_PLANAR_SPLIT", "0")
+    monkeypatch.setenv("VBC_SLOT_KEYS16", keys16)
+    monkeypatch.setenv("VBC_PLANAR_MASK", mask)
+    A = V.synthetic.fe_stiffness_3d(90000, 4_000_000, 3, np.float64).tocsc()
+    A = A.tolil()
+    A[30:33, :] = 0.0  # node 10 couples to nothing: empty output rows
+    A = A.tocsc()
+    A.eliminate_zeros()
+    B = V.SparseMatrix1DVBC[8](A.T.tocsc(), V.StrictChunker(8))  # bin/test_table.jl:27
+    R = ref_of(B)
+    rng = np.random.default_rng(31)
+    outs = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("VBC_PLANAR_PAIR", pair)
+        B.release()
+        inf = B.info(trans=False)
+        assert bool(inf["planar_mask"] & 2048) == (pair == "1") and inf["fwd_run"] == 3, inf["planar_mask"]
+        x = rng.uniform(-1, 1, B.n)
+        y = torch.full((B.m,), float("nan"), dtype=torch.float64, device=DEV)
+        V.mul_(y, B, dev(x))
+        ref = O.mul(R, x, np.zeros(B.m))
+        assert np.array_equal(y.cpu().numpy(), ref), pair
+        outs[pair] = y.cpu().numpy()
+        y0 = rng.uniform(-1, 1, B.m)
+        yb = dev(y0.copy())
+        V.mul_(yb, B, dev(x), 0.5, -1.5)
+        assert rel(yb.cpu().numpy(), O.mul(R, x, y0.copy(), 0.5, -1.5, ref_semantics=False)) <= 1e-14
+        outs[pair + "ab"] = yb.cpu().numpy()
+        rng = np.random.default_rng(31)  # the same x / y0 for the other layout
+    assert np.array_equal(outs["1"], outs["0"]) and np.array_equal(outs["1ab"], outs["0ab"])
