@@ -227,8 +227,9 @@ typedef struct vbc_sharded vbc_sharded; /* opaque */
  * VBC_CREATE_TRANSPOSED or no direction flag is given, B x when VBC_CREATE_FORWARD): per product the slowest
  * shard's kernel (3.1 us + its bytes at 5.7 TB/s, both measured on one MI355X) plus the exchange through
  * devices[0] (x broadcast + y slices gathered, or x slices + ncclReduce of y) at an ASSUMED ring-collective
- * rate of 7 xGMI links x 76.8 GB/s x 0.6 with 2 us per ring step.  vbc_sharded_split reports
- * the choice. */
+ * rate of 7 xGMI links x 76.8 GB/s x 0.6 with 2 us per ring step; costs within 2 % tie, and a
+ * tie goes to the split with disjoint outputs for the one direction built (stripes when both are built).
+ * vbc_sharded_split reports the choice. */
 #define VBC_SPLIT_AUTO 2
 
 /* Same matrix arguments as vbc1d_create_ex (types: Tv, Ti, compute eltype); `flags` as vbc1d_create

@@ -434,12 +434,18 @@ double predict_us(const Fields &f, int csz, int N, int split, int trans)
     const bool disj = disjoint_output(split, trans);
     const double kern = kModelT0Us + (mat + (disj ? nx : nx / N) + (disj ? ny / N : ny)) / (kModelStreamGBs * 1e3);
     if (N <= 1) return kern;
+    // a ring broadcast / reduce moves the whole vector through every hop (pipelined); the root's direct sends
+    // and receives of slices move (N-1)/N of it
     const double part = (double)(N - 1) / N, lat = (N - 1) * kModelStepUs, bw = kModelCollGBs * 1e3;
-    const double coll = disj ? (nx / bw + lat) + (part * ny / bw + lat)     // broadcast x, gather y
-                             : (part * nx / bw + lat) + (part * ny / bw + lat);  // scatter x, reduce y
+    const double coll = disj ? (nx / bw + lat) + (part * ny / bw + lat)  // broadcast x, gather y slices
+                             : (part * nx / bw + lat) + (ny / bw + lat);  // scatter x slices, reduce y
     return kern + coll;
 }
 
+// Within 2 % the costs tie (a square operator: the two splits mirror each other); a tie goes to the split
+// whose outputs are disjoint for the one direction built (bit-identical to the single-GPU product, no
+// reduction), and to the stripe split when both are (the reference's own parallel direction,
+// multiply_1DVBC.jl:169-177).
 int auto_split(const Fields &f, int csz, int N, unsigned flags)
 {
     const bool t = (flags & VBC_CREATE_TRANSPOSED) || !(flags & VBC_CREATE_FORWARD);
@@ -449,7 +455,9 @@ int auto_split(const Fields &f, int csz, int N, unsigned flags)
         if (t) cost[sp] += predict_us(f, csz, N, sp, 1);
         if (fw) cost[sp] += predict_us(f, csz, N, sp, 0);
     }
-    return cost[VBC_SPLIT_ROWS] < cost[VBC_SPLIT_STRIPES] * (1 - 1e-9) ? VBC_SPLIT_ROWS : VBC_SPLIT_STRIPES;
+    if (cost[VBC_SPLIT_ROWS] < 0.98 * cost[VBC_SPLIT_STRIPES]) return VBC_SPLIT_ROWS;
+    if (cost[VBC_SPLIT_STRIPES] < 0.98 * cost[VBC_SPLIT_ROWS]) return VBC_SPLIT_STRIPES;
+    return (fw && !t) ? VBC_SPLIT_ROWS : VBC_SPLIT_STRIPES;
 }
 
 int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *types, int ngpus, const int *devices,
