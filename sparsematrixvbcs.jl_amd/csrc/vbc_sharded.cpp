@@ -413,6 +413,28 @@ int create_shard(const Fields &f, vbc_handle **out, int64_t m, int64_t n, int64_
     return vbc1d_create_ex(out, m, n, f.W, L, spl, pos, idx, ofs, nv > 0 ? val : nullptr, nv, t64, device, flags);
 }
 
+// The largest R in {3, 2} such that R divides m and every stripe's stored rows come in aligned runs of R
+// consecutive rows (a node's dof rows); 1 otherwise (distributed.py row_runs).  Row cuts at multiples of R
+// keep every row shard node-blocked (its forward lane pairs / row runs need m_local % 3 == 0).
+int64_t row_runs(const Fields &f)
+{
+    const int64_t L = f.L;
+    for (int64_t R = 3; R >= 2; R--) {
+        if (f.m % R) continue;
+        bool ok = true;
+        for (int64_t l = 0; l < L && ok; l++) {
+            const int64_t a = f.P[l] - 1, b = f.P[l + 1] - 1;
+            if ((b - a) % R) { ok = false; break; }
+            for (int64_t r = a; r < b && ok; r++) {
+                const int64_t k = (r - a) % R, row = f.I[r] - 1;
+                ok = row % R == k && (k == 0 || row == f.I[r - 1]);
+            }
+        }
+        if (ok) return R;
+    }
+    return 1;
+}
+
 // VBC_SPLIT_AUTO (vbc.h): the split with the smaller predicted time of the products `flags` builds (B'x for
 // VBC_CREATE_TRANSPOSED or no direction flag, B x for VBC_CREATE_FORWARD).  The model is distributed.py's
 // predict_product_us for this one-process handle's exchange: the slowest shard's kernel -- a
@@ -527,7 +549,12 @@ int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *
             for (int64_t r = P[l] - 1; r < P[l + 1] - 1; r++)
                 per[I[r]] += (double)(f.u(I[r] - 1) * (S[l + 1] - S[l]) * csz + 4);  // I is 1-based: prefix index
         for (int64_t k = 0; k < K; k++) per[k + 1] += per[k];
-        const std::vector<int64_t> kc = balanced_cuts(per, ngpus);  // block-row ranges
+        std::vector<int64_t> kc = balanced_cuts(per, ngpus);  // block-row ranges
+        if (!f.is2d) {  // a 1DVBC's node runs stay whole (distributed.py row_split / row_runs)
+            const int64_t a = row_runs(f);
+            if (a > 1)
+                for (int g = 1; g < ngpus; g++) kc[g] = std::max(kc[g - 1], std::min(K, (kc[g] + a / 2) / a * a));
+        }
         s->cut.resize(ngpus + 1);
         for (int g = 0; g <= ngpus; g++) s->cut[g] = f.is2d ? f.PS[kc[g]] - 1 : kc[g];  // row ranges
         for (int g = 0; g < ngpus; g++) {

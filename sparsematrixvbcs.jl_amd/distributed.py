@@ -57,13 +57,37 @@ def _row_widths(B):
     return np.repeat(w, np.diff(B.pos))
 
 
-def row_split(B, parts):
-    """Row boundaries r_0 = 0 < ... < r_parts = m (0-based) balancing the stored bytes per part."""
+def row_runs(B):
+    """The largest R in {3, 2} such that R divides m and every stripe's stored rows come in aligned runs of
+    R consecutive rows (a node's dof rows in a stiffness operator); 1 otherwise."""
+    idx = B.idx.astype(np.int64) - 1
+    cnt = np.diff(B.pos).astype(np.int64)
+    for R in (3, 2):
+        if B.m % R or np.any(cnt % R):
+            continue
+        if len(idx) == 0:
+            return R
+        ph = (np.arange(len(idx), dtype=np.int64) - np.repeat(B.pos[:-1].astype(np.int64) - 1, cnt)) % R
+        if not np.all(idx % R == ph):  # the k-th stored row of a run sits at row k of its aligned group
+            continue
+        cont = (ph[:-1] == R - 1) | (idx[1:] == idx[:-1] + 1)  # inside a run the rows are consecutive
+        if np.all(cont):
+            return R
+    return 1
+
+
+def row_split(B, parts, align=None):
+    """Row boundaries r_0 = 0 < ... < r_parts = m (0-based) balancing the stored bytes per part, each a
+    multiple of `align` (default row_runs(B): a cut never splits a node's rows, so every row shard keeps
+    the node-blocked layouts -- the forward lane pairs / row runs need m_local % 3 == 0)."""
     esz = B.val.dtype.itemsize
     per_row = np.bincount(B.idx - 1, weights=_row_widths(B) * esz + 4, minlength=B.m)
     cost = np.concatenate([[0.0], np.cumsum(per_row)])
     targets = cost[-1] * np.arange(1, parts) / parts
     cuts = np.clip(np.searchsorted(cost, targets, side="left"), 0, B.m)
+    a = row_runs(B) if align is None else int(align)
+    if a > 1:
+        cuts = np.clip((cuts + a // 2) // a * a, 0, B.m)
     return np.concatenate([[0], np.maximum.accumulate(cuts), [B.m]]).astype(np.int64)
 
 

@@ -61,7 +61,7 @@ def cpu_time(R, x, n, reps=5, trsp=None, B=None):
     """CPU time of the same product: the reference's SIMD kernel (oracle/vbc_simd.c) for 1DVBC B'x on
     all host threads with the reference's one-stripe grabs (multiply_1DVBC.jl:169-177) and on 1 core,
     its serial TrSpMV! for the CSC row; the scalar oracle for 2D VBC (no SIMD port).  Returns
-    (seconds all threads, threads, seconds 1 core, kind)."""
+    (seconds all threads, threads, seconds 1 core, kind, seconds all threads with 64-stripe grabs or None)."""
     from oracle import oracle as O
     from oracle import simd as S
     th = S.host_threads()
@@ -79,12 +79,14 @@ def cpu_time(R, x, n, reps=5, trsp=None, B=None):
         cp = np.add(trsp.indptr, 1, dtype=np.int64)
         rv = np.add(trsp.indices, 1, dtype=np.int64)
         t1 = med(lambda: S.trspmv(cp, rv, trsp.data, trsp.shape[0], trsp.shape[1], x, y))
-        return t1, 1, t1, "simd (serial, TrSpMV.jl)"
+        return t1, 1, t1, "simd (serial, TrSpMV.jl)", None
     if B is not None and not hasattr(B, "Pi"):
+        # the reference's schedule (one stripe per atomic grab) and the same kernel with 64-stripe grabs (the
+        # atomic counter is contended by the one-stripe grabs of these small matrices)
         return (med(lambda: S.mul_t(B, x, y, th, 1)), th, med(lambda: S.mul_t(B, x, y, 1, 1)),
-                "simd (multiply_1DVBC.jl:90-180)")
+                "simd (multiply_1DVBC.jl:90-180)", med(lambda: S.mul_t(B, x, y, th, 64)))
     t = med(lambda: O.mul(R, x, y, trans=True, nthreads=th))
-    return t, th, med(lambda: O.mul(R, x, y, trans=True, nthreads=1)), "scalar oracle"
+    return t, th, med(lambda: O.mul(R, x, y, trans=True, nthreads=1)), "scalar oracle", None
 
 
 def main():
@@ -124,10 +126,11 @@ def main():
     def record(name, setup, mem, B=None, R=None, trsp=None, model_us=None):
         t_gpu = gpu_time(B, x, y, args.reps)
         err = float(np.linalg.norm(y.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref))
-        t_cpu, th, t_cpu1, kind = cpu_time(R, xh, n, trsp=trsp, B=B)
+        t_cpu, th, t_cpu1, kind, t_cpu64 = cpu_time(R, xh, n, trsp=trsp, B=B)
         bytes_ = B.info()["bytes_t"] if hasattr(B, "info") else None
         row = dict(method=name, setup_s=round(setup, 4), memory=int(mem), gpu_us=round(t_gpu * 1e6, 2),
                    cpu_us=round(t_cpu * 1e6, 1), cpu_threads=th, cpu_1core_us=round(t_cpu1 * 1e6, 1), cpu_kind=kind,
+                   cpu_chunk64_us=round(t_cpu64 * 1e6, 1) if t_cpu64 is not None else None,
                    speedup=round(t_cpu / t_gpu, 1),
                    gpu_GBs=round(bytes_ / t_gpu / 1e9, 1) if bytes_ else None, rel_err=err, model_us=model_us)
         if hasattr(B, "Phi"):
