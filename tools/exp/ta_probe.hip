@@ -7,6 +7,10 @@
 //   5 dwordx4, 4 groups of 12 lanes (192 B each) at random blocks, 16 lanes idle
 //   6 dword, every lane the same address in its group of 16 (broadcast), 4 groups
 //   7 dwordx3 broadcast (16 lanes same 12 B), 4 groups
+//   8 dwordx4, 16 groups of 4 lanes (64 B each) at random lines (all 64 lanes: a planar tile row's X rows)
+//   9 dwordx3, 48 lanes, 576 B contiguous (16 tiles' 3 x 3 values, lanes q < 3 of each group of 4)
+//  10 dword, 16 groups of 4 lanes reading the same 4 B, 64 B contiguous (16 keys, each read by 4 lanes)
+//  11 dwordx4, 64 lanes contiguous 1 KB STORE (16 stripes' outputs)
 // Prints ns per load instruction per CU (all waves of the chip together).
 #include <hip/hip_runtime.h>
 
@@ -56,9 +60,24 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ t, uint32
                 }
             } else if constexpr (SHAPE == 6) {
                 acc += t[(size_t)(h & (nlines - 1)) * 16];
-            } else {
+            } else if constexpr (SHAPE == 7) {
                 const f3 v = *(const f3 *)(t + (size_t)(h & (nlines - 1)) * 16);
                 acc += v.x + v.z;
+            } else if constexpr (SHAPE == 8) {
+                const uint32_t h16 = hash(wid * 7919u + (lane >> 2) * 31u) + (uint32_t)(it + u) * 40503u;
+                const f4 v = *(const f4 *)(t + (size_t)(h16 & (nlines - 1)) * 16 + (lane & 3) * 4);
+                acc += v.x + v.w;
+            } else if constexpr (SHAPE == 9) {
+                if ((lane & 3) < 3) {
+                    const f3 v = *(const f3 *)(t + (size_t)(((base0 + (uint32_t)(it + u) * 40503u) & (nlines / 16 - 1))) * 256 +
+                                               (lane >> 2) * 9 + (lane & 3) * 3);
+                    acc += v.x + v.z;
+                }
+            } else if constexpr (SHAPE == 10) {
+                acc += t[(size_t)(((base0 + (uint32_t)(it + u) * 40503u) & (nlines - 1))) * 16 + (lane >> 2)];
+            } else {
+                f4 *o = (f4 *)(out + 64 + (size_t)(((base0 + (uint32_t)(it + u) * 40503u) & (1023u))) * 256) + lane;
+                *o = f4{acc, acc, acc, acc};
             }
         }
     }
@@ -86,7 +105,7 @@ int main()
     const size_t bytes = 4 << 20;  // L2-resident
     float *t, *out;
     CHECK(hipMalloc(&t, bytes + 4096));
-    CHECK(hipMalloc(&out, 64));
+    CHECK(hipMalloc(&out, 64 * 4 + 1024 * 1024 + 4096));
     CHECK(hipMemset(t, 0, bytes + 4096));
     const uint32_t nlines = bytes / 64;
     int cus = 256;
@@ -94,8 +113,9 @@ int main()
     const int iters = 512;
     const char *names[] = {"dword contiguous 256 B", "dword 4 x 64 B random", "dwordx4 contiguous 1 KB",
                            "dwordx4 4 x 64 B (16 lanes)", "dwordx3 4 x 192 B", "dwordx4 4 x 192 B (48 lanes)",
-                           "dword broadcast x4 groups", "dwordx3 broadcast x4 groups"};
-    float ms[8];
+                           "dword broadcast x4 groups", "dwordx3 broadcast x4 groups", "dwordx4 16 x 64 B random",
+                           "dwordx3 48 lanes 576 B contiguous", "dword 16 x 4 B, 4 lanes each", "dwordx4 store 1 KB"};
+    float ms[12];
     ms[0] = run<0>(t, nlines, iters, out, grid);
     ms[1] = run<1>(t, nlines, iters, out, grid);
     ms[2] = run<2>(t, nlines, iters, out, grid);
@@ -104,8 +124,12 @@ int main()
     ms[5] = run<5>(t, nlines, iters, out, grid);
     ms[6] = run<6>(t, nlines, iters, out, grid);
     ms[7] = run<7>(t, nlines, iters, out, grid);
+    ms[8] = run<8>(t, nlines, iters, out, grid);
+    ms[9] = run<9>(t, nlines, iters, out, grid);
+    ms[10] = run<10>(t, nlines, iters, out, grid);
+    ms[11] = run<11>(t, nlines, iters, out, grid);
     const double per_cu = (double)grid * 4 * iters / cus;  // wave-instructions per CU
-    for (int s = 0; s < 8; s++)
+    for (int s = 0; s < 12; s++)
         printf("shape %d %-32s %8.3f ms  %6.2f cycles/instr/CU at 2.4 GHz\n", s, names[s], ms[s],
                ms[s] * 1e-3 * 2.4e9 / per_cu);
     return 0;
