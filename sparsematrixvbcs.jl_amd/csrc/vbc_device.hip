@@ -2173,13 +2173,16 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
         slot_total += 4 * len;
         if (slot_total >= (int64_t(1) << 31) / std::max(1, TV)) return false;
     }
-    const int64_t kpad = 3 * nbt + 16, vpad = (int64_t)(2 * nbt + 2) * TV + 64;
+    // over-read padding past the last stream: keys 3 D batches ahead, values 2 D (vbc_tiles.h)
+    const int dep = h->tile_depth;
+    const int64_t kpad = 3 * dep * nbt + 16, vpad = (int64_t)(2 * dep * nbt + 2) * TV + 64;
     pp = PendingPanel{};
     pp.tile = true;
     TileBin &tb = pp.tb;
     tb.w = w;
     tb.ub = ub;
     tb.nbt = nbt;
+    tb.depth = dep;
     if (const char *e = ablation_knob("VBC_TILE_DIAG")) tb.diag = atoi(e);
     {
         int64_t most = 1;
@@ -2881,6 +2884,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = layout_knob("VBC_PANEL_TILES")) h->panel_tiles = atoi(e) < 0 ? -1 : atoi(e) != 0;
         if (const char *e = tuning_knob("VBC_TILE_NBT")) h->tile_nbt = atoi(e) >= 8 ? 8 : 4;
         if (const char *e = tuning_knob("VBC_TILE_SPR")) h->tile_spr = std::max(1, atoi(e));
+        if (const char *e = tuning_knob("VBC_TILE_DEPTH")) h->tile_depth = atoi(e) == 3 ? 3 : 2;
         h->occ_tiles = occupancy_tiles(h->esz);
     }
 

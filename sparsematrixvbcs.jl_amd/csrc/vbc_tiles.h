@@ -51,6 +51,7 @@ struct TileBin {
     int32_t out_base;
     int32_t out_stride;
     int32_t nbt;          // tiles per stream per pipeline stage (the kernel's NBT; streams padded to 2 NBT)
+    int32_t depth;        // register sets of the kernel's pipeline (its D: 2, or 3 in the VBC_ABLATION build)
     int32_t stage_bytes;  // LDS output stage per wave: the most stripes of a range x w x 16 sums (dynamic LDS)
     int32_t diag;         // VBC_TILE_DIAG ablation (the VBC_ABLATION build only; 0 in the product library): 8 no output
                           // stores
@@ -139,7 +140,12 @@ __device__ __forceinline__ void fmac_bcast_rt(T &acc, T v, T x, int n)
 // BUF: X addressed by 32-bit buffer offsets (X below 2 GiB; an invalid key reads past the buffer: 0);
 // else 64-bit addresses with the value selected to 0.  FAST: the range's outputs are one contiguous run of
 // Y (affine stripe map with stride w, Y row-major with 16 contiguous right-hand sides): 16-B stores.
-template <typename T, int UB, int W, int NBT, bool MASKU, bool BUF>
+// D (round 6): register sets of the software pipeline.  D = 2 ping-pong (keys a pair of batches ahead, one
+// load per two batches); D >= 3 a ring of D sets -- batch b's values and X gathers are issued D - 1 folds
+// before batch b is folded, the next D batches' keys one whole ring ahead -- so a wave keeps D - 1 batches
+// of gathers in flight instead of one (the kernel is bound by the memory latency per wave);
+// streams are then padded to whole batches and a fold past a stream's end is skipped (uniform test).
+template <typename T, int UB, int W, int NBT, bool MASKU, bool BUF, int D = 2>
 __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, const T *__restrict__ X, int64_t sxr,
                                                             int64_t sxc, uint32_t xbytes, T *__restrict__ Y, int64_t syr,
                                                             int64_t syc, int nrhs, T alpha, T beta, int rd_i, int fast)
@@ -174,7 +180,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
     for (int c = 0; c < W; c++) acc[c] = zero;
 
     // lane j of the row holds the key of step t0 + j, j < 2 NBT (the bin carries padding past its end)
-    static_assert(2 * NBT <= 16, "one key load covers two batches of a 16-lane row");
+    static_assert(2 * NBT <= 16 && D >= 2, "one key load covers two batches of a 16-lane row");
     auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < 2 * NBT ? j : 2 * NBT - 1)]; };
     auto load_vals = [&](int t0, tv (&V)[NV]) {
         const gptr<const T> p = val + (kb + t0) * TV + j * EPL;
@@ -239,31 +245,73 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
         }
     };
 
-    // Two register sets in ping-pong (copying a set would wait for its loads): while batch b is folded
-    // from one set, batch b + 1's values and X gathers fill the other.  One key load covers two batches
-    // (lane j of the row: step t0 + j), issued a pair ahead; the pair's register is copied only once its
-    // keys have been consumed by the X gathers.
-    uint32_t KA = load_keys(0);
-    tv V0[NV], V1[NV];
-    T X0[NBT][UB], X1[NBT][UB];
-    load_vals(0, V0);
-    load_x(KA, 0, X0);
-    // (sched_barrier: the fold's DPP reads of a set must not be hoisted above the other set's loads,
-    // which would make those loads wait for this set's data)
-    for (int t0 = 0; t0 < len; t0 += 2 * NBT) {
-        const uint32_t KB = load_keys(t0 + 2 * NBT);
-        load_vals(t0 + NBT, V1);
-        load_x(KA, NBT, X1);
-        const uint64_t lastm = __builtin_amdgcn_ballot_w64((KA & kTileLast) != 0);
-        __builtin_amdgcn_sched_barrier(0);
-        fold(t0, KA, lastm, 0, V0, X0);
-        __builtin_amdgcn_sched_barrier(0);
-        load_vals(t0 + 2 * NBT, V0);
-        load_x(KB, 0, X0);
-        __builtin_amdgcn_sched_barrier(0);
-        fold(t0 + NBT, KA, lastm, NBT, V1, X1);
-        __builtin_amdgcn_sched_barrier(0);
-        KA = KB;
+    if constexpr (D == 2) {
+        // Two register sets in ping-pong (copying a set would wait for its loads): while batch b is folded
+        // from one set, batch b + 1's values and X gathers fill the other.  One key load covers two batches
+        // (lane j of the row: step t0 + j), issued a pair ahead; the pair's register is copied only once its
+        // keys have been consumed by the X gathers.
+        uint32_t KA = load_keys(0);
+        tv V0[NV], V1[NV];
+        T X0[NBT][UB], X1[NBT][UB];
+        load_vals(0, V0);
+        load_x(KA, 0, X0);
+        // (sched_barrier: the fold's DPP reads of a set must not be hoisted above the other set's loads,
+        // which would make those loads wait for this set's data)
+        for (int t0 = 0; t0 < len; t0 += 2 * NBT) {
+            const uint32_t KB = load_keys(t0 + 2 * NBT);
+            load_vals(t0 + NBT, V1);
+            load_x(KA, NBT, X1);
+            const uint64_t lastm = __builtin_amdgcn_ballot_w64((KA & kTileLast) != 0);
+            __builtin_amdgcn_sched_barrier(0);
+            fold(t0, KA, lastm, 0, V0, X0);
+            __builtin_amdgcn_sched_barrier(0);
+            load_vals(t0 + 2 * NBT, V0);
+            load_x(KB, 0, X0);
+            __builtin_amdgcn_sched_barrier(0);
+            fold(t0 + NBT, KA, lastm, NBT, V1, X1);
+            __builtin_amdgcn_sched_barrier(0);
+            KA = KB;
+        }
+    } else {
+        // A ring of D sets.  At step d of an iteration (batch t0 + d NBT folded from set d), the set freed by the
+        // previous fold takes batch t0 + (d + D - 1) NBT, whose key is K[D - 1] for d = 0 and KN[d - 1] after.
+        // Keys run a ring further ahead (KNN, issued when the iteration begins, consumed by the next one's
+        // gathers), so no gather waits for a key load issued less than D folds earlier.  Lane j of a row holds
+        // the key of step j of its batch (j < NBT).  Loads are unconditional (a load inside a branch would make
+        // the compiler wait for every load in flight); a fold past the stream's end is skipped.
+        auto load_keys1 = [&](int t0) -> uint32_t { return key[kb + t0 + (j < NBT ? j : NBT - 1)]; };
+        uint32_t K[D], KN[D], KNN[D];
+        tv V[D][NV];
+        T Xs[D][NBT][UB];
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            K[d] = load_keys1(d * NBT);
+            KN[d] = load_keys1((D + d) * NBT);
+        }
+#pragma unroll
+        for (int d = 0; d < D - 1; d++) {
+            load_vals(d * NBT, V[d]);
+            load_x(K[d], 0, Xs[d]);
+        }
+        for (int t0 = 0; t0 < len; t0 += D * NBT) {
+#pragma unroll
+            for (int d = 0; d < D; d++) KNN[d] = load_keys1(t0 + (2 * D + d) * NBT);
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const int e = (d + D - 1) % D;
+                load_vals(t0 + (d + D - 1) * NBT, V[e]);
+                load_x(d == 0 ? K[D - 1] : KN[d - 1], 0, Xs[e]);
+                const uint64_t lastm = __builtin_amdgcn_ballot_w64((K[d] & kTileLast) != 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t0 + d * NBT < len) fold(t0 + d * NBT, K[d], lastm, 0, V[d], Xs[d]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                K[d] = KN[d];
+                KN[d] = KNN[d];
+            }
+        }
     }
     // the range's outputs (stripes s0 .. s0 + ns - 1, every slot written once) from the LDS stage
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -9,13 +9,13 @@
 
 namespace vbc {
 
-template <typename T, int UB, int W, int NBT>
+template <typename T, int UB, int W, int NBT, int D>
 static void launch_tiles_uwn(const TileBin &tb, int grid, hipStream_t s, const T *xs, int64_t sxr, int64_t sxc,
                              uint32_t xb, bool buf, T *ys, int64_t syr, int64_t syc, int nr, T alpha, T beta, int rd,
                              int fast)
 {
 #define VBC_TILES(MASKU, BUF)                                                                                      \
-    hipLaunchKernelGGL((spmm_tiles<T, UB, W, NBT, MASKU, BUF>), dim3(grid), dim3(kBlockThreads),                 \
+    hipLaunchKernelGGL((spmm_tiles<T, UB, W, NBT, MASKU, BUF, D>), dim3(grid), dim3(kBlockThreads),                 \
                        (size_t)tb.stage_bytes * kWavesPerBlock, s, tb, xs, sxr,                                  \
                        sxc, xb, ys, syr, syc, nr, alpha, beta, rd, fast)
     if (tb.masku) {
@@ -33,8 +33,15 @@ static void launch_tiles_uw(const TileBin &tb, int grid, hipStream_t s, const T 
                             uint32_t xb, bool buf, T *ys, int64_t syr, int64_t syc, int nr, T alpha, T beta, int rd,
                             int fast)
 {
-    if (tb.nbt == 8) launch_tiles_uwn<T, UB, W, 8>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, alpha, beta, rd, fast);
-    else launch_tiles_uwn<T, UB, W, 4>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, alpha, beta, rd, fast);
+#ifdef VBC_ABLATION
+    if (tb.depth == 3) {
+        if (tb.nbt == 8) launch_tiles_uwn<T, UB, W, 8, 3>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, alpha, beta, rd, fast);
+        else launch_tiles_uwn<T, UB, W, 4, 3>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, alpha, beta, rd, fast);
+        return;
+    }
+#endif
+    if (tb.nbt == 8) launch_tiles_uwn<T, UB, W, 8, 2>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, alpha, beta, rd, fast);
+    else launch_tiles_uwn<T, UB, W, 4, 2>(tb, grid, s, xs, sxr, sxc, xb, buf, ys, syr, syc, nr, alpha, beta, rd, fast);
 }
 
 template <typename T, int UB>

@@ -34,6 +34,8 @@ FORMER = {  # variable -> the values it used to accept (round 5's libvbc.so)
     "VBC_TARGET_RANGES": ["1", "7"],
     "VBC_TILE_SPR": ["1"],
     "VBC_TILE_K": ["4"],
+    "VBC_TILE_NBT": ["4"],
+    "VBC_TILE_DEPTH": ["3"],
     "VBC_PIPE": ["3"],
     "VBC_PAD": ["3:4"],
 }

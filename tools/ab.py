@@ -35,7 +35,13 @@ def main():
                          "does: per-launch event brackets inflate small kernels")
     ap.add_argument("--copies", type=int, default=1,
                     help="build every variant this many times (A B .. A B ..): placement effects show as spread")
+    ap.add_argument("--fresh", action="store_true",
+                    help="run every variant as its own bench.py process (fresh allocation and placement), "
+                         "--rounds rounds interleaved A B .. A B ..: the bench's own harness, required for a "
+                         "default change under 3 %% (VERDICT r5)")
     args = ap.parse_args()
+    if args.fresh:
+        return fresh(args)
     import torch
 
     import bench
@@ -163,5 +169,47 @@ def main():
         libs[i].vbc_destroy(hp)
 
 
+def fresh(args):
+    """Each variant in a fresh `python bench.py --workload W` process (its env knobs set, "@lib=path" ->
+    VBC_LIBRARY), rounds interleaved; reports the median and spread of the line's avg_launch_ms (events
+    around the graph-replayed products) and ms_per_step (wall), and the line's parity."""
+    import json
+    import subprocess
+    wl = args.workload + ("" if args.trans else "-fwd")
+    variants = [v for v in args.variants.split(";")]
+    res = {v: [] for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            env = dict(os.environ)
+            for kv in v.split(","):
+                kv = kv.strip()
+                if kv.startswith("@lib="):
+                    env["VBC_LIBRARY"] = str(Path(kv[5:]).resolve())
+                elif "=" in kv and not kv.startswith("@"):
+                    k, val = kv.split("=", 1)
+                    env[k.strip()] = val.strip()
+            cmd = [sys.executable, str(ROOT / "bench.py"), "--workload", wl, "--dtype", args.dtype, "--steps",
+                   str(args.reps), "--no-cpu-baseline", "--no-secondary", "--scale", str(args.scale)]
+            if args.nrhs:
+                cmd += ["--nrhs", str(args.nrhs)]
+            r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode or not line:
+                print(f"{v}: failed ({r.returncode}): {r.stderr[-800:]}", flush=True)
+                return 1
+            d = json.loads(line[-1])
+            res[v].append((d["roofline"]["avg_launch_ms"] * 1e3, d["ms_per_step"] * 1e3,
+                           (d.get("parity") or {}).get("rel_err")))
+            print(f"  {v:40s} {res[v][-1][0]:8.2f} us (events)  {res[v][-1][1]:8.2f} us (wall)  rel_err {res[v][-1][2]}",
+                  flush=True)
+    print("fresh-process A/B (bench.py per variant, rounds interleaved):")
+    for v in variants:
+        ev = np.array([t[0] for t in res[v]])
+        wall = np.array([t[1] for t in res[v]])
+        print(f"{v:40s} events median {np.median(ev):8.2f} us [{ev.min():.2f}, {ev.max():.2f}]  wall median "
+              f"{np.median(wall):8.2f} us", flush=True)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
