@@ -42,6 +42,15 @@ __device__ __forceinline__ gptr<T> G(T *p) { return (gptr<T>)p; }
 template <typename T>
 __device__ __forceinline__ gptr<const T> G(const T *p) { return (gptr<const T>)p; }
 
+// A 16-B (or narrower) piece of y: a plain store, or a non-temporal one when `nt` (SlotBin / TileBin diag
+// bit 16 -- the VBC_ABLATION build's A/B of streaming y stores; the product library passes false).
+template <typename V>
+__device__ __forceinline__ void st_y(gptr<V> p, V v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Fused multiply-add in T (__builtin_fma is the double version: on floats it would widen).
 __device__ __forceinline__ float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double fmadd(double a, double b, double c) { return __builtin_fma(a, b, c); }

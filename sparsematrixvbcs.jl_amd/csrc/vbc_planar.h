@@ -164,7 +164,7 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
             for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
                 if (off + 16 <= bytes) {
-                    *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                    st_y((gptr<u4>)(dst + off), *reinterpret_cast<const u4 *>(lds_wave + off), VBC_ABL(b.diag & 16) != 0);
                 } else {
                     for (int64_t q = off; q < bytes; q += sizeof(T))
                         *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);
@@ -449,7 +449,7 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
 #pragma unroll
                     for (int e = 0; e < VE; e++) q[e] = fmadd(beta, yo[e], q[e]);
                 }
-                *(gptr<vt>)(dst + i) = q;
+                st_y((gptr<vt>)(dst + i), q, VBC_ABL(b.diag & 16) != 0);
             } else {
                 for (int e = i; e < n; e++) {
                     T q = alpha * buf[e];
@@ -541,7 +541,7 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
         if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
             for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
-                if (off + 16 <= bytes) *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                if (off + 16 <= bytes) st_y((gptr<u4>)(dst + off), *reinterpret_cast<const u4 *>(lds_wave + off), VBC_ABL(b.diag & 16) != 0);
                 else
                     for (int64_t q = off; q < bytes; q += sizeof(T))
                         *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);
@@ -788,7 +788,7 @@ __device__ __forceinline__ void run_pair(const SlotBin &b, int r, int lane, cons
         if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
             for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
-                if (off + 16 <= bytes) *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                if (off + 16 <= bytes) st_y((gptr<u4>)(dst + off), *reinterpret_cast<const u4 *>(lds_wave + off), VBC_ABL(b.diag & 16) != 0);
                 else
                     for (int64_t q = off; q < bytes; q += 8)
                         *(gptr<double>)(dst + q) = *reinterpret_cast<const double *>(lds_wave + q);

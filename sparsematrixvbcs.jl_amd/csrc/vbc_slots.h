@@ -116,7 +116,7 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
             for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
                 if (off + 16 <= bytes) {
-                    *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                    st_y((gptr<u4>)(dst + off), *reinterpret_cast<const u4 *>(lds_wave + off), VBC_ABL(b.diag & 16) != 0);
                 } else {
                     for (int64_t q = off; q < bytes; q += sizeof(T))
                         *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);
@@ -314,7 +314,7 @@ __device__ __forceinline__ void run_slots_narrow(const SlotBin &b, int r, int la
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
             for (int64_t off = (int64_t)lane * 16; off < bytes; off += 1024) {
                 if (off + 16 <= bytes) {
-                    *(gptr<u4>)(dst + off) = *reinterpret_cast<const u4 *>(lds_wave + off);
+                    st_y((gptr<u4>)(dst + off), *reinterpret_cast<const u4 *>(lds_wave + off), VBC_ABL(b.diag & 16) != 0);
                 } else {
                     for (int64_t q = off; q < bytes; q += sizeof(T))
                         *(gptr<T>)(dst + q) = *reinterpret_cast<const T *>(lds_wave + q);

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
 #pragma unroll
                 for (int q = 0; q < EPL; q++) o[q] = fmadd(beta, yo0[q], o[q]);
             }
-            *(gptr<tv>)yo = o;
+            st_y((gptr<tv>)yo, o, VBC_ABL(b.diag & 16) != 0);
         }
     } else if (fast) {
         gptr<T> yb = G(Y) + ((int64_t)b.out_base + (int64_t)s0 * W) * 16;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
 #pragma unroll
                 for (int q = 0; q < EPL; q++) o[q] = fmadd(beta, yo[q], o[q]);
             }
-            *(gptr<tv>)(yb + e) = o;
+            st_y((gptr<tv>)(yb + e), o, VBC_ABL(b.diag & 16) != 0);
         }
     } else {
         for (int e = lane; e < total; e += 64) {
