@@ -24,7 +24,7 @@
 /* ABI version (major*10000 + minor*100 + patch), returned by vbc_version().  A binding checks the major
  * version at load time: 3.x changed vbc_info (VBC_INFO_SIZE bytes, written whole by vbc_get_info) and
  * added the I64 / I32 / BOOL eltypes, the sharded 2D handle and the *_ex sharded product. */
-#define VBC_VERSION 30100
+#define VBC_VERSION 30200
 #define VBC_INFO_SIZE 152
 
 #ifdef __cplusplus
@@ -205,7 +205,8 @@ VBC_API int vbc_mul_mat_ex(vbc_handle *h, int trans, int64_t nrhs, const void *X
  * (multiply_1DVBC.jl:169-177, multiply_VBC.jl:182-189), by a split of the matrix over GPUs: ranges
  * balanced by HBM bytes, one single-GPU handle per device (vbc1d_create_ex on each slice).
  *   VBC_SPLIT_STRIPES: GPU g owns stripes [l_g, l_g+1) (columns [c_g, c_g+1) of B; block rows of A
- *     when B stores Aᵀ, as bin/test_table.jl:27 does).  B'x: x broadcast, y slices gathered to the
+ *     when B stores Aᵀ, as bin/test_table.jl:27 does).  B'x: each GPU receives the span of x its stripes
+ *     read (vbc_sharded_xspan; a mesh operator's shard: its share plus a halo), y slices gathered to the
  *     root (disjoint; each stripe summed in stored row order, bit-identical to one GPU and to the
  *     reference, unless a shard's layout runs the split planar product -- vbc_info.planar_split > 1,
  *     small shards only -- which sums a chunk's rows in P slices; VBC_CREATE_SERIAL forbids it).
@@ -215,8 +216,8 @@ VBC_API int vbc_mul_mat_ex(vbc_handle *h, int trans, int64_t nrhs, const void *X
  *     kernels associate a block's w-term dot product differently (~1 ulp), and a small shard may run
  *     the split forward product (planar_mask bit 3), which VBC_CREATE_SERIAL forbids.
  *     Bx: x slices scattered, ncclReduce(sum) of y.
- *   VBC_SPLIT_ROWS: GPU g owns the stored rows [r_g, r_g+1) of every stripe.  Bx: x broadcast, y slices
- *     gathered (disjoint).  B'x: x slices, ncclReduce(sum) of y.
+ *   VBC_SPLIT_ROWS: GPU g owns the stored rows [r_g, r_g+1) of every stripe.  Bx: the span of x its
+ *     stripes read (vbc_sharded_xspan) to each GPU, y slices gathered (disjoint).  B'x: x slices, ncclReduce(sum) of y.
  * devices: all distinct (one RCCL communicator per device, ncclCommInitAll) or all the same device
  * (shards share it; no communicators -- oversubscription and single-GPU testing).
  * ------------------------------------------------------------------------------------------- */
@@ -226,8 +227,8 @@ typedef struct vbc_sharded vbc_sharded; /* opaque */
 /* VBC_SPLIT_AUTO: the split with the smaller predicted time of the products `flags` builds (B'x when
  * VBC_CREATE_TRANSPOSED or no direction flag is given, B x when VBC_CREATE_FORWARD): per product the slowest
  * shard's kernel (3.1 us + its bytes at 5.7 TB/s, both measured on one MI355X) plus the exchange through
- * devices[0] (x broadcast + y slices gathered, or x slices + ncclReduce of y) at an ASSUMED ring-collective
- * rate of 7 xGMI links x 76.8 GB/s x 0.6 with 2 us per ring step; costs within 2 % tie, and a
+ * devices[0] (x spans over the root's links + y slices gathered, or x slices + ncclReduce of y) at ASSUMED
+ * xGMI rates of 76.8 GB/s x 0.6 per link, 7 links, 2 us per ring step; costs within 2 % tie, and a
  * tie goes to the split with disjoint outputs for the one direction built (stripes when both are built).
  * vbc_sharded_split reports the choice. */
 #define VBC_SPLIT_AUTO 2
@@ -275,6 +276,11 @@ VBC_API int vbc_sharded_split(const vbc_sharded *s, int *split);
 /* Shard g: its single-GPU handle (owned by s), its 0-based range [lo, hi) of the split dimension
  * (columns for VBC_SPLIT_STRIPES, rows for VBC_SPLIT_ROWS) and its device. */
 VBC_API int vbc_sharded_shard(const vbc_sharded *s, int g, vbc_handle **h, int64_t *lo, int64_t *hi, int *device);
+/* Shard g's x span: the 0-based range [lo, hi) of x that its disjoint-output product reads (the rows its
+ * stripes store for VBC_SPLIT_STRIPES' B'x, the columns of the stripes with a stored row in its range for
+ * VBC_SPLIT_ROWS' B x; [0, 0) when it reads none).  devices[0] sends each shard that span instead of
+ * broadcasting x; a caller that distributes x itself needs no more on shard g's device. */
+VBC_API int vbc_sharded_xspan(const vbc_sharded *s, int g, int64_t *lo, int64_t *hi);
 
 /* ---------------------------------------------------------------------------------------------
  * Introspection (for the Julia shim's size(), and for roofline accounting in bench.py)

@@ -30,7 +30,7 @@ ABI_SYMBOLS = (
     "vbc1d_create_ex", "vbc2d_create_ex", "vbc_csc_create_ex", "vbc_mul_ex", "vbc_mul_mat_ex",
     "vbc_get_info", "vbc_last_error", "vbc_version",
     "vbc1d_create_sharded", "vbc2d_create_sharded", "vbc_sharded_mul", "vbc_sharded_mul_ex", "vbc_sharded_destroy",
-    "vbc_sharded_count", "vbc_sharded_shard", "vbc_sharded_split",
+    "vbc_sharded_count", "vbc_sharded_shard", "vbc_sharded_split", "vbc_sharded_xspan",
     "vbcx_partition_equi", "vbcx_partition_strict", "vbcx_partition_overlap",
     "vbcx_partition_dynamic", "vbcx_partition_dynamic_table", "vbcx_partition_block", "vbcx_1dvbc_count", "vbcx_1dvbc_fill", "vbcx_vbc_count",
     "vbcx_vbc_fill", "vbcx_transpose_pattern",
@@ -116,6 +116,7 @@ def lib():
         L.vbc_sharded_count.argtypes = [P, C.POINTER(INT)]
         L.vbc_sharded_split.argtypes = [P, C.POINTER(INT)]
         L.vbc_sharded_shard.argtypes = [P, INT, C.POINTER(P), C.POINTER(I64), C.POINTER(I64), C.POINTER(INT)]
+        L.vbc_sharded_xspan.argtypes = [P, INT, C.POINTER(I64), C.POINTER(I64)]
         L.vbc_mul.argtypes = [P, INT, P, I64, P, I64, D, D, INT, P, U]
         L.vbc_mul_mat.argtypes = [P, INT, I64, P, I64, I64, P, I64, I64, D, D, INT, P, U]
         L.vbc_mul_mat_ex.argtypes = [P, INT, I64, P, INT, I64, I64, P, INT, I64, I64, D, D, INT, P, U]

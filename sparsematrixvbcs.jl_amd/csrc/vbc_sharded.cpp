@@ -35,6 +35,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -58,6 +59,7 @@ struct vbc_sharded {
     std::vector<int> dev;
     std::vector<vbc_handle *> h;
     std::vector<int64_t> cut;        // ngpus+1 0-based cuts of the split dimension (columns or rows)
+    std::vector<int64_t> xlo, xhi;   // per shard: the span [xlo, xhi) of x its disjoint-output product reads
     std::vector<ncclComm_t> comm;
     std::vector<hipStream_t> st;     // per shard: internal stream (root: host-pointer products only)
     std::vector<hipEvent_t> done;    // per shard: end of its part of a product
@@ -222,14 +224,18 @@ int mul_device(vbc_sharded *s, int trans, const char *x, int64_t nx, char *y, in
         VBC_HIPS(hipStreamWaitEvent(s->st[g], s->start, 0));
     }
     auto stream = [&](int g) { return g == 0 ? s0 : s->st[g]; };
-    // 1. x to the shards: broadcast (replicated x) or one slice each
+    // 1. x to the shards: the span each one reads (disjoint output) or its slice (partial output)
     if (!s->comm.empty()) {
         *issued = true;
         NcclGroup grp;
         for (int g = 0; g < G && grp.ok(); g++) {
-            if (disj) {
-                grp.note(ncclBroadcast(x, g == 0 ? (void *)x : s->xb[g], (size_t)nx, dt, 0, s->comm[g], stream(g)),
-                         "ncclBroadcast(x)");
+            if (disj) {  // the span of x shard g reads, straight from the root (shard 0 reads the root's x)
+                const int64_t xl = s->xlo[g], xn = s->xhi[g] - s->xlo[g];
+                if (g == 0 || xn <= 0) continue;
+                grp.note(ncclSend(x + xl * esz, (size_t)xn, dt, g, s->comm[0], s0), "ncclSend(x span)");
+                if (grp.ok())
+                    grp.note(ncclRecv(static_cast<char *>(s->xb[g]) + xl * esz, (size_t)xn, dt, 0, s->comm[g], s->st[g]),
+                             "ncclRecv(x span)");
             } else if (g > 0 && len(g) > 0) {
                 grp.note(ncclSend(x + lo(g) * esz, (size_t)len(g), dt, g, s->comm[0], s0), "ncclSend(x)");
                 if (grp.ok()) grp.note(ncclRecv(s->xb[g], (size_t)len(g), dt, 0, s->comm[g], s->st[g]), "ncclRecv(x)");
@@ -435,17 +441,73 @@ int64_t row_runs(const Fields &f)
     return 1;
 }
 
+// The cuts of a split (byte-balanced, distributed.py stripe_split / row_split: value bytes + 4-B keys + stripe
+// headers) and, per shard, the span [xlo, xhi) of x its disjoint-output product reads -- the rows its stripes
+// store (stripe split, B'x) or the columns of the stripes with a stored row in its row range (row split, B x).
+// The root sends each shard that span instead of broadcasting x; a mesh operator's shard reads its own share
+// of x plus a halo.
+struct Plan {
+    std::vector<int64_t> cuts;      // stripe split: N+1 stripe cuts; row split: N+1 block-row (1D: row) cuts
+    std::vector<int64_t> xlo, xhi;  // per shard, 0-based; [0, 0) when it reads none
+};
+
+Plan plan_split(const Fields &f, int csz, int N, int split)
+{
+    const int64_t L = f.L;
+    const std::vector<int64_t> &S = f.S, &P = f.P, &I = f.I, &O = f.O;
+    Plan p;
+    p.xlo.assign(N, INT64_MAX);
+    p.xhi.assign(N, INT64_MIN);
+    if (split == VBC_SPLIT_STRIPES) {
+        std::vector<double> cost(L + 1, 0.0);
+        for (int64_t l = 0; l < L; l++)
+            cost[l + 1] = cost[l] + (double)((O[l + 1] - O[l]) * csz + (P[l + 1] - P[l]) * 4 + 12);
+        p.cuts = balanced_cuts(cost, N);
+        for (int g = 0; g < N; g++)
+            for (int64_t r = P[p.cuts[g]] - 1; r < P[p.cuts[g + 1]] - 1; r++) {
+                const int64_t k = I[r] - 1;
+                p.xlo[g] = std::min(p.xlo[g], f.is2d ? f.PS[k] - 1 : k);
+                p.xhi[g] = std::max(p.xhi[g], f.is2d ? f.PS[k + 1] - 1 : k + 1);
+            }
+    } else {
+        // cost per block row (1D: per row) = its blocks' value bytes + a 4-B key each
+        const int64_t K = f.is2d ? f.K : f.m;
+        std::vector<double> per(K + 1, 0.0);
+        for (int64_t l = 0; l < L; l++)
+            for (int64_t r = P[l] - 1; r < P[l + 1] - 1; r++)
+                per[I[r]] += (double)(f.u(I[r] - 1) * (S[l + 1] - S[l]) * csz + 4);  // I is 1-based: prefix index
+        for (int64_t k = 0; k < K; k++) per[k + 1] += per[k];
+        std::vector<int64_t> kc = balanced_cuts(per, N);  // block-row ranges
+        if (!f.is2d) {  // a 1DVBC's node runs stay whole (distributed.py row_split / row_runs)
+            const int64_t a = row_runs(f);
+            if (a > 1)
+                for (int g = 1; g < N; g++) kc[g] = std::max(kc[g - 1], std::min(K, (kc[g] + a / 2) / a * a));
+        }
+        for (int64_t l = 0; l < L; l++)
+            for (int64_t r = P[l] - 1; r < P[l + 1] - 1; r++) {  // shard g holds 1-based k in (kc[g], kc[g+1]]
+                const int g = (int)(std::lower_bound(kc.begin() + 1, kc.end(), I[r]) - (kc.begin() + 1));
+                p.xlo[g] = std::min(p.xlo[g], S[l] - 1);
+                p.xhi[g] = std::max(p.xhi[g], S[l + 1] - 1);
+            }
+        p.cuts = std::move(kc);
+    }
+    for (int g = 0; g < N; g++)
+        if (p.xhi[g] <= p.xlo[g]) p.xlo[g] = p.xhi[g] = 0;
+    return p;
+}
+
 // VBC_SPLIT_AUTO (vbc.h): the split with the smaller predicted time of the products `flags` builds (B'x for
 // VBC_CREATE_TRANSPOSED or no direction flag, B x for VBC_CREATE_FORWARD).  The model is distributed.py's
 // predict_product_us for this one-process handle's exchange: the slowest shard's kernel -- a
 // measured launch-and-ramp floor plus its bytes (matrix share, x reads, y writes) at the measured streaming
-// rate -- plus the exchange through the root: x broadcast and y slices gathered (disjoint output), or x
-// slices scattered and an ncclReduce of y (partial output), at ASSUMED xGMI rates (7 links of 76.8 GB/s per
-// direction, 60 % reached by a ring collective, 2 us per ring step; no multi-GPU box was available to measure).
+// rate -- plus the exchange through the root: each shard's x span sent over its own link and y slices
+// gathered (disjoint output), or x slices scattered and an ncclReduce of y (partial output), at ASSUMED xGMI
+// rates (7 links of 76.8 GB/s per direction, 60 % of it reached, 2 us per ring step; no multi-GPU box was
+// available to measure).
 constexpr double kModelT0Us = 3.1, kModelStreamGBs = 5700.0;
-constexpr double kModelCollGBs = 7 * 76.8 * 0.6, kModelStepUs = 2.0;
+constexpr double kModelLinkGBs = 76.8 * 0.6, kModelCollGBs = 7 * kModelLinkGBs, kModelStepUs = 2.0;
 
-double predict_us(const Fields &f, int csz, int N, int split, int trans)
+double predict_us(const Fields &f, int csz, int N, int split, int trans, const Plan &p)
 {
     const int64_t L = f.L;
     double mat = (double)csz * (double)(f.O[L] - 1) + 4.0 * (double)(f.P[L] - 1) + 4.0 * (3.0 * L + 3.0) +
@@ -454,12 +516,17 @@ double predict_us(const Fields &f, int csz, int N, int split, int trans)
     if (split == VBC_SPLIT_ROWS && N > 1) mat += 12.0 * (double)L * (N - 1) / N;  // every row shard keeps the headers
     const double nx = (double)(trans ? f.m : f.n) * csz, ny = (double)(trans ? f.n : f.m) * csz;
     const bool disj = disjoint_output(split, trans);
-    const double kern = kModelT0Us + (mat + (disj ? nx : nx / N) + (disj ? ny / N : ny)) / (kModelStreamGBs * 1e3);
+    double span = 0.0, sent = 0.0;  // the widest x span a shard reads; the widest the root sends
+    for (int g = 0; g < N; g++) {
+        span = std::max(span, (double)(p.xhi[g] - p.xlo[g]) * csz);
+        if (g > 0) sent = std::max(sent, (double)(p.xhi[g] - p.xlo[g]) * csz);
+    }
+    const double kern = kModelT0Us + (mat + (disj ? span : nx / N) + (disj ? ny / N : ny)) / (kModelStreamGBs * 1e3);
     if (N <= 1) return kern;
-    // a ring broadcast / reduce moves the whole vector through every hop (pipelined); the root's direct sends
-    // and receives of slices move (N-1)/N of it
+    // a ring reduce moves the whole vector through every hop (pipelined); the root's direct sends and receives
+    // of slices move (N-1)/N of it; the x spans go out over the root's N-1 links at once
     const double part = (double)(N - 1) / N, lat = (N - 1) * kModelStepUs, bw = kModelCollGBs * 1e3;
-    const double coll = disj ? (nx / bw + lat) + (part * ny / bw + lat)  // broadcast x, gather y slices
+    const double coll = disj ? (sent / (kModelLinkGBs * 1e3) + kModelStepUs) + (part * ny / bw + lat)  // x spans, y slices
                              : (part * nx / bw + lat) + (ny / bw + lat);  // scatter x slices, reduce y
     return kern + coll;
 }
@@ -474,8 +541,9 @@ int auto_split(const Fields &f, int csz, int N, unsigned flags)
     const bool fw = (flags & VBC_CREATE_FORWARD) != 0;
     double cost[2] = {0.0, 0.0};
     for (int sp = 0; sp < 2; sp++) {
-        if (t) cost[sp] += predict_us(f, csz, N, sp, 1);
-        if (fw) cost[sp] += predict_us(f, csz, N, sp, 0);
+        const Plan p = plan_split(f, csz, N, sp);
+        if (t) cost[sp] += predict_us(f, csz, N, sp, 1, p);
+        if (fw) cost[sp] += predict_us(f, csz, N, sp, 0, p);
     }
     if (cost[VBC_SPLIT_ROWS] < 0.98 * cost[VBC_SPLIT_STRIPES]) return VBC_SPLIT_ROWS;
     if (cost[VBC_SPLIT_STRIPES] < 0.98 * cost[VBC_SPLIT_ROWS]) return VBC_SPLIT_STRIPES;
@@ -521,12 +589,11 @@ int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *
     t64.index_bits = 64;
     const std::vector<int64_t> &S = f.S, &P = f.P, &I = f.I, &O = f.O;
 
-    // byte-balanced cuts (distributed.py stripe_split / row_split): value bytes + 4-B keys + stripe headers
+    Plan plan = plan_split(f, csz, ngpus, split);
+    s->xlo = plan.xlo;
+    s->xhi = plan.xhi;
     if (split == VBC_SPLIT_STRIPES) {
-        std::vector<double> cost(L + 1, 0.0);
-        for (int64_t l = 0; l < L; l++)
-            cost[l + 1] = cost[l] + (double)((O[l + 1] - O[l]) * csz + (P[l + 1] - P[l]) * 4 + 12);
-        const std::vector<int64_t> lc = balanced_cuts(cost, ngpus);
+        const std::vector<int64_t> &lc = plan.cuts;
         s->cut.resize(ngpus + 1);
         for (int g = 0; g <= ngpus; g++) s->cut[g] = S[lc[g]] - 1;  // column ranges
         for (int g = 0; g < ngpus; g++) {
@@ -542,19 +609,7 @@ int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *
             if (st) { destroy_all(s); return st; }
         }
     } else {
-        // cost per block row (1D: per row) = its blocks' value bytes + a 4-B key each
-        const int64_t K = f.is2d ? f.K : m;
-        std::vector<double> per(K + 1, 0.0);
-        for (int64_t l = 0; l < L; l++)
-            for (int64_t r = P[l] - 1; r < P[l + 1] - 1; r++)
-                per[I[r]] += (double)(f.u(I[r] - 1) * (S[l + 1] - S[l]) * csz + 4);  // I is 1-based: prefix index
-        for (int64_t k = 0; k < K; k++) per[k + 1] += per[k];
-        std::vector<int64_t> kc = balanced_cuts(per, ngpus);  // block-row ranges
-        if (!f.is2d) {  // a 1DVBC's node runs stay whole (distributed.py row_split / row_runs)
-            const int64_t a = row_runs(f);
-            if (a > 1)
-                for (int g = 1; g < ngpus; g++) kc[g] = std::max(kc[g - 1], std::min(K, (kc[g] + a / 2) / a * a));
-        }
+        const std::vector<int64_t> &kc = plan.cuts;  // block-row ranges
         s->cut.resize(ngpus + 1);
         for (int g = 0; g <= ngpus; g++) s->cut[g] = f.is2d ? f.PS[kc[g]] - 1 : kc[g];  // row ranges
         for (int g = 0; g < ngpus; g++) {
@@ -608,8 +663,10 @@ int create_sharded(vbc_sharded **out, Fields &f, int64_t nval, const vbc_types *
             destroy_all(s);
             return vbc::fail(VBC_HIP_ERROR, "event creation failed");
         }
+        // (x buffers zeroed once: a shard's product reads only its x span, which every product refreshes)
         if (g > 0 && !s->local &&
-            (hipMalloc(&s->xb[g], big * csz) != hipSuccess || hipMalloc(&s->yb[g], big * csz) != hipSuccess)) {
+            (hipMalloc(&s->xb[g], big * csz) != hipSuccess || hipMalloc(&s->yb[g], big * csz) != hipSuccess ||
+             hipMemset(s->xb[g], 0, big * csz) != hipSuccess)) {
             destroy_all(s);
             return vbc::fail(VBC_HIP_ERROR, "hipMalloc of an exchange buffer failed");
         }
@@ -706,6 +763,14 @@ int vbc_sharded_shard(const vbc_sharded *s, int g, vbc_handle **h, int64_t *lo, 
     if (lo) *lo = s->cut[g];
     if (hi) *hi = s->cut[g + 1];
     if (device) *device = s->dev[g];
+    return VBC_OK;
+}
+
+int vbc_sharded_xspan(const vbc_sharded *s, int g, int64_t *lo, int64_t *hi)
+{
+    if (!s || g < 0 || g >= s->ngpus) return fail(VBC_INVALID_ARG, "no such shard");
+    if (lo) *lo = s->xlo[g];
+    if (hi) *hi = s->xhi[g];
     return VBC_OK;
 }
 

@@ -299,7 +299,7 @@ class MultiGPUSparseMatrix1DVBC:
     threaded the same way, multiply_VBC.jl:182-189; its row split keeps Π's block rows whole).
 
         S = MultiGPUSparseMatrix1DVBC(B, devices=[0, 1, 2, 3], split="stripes")
-        mul_(y, S.T, x)      # mul!(y, B', x): x broadcast, y slices gathered on devices[0]
+        mul_(y, S.T, x)      # mul!(y, B', x): each shard's x span sent, y slices gathered on devices[0]
         mul_(y, S, x)        # mul!(y, B, x): x slices, ncclReduce(sum) of y
 
     `devices` all equal (e.g. [0, 0, 0]) runs every shard on that device with no communicator.
@@ -359,6 +359,26 @@ class MultiGPUSparseMatrix1DVBC:
             _L.check(_L.lib().vbc_sharded_shard(self._h, g, None, C.byref(lo), C.byref(hi), C.byref(dev)), "shard")
             out.append((lo.value, hi.value, dev.value))
         return out
+
+    def x_spans(self):
+        """[(lo, hi)] per shard: the 0-based span of x its disjoint-output product reads (vbc_sharded_xspan) --
+        what devices[0] sends it instead of broadcasting x."""
+        import ctypes as C
+        from . import _lib as _L
+        out = []
+        for g in range(len(self.devices)):
+            lo, hi = C.c_int64(), C.c_int64()
+            _L.check(_L.lib().vbc_sharded_xspan(self._h, g, C.byref(lo), C.byref(hi)), "xspan")
+            out.append((lo.value, hi.value))
+        return out
+
+    def shard_handle(self, g):
+        """Shard g's single-GPU handle (a raw vbc_handle pointer owned by this object)."""
+        import ctypes as C
+        from . import _lib as _L
+        h = C.c_void_p()
+        _L.check(_L.lib().vbc_sharded_shard(self._h, g, C.byref(h), None, None, None), "shard")
+        return h
 
     def shard_info(self, g):
         """vbc_get_info of shard g's single-GPU handle (its layouts: planar_split, planar_mask, ...)."""

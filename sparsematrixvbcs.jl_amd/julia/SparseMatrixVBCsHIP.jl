@@ -285,6 +285,12 @@ function split_kind(A::HIPShardedSparseMatrix)
     check(ccall((:vbc_sharded_split, libvbc), Cint, (Ptr{Cvoid}, Ptr{Cint}), A.handle, sp))
     return sp[] == VBC_SPLIT_STRIPES ? :stripes : :rows
 end
+"Shard g's x span (0-based lo:hi-1 as a Julia range lo+1:hi): the part of x its disjoint-output product reads."
+function x_span(A::HIPShardedSparseMatrix, g::Integer)
+    lo, hi = Ref{Int64}(0), Ref{Int64}(0)
+    check(ccall((:vbc_sharded_xspan, libvbc), Cint, (Ptr{Cvoid}, Cint, Ptr{Int64}, Ptr{Int64}), A.handle, g, lo, hi))
+    return (lo[] + 1):hi[]
+end
 Base.size(A::HIPShardedSparseMatrix, d::Integer) = size(A.host, d)
 Base.eltype(A::HIPShardedSparseMatrix) = eltype(A.host)
 

@@ -160,6 +160,7 @@ def test_sharded_create_validation_without_gpu():
     n = C.c_int()
     assert lib.vbc_sharded_count(None, C.byref(n)) == L.VBC_INVALID_ARG
     assert lib.vbc_sharded_shard(None, 0, None, None, None, None) == L.VBC_INVALID_ARG
+    assert lib.vbc_sharded_xspan(None, 0, None, None) == L.VBC_INVALID_ARG
     assert lib.vbc_sharded_destroy(None) == L.VBC_OK
 
 

@@ -348,3 +348,52 @@ def test_sharded_auto_split(forward, transposed, want):
         V.mul_(y, S.T if trans else S, dev(x))
         assert rel(y.cpu().numpy(), O.mul(R, x, np.zeros(ny), trans=trans)) <= TOL64, trans
     S.release()
+
+
+@pytest.mark.parametrize("split", ["stripes", "rows"])
+@pytest.mark.parametrize("which", ["ldoor", "random"])
+def test_x_spans_cover_every_read(mat, split, which):
+    """vbc_sharded_xspan: a shard's disjoint-output product (stripes: B'x, rows: B x) reads x only inside its
+    span -- what devices[0] sends a shard on another GPU instead of broadcasting x.  Each shard's product with
+    x poisoned (NaN) outside the span equals its product with the whole x bit for bit; on the mesh stand-in
+    the spans are a share of x plus a halo, far narrower than x."""
+    import ctypes as C
+    from sparsematrixvbcs_amd import _lib as L
+    if which == "ldoor":
+        B = V.SparseMatrix1DVBC[8](V.synthetic.standin("GHS_psdef/ldoor", scale=0.01).T.tocsc(), V.StrictChunker(8))
+    else:
+        B = mat
+    world = 4
+    S = D.MultiGPUSparseMatrix1DVBC(B, devices=[0] * world, split=split)
+    trans = split == "stripes"
+    nx = B.m if trans else B.n
+    rng = np.random.default_rng(21)
+    x = rng.uniform(-1, 1, nx)
+    stream = torch.cuda.current_stream().cuda_stream
+    spans, shards = S.x_spans(), S.shards()
+    try:
+        for g, ((lo, hi), (a, b, _)) in enumerate(zip(spans, shards)):
+            assert 0 <= lo <= hi <= nx, (g, lo, hi)
+            ny = b - a
+            xp = x.copy()
+            xp[:lo] = np.nan
+            xp[hi:] = np.nan
+            ys = []
+            for xv in (x, xp):
+                xd = dev(xv)
+                y = torch.full((ny,), float("nan"), dtype=torch.float64, device=DEV)
+                L.check(L.lib().vbc_mul(S.shard_handle(g), int(trans), xd.data_ptr(), nx, y.data_ptr(), ny, 1.0, 0.0,
+                                        L.VBC_MEM_DEVICE, stream, 0))
+                torch.cuda.synchronize()
+                ys.append(y.cpu().numpy())
+            assert not np.isnan(ys[1]).any(), (g, lo, hi)
+            assert np.array_equal(ys[0], ys[1]), g
+        if which == "ldoor":  # row-major 3D mesh: each shard's x is its quarter plus a halo
+            assert max(hi - lo for lo, hi in spans) < 0.5 * nx, spans
+        # and the sharded product as a whole (the spans are what a distinct-device exchange sends)
+        y = torch.full((B.n if trans else B.m,), float("nan"), dtype=torch.float64, device=DEV)
+        V.mul_(y, S.T if trans else S, dev(x))
+        ny = len(y)
+        assert rel(y.cpu().numpy(), O.mul(ref_of(B), x, np.zeros(ny), trans=trans)) <= TOL64
+    finally:
+        S.release()
