@@ -15,6 +15,11 @@ every rank builds its own libvbc handle from its slice:
       `mul` replicates y with one all_gather;
     * mul!(y, B', x): partial y from the rank's rows, one all_reduce(sum).
 
+Each rank's handle covers only what its shard touches: a stripe shard's rows are rebased to the span its
+stripes store (`rebase_rows`), a row shard drops the stripes that store none of its rows (`trim_stripes`), so
+the partial-output product writes that span (the rest of the partial is zero) instead of every row or column
+(the ldoor 1/8 stripe shard's B x: 16.4 -> 11.9 us), and x is read from the matching slice.
+
 `comm="cpu"` runs the collectives on host copies (gloo process groups on one GPU in tests); the
 per-rank product is always libvbc's GPU kernel unless a `local_mul` is injected (CPU-only tests).
 The reference has no distributed code at all; this is new in the build.
@@ -117,6 +122,27 @@ def row_shard(B, r0, r1):
                              val)
 
 
+def rebase_rows(S):
+    """S restricted to the span of rows its stripes store: (the (hi - lo) x n matrix, lo).  A shard of a mesh
+    operator's stripes stores its own rows plus a halo; its forward product then writes that span only, and
+    its transposed product reads x[lo:hi].  (S itself, 0 when it stores no row or spans every row.)"""
+    if len(S.idx) == 0:
+        return S, 0
+    lo, hi = int(S.idx.min()) - 1, int(S.idx.max())
+    if lo == 0 and hi == S.m:
+        return S, 0
+    return SparseMatrix1DVBC(S.W, hi - lo, S.n, S.Phi, S.pos, S.idx - lo, S.ofs, S.val), lo
+
+
+def trim_stripes(S):
+    """S without its leading and trailing stripes that store no row: (the matrix, its first column).  A row
+    shard of a mesh operator keeps the stripes of its rows plus a halo."""
+    nz = np.nonzero(np.diff(S.pos))[0]
+    if len(nz) == 0 or (nz[0] == 0 and nz[-1] == len(S.Phi) - 1):
+        return S, 0
+    return shard(S, int(nz[0]), int(nz[-1]) + 1)
+
+
 # --- cost model of a sharded product (SURVEY §8e; DESIGN §7) --------------------------------------------
 # Shard kernel: a fixed launch-and-ramp cost plus its bytes at the streaming rate one MI355X sustains -- both
 # MEASURED on this code (DESIGN §5.1b: a graph-replayed near-empty product 3.1 us; tools/exp/keep_probe.hip
@@ -193,17 +219,18 @@ class ShardedSparseMatrix1DVBC:
         self.m, self.n, self.W = B.m, B.n, B.W
         self.rank, self.world, self.group = rank, world, group
         self.split, self.comm = split, comm
+        # the local handle covers rows [row0, row0 + m_local) and columns [col0, col0 + n_local) of B
         if split == "stripes":
             self.cuts = stripe_split(B, world)
-            self.splits = [int(B.Phi.spl[c] - 1) for c in self.cuts]  # column ranges
-            self.local, self.col0 = shard(B, int(self.cuts[rank]), int(self.cuts[rank + 1]))
-            self.row0, self.n_local, self.m_local = 0, self.local.n, B.m
+            self.splits = [int(c) for c in (B.Phi.spl[self.cuts] - 1)]  # column ranges
+            sh, self.col0 = shard(B, int(self.cuts[rank]), int(self.cuts[rank + 1]))
+            self.local, self.row0 = rebase_rows(sh)
         else:
             self.cuts = row_split(B, world)
             self.splits = [int(c) for c in self.cuts]  # row ranges
             self.row0 = int(self.cuts[rank])
-            self.local = row_shard(B, self.row0, int(self.cuts[rank + 1]))
-            self.col0, self.n_local, self.m_local = 0, B.n, self.local.m
+            self.local, self.col0 = trim_stripes(row_shard(B, self.row0, int(self.cuts[rank + 1])))
+        self.m_local, self.n_local = self.local.m, self.local.n
         self.col_splits = self.splits if split == "stripes" else None  # (round-1 name)
         if local_mul is None:
             from .multiply import mul_
@@ -253,14 +280,29 @@ class ShardedSparseMatrix1DVBC:
             out[self.splits[r] - self.splits[0]:self.splits[r] - self.splits[0] + s].copy_(flat[r * ms:r * ms + s])
         return out
 
+    @staticmethod
+    def _outside(y, lo, n, beta):
+        """The entries of a full-length partial outside [lo, lo + n): beta * y (0 when beta is 0; then the
+        whole vector is zeroed in one fill -- the product overwrites [lo, lo + n) -- one launch, not two)."""
+        if beta == 0.0:
+            y.zero_()
+            return
+        if beta != 1.0:
+            for part in (y[:lo], y[lo + n:]):
+                part.mul_(beta)
+
     # --- mul!(y, B', x) ---------------------------------------------------------------------------
     def local_mul_t(self, y_local, x, alpha=1.0, beta=0.0):
-        """This rank's part of α·B'x + β·y.  stripes: y_local = columns col0 .. col0+n_local-1 of y
-        (final, no collective); rows: a length-n partial from x[row0 : row0+m_local] (β applied)."""
-        if self.split == "stripes":
-            return self._product(y_local, self.local.T, x, alpha, beta)
+        """This rank's part of α·B'x + β·y (x: length m, or already its rows [row0, row0 + m_local)).
+        stripes: y_local = columns col0 .. col0+n_local-1 of y (final, no collective); rows: y_local is a
+        length-n partial -- the product over the rank's columns, zero elsewhere (β applied on rank 0)."""
         xs = x[self.row0:self.row0 + self.m_local] if len(x) == self.m else x
-        return self._product(y_local, self.local.T, xs, alpha, beta if self.rank == 0 else 0.0)
+        if self.split == "stripes":
+            return self._product(y_local, self.local.T, xs, alpha, beta)
+        b = beta if self.rank == 0 else 0.0
+        self._outside(y_local, self.col0, self.n_local, b)
+        self._product(y_local[self.col0:self.col0 + self.n_local], self.local.T, xs, alpha, b)
+        return y_local
 
     def mul_t(self, y, x, alpha=1.0, beta=0.0):
         """Replicated y (length n) = α·B'x + β·y; x replicated (length m)."""
@@ -273,12 +315,17 @@ class ShardedSparseMatrix1DVBC:
 
     # --- mul!(y, B, x) ----------------------------------------------------------------------------
     def local_mul(self, y_local, x, alpha=1.0, beta=0.0):
-        """This rank's part of α·Bx + β·y.  rows: y_local = rows row0 .. row0+m_local-1 of y (final,
-        no collective); stripes: a length-m partial from x[col0 : col0+n_local] (β applied on rank 0)."""
-        if self.split == "rows":
-            return self._product(y_local, self.local, x, alpha, beta)
+        """This rank's part of α·Bx + β·y (x: length n, or already its columns [col0, col0 + n_local)).
+        rows: y_local = rows row0 .. row0+m_local-1 of y (final, no collective); stripes: y_local is a
+        length-m partial -- the product over the rows the rank's stripes store, zero elsewhere (β applied
+        on rank 0)."""
         xs = x[self.col0:self.col0 + self.n_local] if len(x) == self.n else x
-        return self._product(y_local, self.local, xs, alpha, beta if self.rank == 0 else 0.0)
+        if self.split == "rows":
+            return self._product(y_local, self.local, xs, alpha, beta)
+        b = beta if self.rank == 0 else 0.0
+        self._outside(y_local, self.row0, self.m_local, b)
+        self._product(y_local[self.row0:self.row0 + self.m_local], self.local, xs, alpha, b)
+        return y_local
 
     def mul(self, y, x, alpha=1.0, beta=0.0):
         """Replicated y (length m) = α·Bx + β·y; x replicated (length n)."""

@@ -25,16 +25,18 @@ def oracle_mul(y, op, x, alpha, beta):
     return y
 
 
-def make_matrix():
+def make_matrix(kind="random"):
+    if kind == "mesh":  # a 3D stiffness operator: every shard touches its own rows / columns plus a halo
+        return V.SparseMatrix1DVBC[8](V.synthetic.fe_stiffness_3d(3000, 60000), V.StrictChunker(8))
     w = np.arange(60) % 5 + 1
     return V.synthetic.vbr_1dvbc(500, 60, 700, w, W=8, seed=7)
 
 
-def _worker(rank, world, port, q, split):
+def _worker(rank, world, port, q, split, kind="random"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        B = make_matrix()
+        B = make_matrix(kind)
         S = V.distributed.ShardedSparseMatrix1DVBC(B, rank, world, local_mul=oracle_mul, split=split)
         rng = np.random.default_rng(3)
         xt = torch.from_numpy(rng.uniform(-1, 1, B.m))
@@ -68,12 +70,16 @@ def free_port():
 
 
 @pytest.mark.parametrize("split", ["stripes", "rows"])
-def test_sharded_products_world2(split):
+@pytest.mark.parametrize("kind", ["random", "mesh"])
+def test_sharded_products_world2(split, kind):
+    """Both splits, both directions, world 2 over gloo (the oracle as each rank's product).  On the mesh
+    operator the local handles are rebased to the rows (stripe split) / trimmed to the columns (row split)
+    their shard touches, and the partial-output products still sum to the oracle's."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -81,7 +87,7 @@ def test_sharded_products_world2(split):
         p.join(timeout=60)
     for r in res:
         assert len(r) == 9, r
-    B = make_matrix()
+    B = make_matrix(kind)
     R = O.Ref1DVBC(B.m, B.n, B.W, B.Phi.spl, B.pos, B.idx, B.ofs, B.val)
     rng = np.random.default_rng(3)
     xt, xf, y0 = rng.uniform(-1, 1, B.m), rng.uniform(-1, 1, B.n), rng.uniform(-1, 1, B.m)
@@ -102,6 +108,8 @@ def test_sharded_products_world2(split):
         assert sum(r[5] for r in res) == B.n
     else:
         assert sum(r[6] for r in res) == B.m
+    if kind == "mesh":  # the other dimension is rebased / trimmed to what each shard touches
+        assert all((r[6] < B.m) if split == "stripes" else (r[5] < B.n) for r in res), [r[5:] for r in res]
 
 
 def test_row_split_reassembly():

@@ -55,33 +55,42 @@ def main():
         per = []
         ranks = [int(r) for r in args.ranks.split(",")] if args.ranks else range(world)
         for r in ranks:
-            if world == 1:
-                S = B
-            elif rows:
-                S = D.row_shard(B, int(cuts[r]), int(cuts[r + 1]))
-            else:
-                S, _ = D.shard(B, int(cuts[r]), int(cuts[r + 1]))
+            # a rank's view of the split (distributed.ShardedSparseMatrix1DVBC: rows rebased / stripes trimmed to
+            # what the shard touches); its products need no collective here -- the partial direction's
+            # reduction is priced by the model below
+            Sh = None if world == 1 else D.ShardedSparseMatrix1DVBC(B, r, world, split=args.split)
+            S = B if world == 1 else Sh.local
 
             def time_dir(trans):
-                nx, ny = (S.m, S.n) if trans else (S.n, S.m)
+                nx, ny = (B.m, B.n) if trans else (B.n, B.m)
                 xs = torch.from_numpy(np.random.default_rng(1 if trans else 2).uniform(-1, 1, nx).astype(dtype)).to(device)
-                ys = torch.empty(ny, dtype=xs.dtype, device=device)
-                op = S.T if trans else S
+                if Sh is None:
+                    op = B.T if trans else B
+                    ys = torch.empty(ny, dtype=xs.dtype, device=device)
+                    step = lambda: V.mul_(ys, op, xs)  # noqa: E731
+                else:  # the disjoint direction writes the rank's slice, the partial one a full-length y
+                    disjoint = trans != rows
+                    ys = torch.empty((Sh.n_local if trans else Sh.m_local) if disjoint else ny, dtype=xs.dtype,
+                                     device=device)
+                    step = (lambda: Sh.local_mul_t(ys, xs)) if trans else (lambda: Sh.local_mul(ys, xs))
                 with torch.cuda.stream(stream):
                     S.handle(0, trans)
                     for _ in range(args.warmup):
-                        V.mul_(ys, op, xs)
+                        step()
                 torch.cuda.synchronize(device)
-                wall, ev_ms, _ = bench.timed_products(lambda: V.mul_(ys, op, xs), args.steps, device, stream, 1)
+                wall, ev_ms, _ = bench.timed_products(step, args.steps, device, stream, 1)
                 return round(ev_ms * 1e3, 2), round(wall / args.steps * 1e6, 2), bench.kernel_name(S, 0, 1, trans=trans)
 
             ev, wall, kern = time_dir(main_t)
             rec = {"rank": r, "range": [int(cuts[r]), int(cuts[r + 1])], "bytes": bench.algorithmic_bytes(S, esz),
                    "us_event": ev, "us_wall": wall, "kernel": kern}
+            if Sh is not None:
+                rec["local_rows"] = [Sh.row0, Sh.row0 + Sh.m_local]
+                rec["local_cols"] = [Sh.col0, Sh.col0 + Sh.n_local]
             if args.forward:  # the other direction: a partial y (length m for stripes' B x, n for rows' B'x)
                 fev, fwall, fkern = time_dir(not main_t)
                 rec.update(fwd_us_event=fev, fwd_us_wall=fwall, fwd_kernel=fkern,
-                           allreduce_bytes=int((S.n if rows else S.m) * esz) if world > 1 else 0)
+                           allreduce_bytes=int((B.n if rows else B.m) * esz) if world > 1 else 0)
             per.append(rec)
             if world > 1:
                 S.release()
