@@ -89,6 +89,76 @@ __device__ __forceinline__ void ld_run(gptr<const T> p, T (&r)[RUN])
     }
 }
 
+// fp64 runs of 3 (24 B at 8-B alignment: a node's x entries) gathered by lane PAIRS (round 6; PAIRS = true:
+// the lane-stream kernel, FE-3D 214.8 / 213.6 -> 210.9 / 210.9 us B'x / B·x, profiles/r06o_*.log; the split
+// kernels of small shards, latency-bound, keep one gather per lane -- the cross-lane swap waits for both
+// loads: ldoor 1/8 forward shard 15.9 -> 17.9 us with pairs).  Each lane
+// still folds its own run, but the pair (l, l ^ 1) loads both runs with two 16-B loads per lane -- load A
+// the even lane's run, load B the odd lane's, the even lane at the run's first element and the odd lane at
+// its second -- instead of one 16-B and one 8-B load per lane: every load instruction then touches 32 runs'
+// lines, not 64 (the vector-memory path costs ≈ 2.4 CU cycles per distinct line: 306 -> 169 cycles per 64
+// runs, tools/exp/ta_probe.hip shapes 12-14).  The slots: A's pair (x0, x1) or (x1, x2), B's likewise; a
+// DPP quad_perm swap gives each lane the element its partner loaded (xrun_values).  Every lane of the wave
+// must be active (the kernels call these at wave-uniform points); a dead or padding lane's index is the
+// in-range index it would have gathered anyway.  Other eltypes / run lengths: ld_run, RUN slots.
+template <typename T, int RUN, bool PAIRS = false>
+__host__ __device__ constexpr bool xrun_pairs()
+{
+#ifdef VBC_XRUN_SINGLE  // (A/B build, tools/exp/build_variant.sh: each lane gathers its own run)
+    return false;
+#else
+    return PAIRS && sizeof(T) == 8 && RUN == 3;
+#endif
+}
+template <typename T, int RUN, bool PAIRS = false>
+__host__ __device__ constexpr int xrun_slots() { return xrun_pairs<T, RUN, PAIRS>() ? 4 : RUN; }
+
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ double pair_swap(double v)
+{
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t lo = pair_swap((uint32_t)u), hi = pair_swap((uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, lo | (hi << 32));
+}
+
+template <typename T, int RUN, bool PAIRS = false>
+__device__ __forceinline__ void ld_xrun(gptr<const T> xg, uint32_t idx, T (&r)[xrun_slots<T, RUN, PAIRS>()])
+{
+    if constexpr (xrun_pairs<T, RUN, PAIRS>()) {
+        const uint32_t odd = threadIdx.x & 1, other = pair_swap(idx);
+        const uint32_t ia = (odd ? other : idx) + odd, ib = (odd ? idx : other) + odd;
+        struct __attribute__((packed, aligned(8))) d2p { double a, b; };
+        typedef const __attribute__((address_space(1))) d2p *pp;
+        const pp A = (pp)(xg + ia), B = (pp)(xg + ib);  // (member reads merge into one 16-B load each)
+        r[0] = A->a;
+        r[1] = A->b;
+        r[2] = B->a;
+        r[3] = B->b;
+    } else {
+        ld_run<T, RUN>(xg + idx, r);
+    }
+}
+
+// The lane's own run from ld_xrun's slots (even lane: A = its (x0, x1), the odd lane's A.b = its x2; odd
+// lane: B = its (x1, x2), the even lane's B.a = its x0).
+template <typename T, int RUN, bool PAIRS = false>
+__device__ __forceinline__ void xrun_values(const T (&r)[xrun_slots<T, RUN, PAIRS>()], T (&x)[RUN])
+{
+    if constexpr (xrun_pairs<T, RUN, PAIRS>()) {
+        const bool odd = (threadIdx.x & 1) != 0;
+        const double pa = pair_swap(r[1]), pb = pair_swap(r[2]);
+        x[0] = odd ? pb : r[0];
+        x[1] = odd ? r[2] : r[1];
+        x[2] = odd ? r[3] : pa;
+    } else {
+#pragma unroll
+        for (int d = 0; d < RUN; d++) x[d] = r[d];
+    }
+}
+
 // One range (wave): chunks [rchunk[r], rchunk[r+1]), rows [rrow[r], rrow[r+1]).
 // RUN > 1 (b.run): every lane's rows come in aligned runs of RUN consecutive x rows (a node's dof
 // rows in a 3-dof stiffness operator): keys and the chunk's LAST flag are read from each run's first
@@ -137,11 +207,11 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
         }
     };
     constexpr uint32_t kPad16 = 0xFFFF8000u;
-    auto gather = [&](const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], T (&xv)[NR][RUN]) {
+    auto gather = [&](const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], T (&xv)[NR][xrun_slots<T, RUN>()]) {
 #pragma unroll
         for (int j = 0; j < NR; j++) {
             const uint32_t gi = KC ? (bs[j] & kSlotIdx) + (kk[j] == kPad16 ? 0u : kk[j]) : kk[j] & kSlotIdx;
-            ld_run<T, RUN>(xg + gi, xv[j]);
+            ld_xrun<T, RUN>(xg, gi, xv[j]);
         }
     };
     T acc[W_];
@@ -206,14 +276,16 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
     auto compute = [&](int R, const uint32_t (&kk)[NR], const uint32_t (&bs)[NR], const int (&nl)[NR],
-                       const T (&v)[U][W_], const T (&xv)[NR][RUN]) {
+                       const T (&v)[U][W_], const T (&xv)[NR][xrun_slots<T, RUN>()]) {
 #pragma unroll
         for (int j = 0; j < NR; j++) {
             const bool pad = MASK ? lane >= nl[j] : (KC ? kk[j] == kPad16 : (kk[j] & kPad) != 0);
             const bool live = R + j * RUN < R1v && !(MASK && pad);  // MASK: lane 0's values, never folded
+            T xr[RUN];
+            xrun_values<T, RUN>(xv[j], xr);
 #pragma unroll
             for (int d = 0; d < RUN; d++) {  // the run's rows in stored (reference) order
-                const T xe = pad ? T(0) : xv[j][d];
+                const T xe = pad ? T(0) : xr[d];
 #pragma unroll
                 for (int e = 0; e < W_; e++) {
                     const T nv = fmadd(v[j * RUN + d][e], xe, acc[e]);
@@ -226,7 +298,7 @@ __device__ __forceinline__ void run_planar(const SlotBin &b, int r, int lane, co
     };
     uint32_t kA[NR], kB[NR], bA[NR], bB[NR];
     int nA[NR], nB[NR];
-    T vA[U][W_], vB[U][W_], xv[NR][RUN];
+    T vA[U][W_], vB[U][W_], xv[NR][xrun_slots<T, RUN>()];
     load(R0, kA, bA, nA, vA);
     __builtin_amdgcn_s_waitcnt(0);
     for (int R = R0; R < R1; R += 2 * U) {
@@ -327,14 +399,16 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
     // fold a step; kk: the runs' keys (or just their PAD / LAST bits)
     auto compute = [&](int R, const uint32_t (&kk)[NR], const int (&nl)[NR], const T (&v)[U][W_],
-                       const T (&xv)[NR][RUN]) {
+                       const T (&xv)[NR][xrun_slots<T, RUN, true>()]) {
 #pragma unroll
         for (int j = 0; j < NR; j++) {
             const bool live = R + j * RUN < R1v && lane < nl[j];  // dead lanes hold lane 0's values
             const bool kpad = (kk[j] & kPad) != 0;                // an empty stripe's zero run
+            T xr[RUN];
+            xrun_values<T, RUN, true>(xv[j], xr);
 #pragma unroll
             for (int d = 0; d < RUN; d++) {  // the run's rows in stored (reference) order
-                const T xe = kpad ? T(0) : xv[j][d];
+                const T xe = kpad ? T(0) : xr[d];
 #pragma unroll
                 for (int e = 0; e < W_; e++) {
                     const T nv = fmadd(v[j * RUN + d][e], xe, acc[e]);
@@ -370,21 +444,21 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
     };
     // DIAG (tools/ab.py ablations, VBC_DIAG): 1 = no x gathers (x taken as 1), 2 = gathers confined to
     // the first 16 K rows of x (L2-resident), 3 = no LDS stores of finished stripes
-    auto gather = [&](const uint32_t (&kk)[NR], T (&xv)[NR][RUN]) {
+    auto gather = [&](const uint32_t (&kk)[NR], T (&xv)[NR][xrun_slots<T, RUN, true>()]) {
 #pragma unroll
         for (int j = 0; j < NR; j++) {
             if constexpr (DIAG == 1) {
 #pragma unroll
-                for (int d = 0; d < RUN; d++) xv[j][d] = T(1);
+                for (int d = 0; d < xrun_slots<T, RUN, true>(); d++) xv[j][d] = T(1);
             } else {
-                ld_run<T, RUN>(xg + (kk[j] & (DIAG == 2 ? 0x3FFFu : kSlotIdx)), xv[j]);
+                ld_xrun<T, RUN, true>(xg, kk[j] & (DIAG == 2 ? 0x3FFFu : kSlotIdx), xv[j]);
             }
         }
     };
     if constexpr (!DEEP) {
         uint32_t kA[NR], kB[NR];
         int nA[NR], nB[NR];
-        T vA[U][W_], vB[U][W_], xv[NR][RUN];
+        T vA[U][W_], vB[U][W_], xv[NR][xrun_slots<T, RUN, true>()];
         load_keys(R0, kA, nA);
         load_vals(R0, nA, vA);
         __builtin_amdgcn_s_waitcnt(0);
@@ -401,7 +475,7 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
     } else {
         // a step's key buffer is free once its gathers are issued (PAD / LAST move to a flags word), so
         // two key buffers rotate with the two value and gather buffers
-        auto issue = [&](const uint32_t (&kk)[NR], T (&xv)[NR][RUN], uint32_t (&fl)[NR]) {
+        auto issue = [&](const uint32_t (&kk)[NR], T (&xv)[NR][xrun_slots<T, RUN, true>()], uint32_t (&fl)[NR]) {
             gather(kk, xv);
 #pragma unroll
             for (int j = 0; j < NR; j++) {
@@ -411,7 +485,7 @@ __device__ __forceinline__ void run_planar_lanes(const SlotBin &b, int r, int la
         };
         uint32_t kA[NR], kB[NR], fA[NR], fB[NR];
         int nA[NR], nB[NR];
-        T vA[U][W_], vB[U][W_], xA[NR][RUN], xB[NR][RUN];
+        T vA[U][W_], vB[U][W_], xA[NR][xrun_slots<T, RUN, true>()], xB[NR][xrun_slots<T, RUN, true>()];
         load_keys(R0, kA, nA);
         load_keys(R0 + U, kB, nB);
         load_vals(R0, nA, vA);
@@ -523,11 +597,11 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
         }
     };
     constexpr uint32_t kPad16 = 0xFFFF8000u;
-    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&bs)[U], T (&xv)[U][W_]) {
+    auto gather = [&](const uint32_t (&kk)[U], const uint32_t (&bs)[U], T (&xv)[U][xrun_slots<T, W_>()]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t gi = KC ? (bs[u] & kSlotIdx) + (kk[u] == kPad16 ? 0u : kk[u]) : kk[u] & kSlotIdx;
-            ld_run<T, W_>(xg + gi, xv[u]);
+            ld_xrun<T, W_>(xg, gi, xv[u]);
         }
     };
     T acc[R];
@@ -578,16 +652,18 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
     int R1v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(R1v) : "s"(R1));
     auto compute = [&](int Rr, const uint32_t (&kk)[U], const uint32_t (&bs)[U], const int (&nl)[U],
-                       const T (&v)[U][WV], const T (&xv)[U][W_]) {
+                       const T (&v)[U][WV], const T (&xv)[U][xrun_slots<T, W_>()]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const bool live = Rr + u < R1v;
             const bool pad = MASK ? lane >= nl[u] : (KC ? kk[u] == kPad16 : (kk[u] & kPad) != 0);
+            T xr[W_];
+            xrun_values<T, W_>(xv[u], xr);
 #pragma unroll
             for (int q = 0; q < R; q++) {  // one dot product per output row of the run
-                T d = v[u][q * W_] * xv[u][0];
+                T d = v[u][q * W_] * xr[0];
 #pragma unroll
-                for (int e = 1; e < W_; e++) d = fmadd(v[u][q * W_ + e], xv[u][e], d);
+                for (int e = 1; e < W_; e++) d = fmadd(v[u][q * W_ + e], xr[e], d);
                 acc[q] = (live && !pad) ? acc[q] + d : acc[q];
             }
             const uint32_t lastw = KC ? bs[u] : (uint32_t)__builtin_amdgcn_readfirstlane((int)kk[u]);
@@ -596,7 +672,7 @@ __device__ __forceinline__ void run_planar_fwd(const SlotBin &b, int r, int lane
     };
     uint32_t kA[U], kB[U], bA[U], bB[U];
     int nA[U], nB[U];
-    T vA[U][WV], vB[U][WV], xv[U][W_];
+    T vA[U][WV], vB[U][WV], xv[U][xrun_slots<T, W_>()];
     load(R0, kA, bA, nA, vA);
     __builtin_amdgcn_s_waitcnt(0);
     for (int Rr = R0; Rr < R1; Rr += 2 * U) {
@@ -656,7 +732,7 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_fwd_split(const SlotBin b,
     for (int q = 0; q < R; q++) acc[q] = T(0);
     for (int Rr = a; Rr < e; Rr += U) {
         uint32_t kk[U];
-        T v[U][WV], xv[U][W_];
+        T v[U][WV], xv[U][xrun_slots<T, W_>()];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int Rc = min(Rr + u, e - 1);
@@ -664,15 +740,17 @@ __global__ __launch_bounds__(64 * P) void spmv_planar_fwd_split(const SlotBin b,
             ld_row<T, WV, 0, false>(val + (size_t)Rc * 64 * WV, lane, v[u]);
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) ld_run<T, W_>(xg + (kk[u] & kSlotIdx), xv[u]);
+        for (int u = 0; u < U; u++) ld_xrun<T, W_>(xg, kk[u] & kSlotIdx, xv[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const bool live = Rr + u < e && (kk[u] & kPad) == 0;
+            T xr[W_];
+            xrun_values<T, W_>(xv[u], xr);
 #pragma unroll
             for (int q = 0; q < R; q++) {
-                T d = v[u][q * W_] * xv[u][0];
+                T d = v[u][q * W_] * xr[0];
 #pragma unroll
-                for (int k = 1; k < W_; k++) d = fmadd(v[u][q * W_ + k], xv[u][k], d);
+                for (int k = 1; k < W_; k++) d = fmadd(v[u][q * W_ + k], xr[k], d);
                 acc[q] = live ? acc[q] + d : acc[q];
             }
         }
@@ -1135,7 +1213,7 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
         // strict 9.1 -> 11.5 us, 'min blocks' 14.7 -> 15.4 us, profiles/r04_ab3_*.log)
         for (int R = a; R < e; R += NB * RUN) {
             uint32_t kk[NB];
-            T v[NB][RUN][W_], xv[NB][RUN];
+            T v[NB][RUN][W_], xv[NB][xrun_slots<T, RUN>()];
 #pragma unroll
             for (int j = 0; j < NB; j++) {
                 const size_t o = (size_t)min(R + j * RUN, e - RUN) * 64 + lane;
@@ -1147,15 +1225,17 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
                 for (int d = 0; d < RUN; d++)
                     ld_row<T, W_, 0, NT>(val + (size_t)min(R + j * RUN + d, e - 1) * 64 * W_, lane, v[j][d]);
 #pragma unroll
-            for (int j = 0; j < NB; j++) ld_run<T, RUN>(xg + (kk[j] & imask), xv[j]);
+            for (int j = 0; j < NB; j++) ld_xrun<T, RUN>(xg, kk[j] & imask, xv[j]);
 #pragma unroll
             for (int j = 0; j < NB; j++) {
                 const bool live = R + j * RUN < e;
                 const bool pad = (kk[j] & kPad) != 0;
+                T xr[RUN];
+                xrun_values<T, RUN>(xv[j], xr);
 #pragma unroll
                 for (int d = 0; d < RUN; d++) {
                     const bool hole = b.holes && !((kk[j] >> (kHoleShift + d)) & 1u);
-                    const T xe = (pad || hole) ? T(0) : xv[j][d];
+                    const T xe = (pad || hole) ? T(0) : xr[d];
 #pragma unroll
                     for (int k = 0; k < W_; k++) {
                         const T nv = fmadd(v[j][d][k], xe, acc[k]);
@@ -1166,7 +1246,7 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
         }
     } else if constexpr (MODE == 1 && !KC && DIAG == 0) {
         uint32_t kA[NR], kB[NR];
-        T vA[U][W_], vB[U][W_], xv[NR][RUN];
+        T vA[U][W_], vB[U][W_], xv[NR][xrun_slots<T, RUN>()];
         // rows past the slice are clamped to its last run (loaded, folded as no-ops): no branch in the
         // loop body, so the compiler's waits stay counted
         auto load = [&](int R, uint32_t (&kk)[NR], T (&v)[U][W_]) {
@@ -1180,17 +1260,19 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
         };
         auto gather = [&](const uint32_t (&kk)[NR]) {
 #pragma unroll
-            for (int j = 0; j < NR; j++) ld_run<T, RUN>(xg + (kk[j] & imask), xv[j]);
+            for (int j = 0; j < NR; j++) ld_xrun<T, RUN>(xg, kk[j] & imask, xv[j]);
         };
         auto fold = [&](int R, const uint32_t (&kk)[NR], const T (&v)[U][W_]) {
 #pragma unroll
             for (int j = 0; j < NR; j++) {
                 const bool live = R + j * RUN < e;
                 const bool pad = (kk[j] & kPad) != 0;
+                T xr[RUN];
+                xrun_values<T, RUN>(xv[j], xr);
 #pragma unroll
                 for (int d = 0; d < RUN; d++) {
                     const bool hole = b.holes && !((kk[j] >> (kHoleShift + d)) & 1u);
-                    const T xe = (pad || hole) ? T(0) : xv[j][d];
+                    const T xe = (pad || hole) ? T(0) : xr[d];
 #pragma unroll
                     for (int k = 0; k < W_; k++) {
                         const T nv = fmadd(v[j * RUN + d][k], xe, acc[k]);
@@ -1211,7 +1293,7 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
     } else
     for (int R = a; R < e; R += NS * U) {
         uint32_t kk[NS][NR], bs[NS][NR];
-        T v[NS][U][W_], xv[NS][NR][RUN];
+        T v[NS][U][W_], xv[NS][NR][xrun_slots<T, RUN>()];
 #pragma unroll
         for (int t = 0; t < NS; t++)
 #pragma unroll
@@ -1235,9 +1317,9 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
                 const uint32_t gi = KC ? (bs[t][j] & kSlotIdx) + (kk[t][j] == kPad16 ? 0u : kk[t][j]) : kk[t][j] & imask;
                 if constexpr (DIAG == 1) {
 #pragma unroll
-                    for (int d = 0; d < RUN; d++) xv[t][j][d] = T(1) + T(gi & 1);
+                    for (int d = 0; d < xrun_slots<T, RUN>(); d++) xv[t][j][d] = T(1) + T(gi & 1);
                 } else {
-                    ld_run<T, RUN>(xg + (DIAG == 2 ? (gi & 0xFFu) : gi), xv[t][j]);
+                    ld_xrun<T, RUN>(xg, DIAG == 2 ? (gi & 0xFFu) : gi, xv[t][j]);
                 }
             }
 #pragma unroll
@@ -1246,10 +1328,12 @@ __device__ __forceinline__ void split_chunk(const SplitView &b, int c, int wv, i
             for (int j = 0; j < NR; j++) {
                 const bool live = R + t * U + j * RUN < e;
                 const bool pad = KC ? kk[t][j] == kPad16 : (kk[t][j] & kPad) != 0;
+                T xr[RUN];
+                xrun_values<T, RUN>(xv[t][j], xr);
 #pragma unroll
                 for (int d = 0; d < RUN; d++) {
                     const bool hole = !KC && b.holes && !((kk[t][j] >> (kHoleShift + d)) & 1u);
-                    const T xe = (pad || hole) ? T(0) : xv[t][j][d];
+                    const T xe = (pad || hole) ? T(0) : xr[d];
 #pragma unroll
                     for (int k = 0; k < W_; k++) {
                         const T nv = fmadd(v[t][j * RUN + d][k], xe, acc[k]);

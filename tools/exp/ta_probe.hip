@@ -11,6 +11,9 @@
 //   9 dwordx3, 48 lanes, 576 B contiguous (16 tiles' 3 x 3 values, lanes q < 3 of each group of 4)
 //  10 dword, 16 groups of 4 lanes reading the same 4 B, 64 B contiguous (16 keys, each read by 4 lanes)
 //  11 dwordx4, 64 lanes contiguous 1 KB STORE (16 stripes' outputs)
+//  12 16 B per lane at its own random 24-B run (8-B aligned: x0, x1 of a fp64 3-dof gather)
+//  13 8 B per lane at its own random 24-B run + 16 (x2 of the same gather)
+//  14 16 B per lane, lane pairs on one random 24-B run (offsets 0 and 8: a cooperative 3-dof gather)
 // Prints ns per load instruction per CU (all waves of the chip together).
 #include <hip/hip_runtime.h>
 
@@ -75,6 +78,17 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ t, uint32
                 }
             } else if constexpr (SHAPE == 10) {
                 acc += t[(size_t)(((base0 + (uint32_t)(it + u) * 40503u) & (nlines - 1))) * 16 + (lane >> 2)];
+            } else if constexpr (SHAPE == 12 || SHAPE == 13 || SHAPE == 14) {
+                struct __attribute__((packed, aligned(8))) d2 { double a, b; };
+                const uint32_t hr = SHAPE == 14 ? hash(wid * 7919u + (lane >> 1) * 31u) + (uint32_t)(it + u) * 40503u
+                                                : hash(wid * 7919u + lane * 31u) + (uint32_t)(it + u) * 40503u;
+                const char *run = (const char *)t + (size_t)(hr & 0x1FFFFu) * 24;
+                if constexpr (SHAPE == 13) {
+                    acc += (float)*(const double *)(run + 16);
+                } else {
+                    const d2 v = *(const d2 *)(run + (SHAPE == 14 ? (lane & 1) * 8 : 0));
+                    acc += (float)(v.a + v.b);
+                }
             } else {
                 f4 *o = (f4 *)(out + 64 + (size_t)(((base0 + (uint32_t)(it + u) * 40503u) & (1023u))) * 256) + lane;
                 *o = f4{acc, acc, acc, acc};
@@ -114,8 +128,9 @@ int main()
     const char *names[] = {"dword contiguous 256 B", "dword 4 x 64 B random", "dwordx4 contiguous 1 KB",
                            "dwordx4 4 x 64 B (16 lanes)", "dwordx3 4 x 192 B", "dwordx4 4 x 192 B (48 lanes)",
                            "dword broadcast x4 groups", "dwordx3 broadcast x4 groups", "dwordx4 16 x 64 B random",
-                           "dwordx3 48 lanes 576 B contiguous", "dword 16 x 4 B, 4 lanes each", "dwordx4 store 1 KB"};
-    float ms[12];
+                           "dwordx3 48 lanes 576 B contiguous", "dword 16 x 4 B, 4 lanes each", "dwordx4 store 1 KB",
+                           "16 B, 64 random 24-B runs", "8 B, 64 random 24-B runs + 16", "16 B, 32 runs, lane pairs"};
+    float ms[15];
     ms[0] = run<0>(t, nlines, iters, out, grid);
     ms[1] = run<1>(t, nlines, iters, out, grid);
     ms[2] = run<2>(t, nlines, iters, out, grid);
@@ -128,8 +143,11 @@ int main()
     ms[9] = run<9>(t, nlines, iters, out, grid);
     ms[10] = run<10>(t, nlines, iters, out, grid);
     ms[11] = run<11>(t, nlines, iters, out, grid);
+    ms[12] = run<12>(t, nlines, iters, out, grid);
+    ms[13] = run<13>(t, nlines, iters, out, grid);
+    ms[14] = run<14>(t, nlines, iters, out, grid);
     const double per_cu = (double)grid * 4 * iters / cus;  // wave-instructions per CU
-    for (int s = 0; s < 12; s++)
+    for (int s = 0; s < 15; s++)
         printf("shape %d %-32s %8.3f ms  %6.2f cycles/instr/CU at 2.4 GHz\n", s, names[s], ms[s],
                ms[s] * 1e-3 * 2.4e9 / per_cu);
     return 0;
