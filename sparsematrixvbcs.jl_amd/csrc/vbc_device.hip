@@ -526,46 +526,23 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     bool affine = true;
     for (size_t q = 1; q < out.size() && affine; q++)
         affine = (int64_t)out[q] == (int64_t)out[0] + (int64_t)q * (out[1] - out[0]);
-    // Chunk interleave (SlotBin::ilv; slotted B'x bins in natural order, several chunks per range): range r
-    // takes chunks r, r + nr, r + 2 nr, ... stored range-major.  The resident waves of an XCD are a contiguous
-    // run of ranges (xcd_chunk), so at any moment they fold a contiguous WINDOW of chunks that advances
-    // through the bin, and the x rows a mesh operator's stripes share across a bandwidth (a 2D grid's node j
-    // couples j +- g) are gathered by waves of the same window within microseconds of each other -- L2 hits --
-    // instead of by waves ~2 ranges apart at different points of their ranges, long after the line left L2.
-    const bool ilv = h->slot_ilv != 0 && !planar && kind == 0 && split == 1 && ks == 1 && order.empty() && affine &&
-                     slot_spl(h, kind, w) == 1 && nr >= 1 && nch >= 2 * nr;
-    std::vector<int64_t> lorder;  // layout chunk -> bin chunk (ilv)
     std::vector<int32_t> rrow{0}, rchunk{0};
     int64_t acc = 0;
-    if (ilv) {
-        lorder.reserve(nch);
-        for (int64_t r = 0; r < nr; r++) {
-            for (int64_t c = r; c < nch; c += nr) {
-                lorder.push_back(c);
-                acc += cr[c];
-            }
-            if (r + 1 < nr) {
-                rrow.push_back((int32_t)acc);
-                rchunk.push_back((int32_t)lorder.size());
-            }
-        }
-    } else {
-        for (int64_t c = 0; c < nch; c++) {
-            acc += cr[c];
-            // a table-mapped bin keeps <= kSlotOutEntries segments per range (their y offsets sit in LDS)
-            const bool full = split > 1 || (!affine && (int64_t)(c + 2 - rchunk.back()) * RPI > kSlotOutEntries);
-            if (c + 1 < nch && (full || ((int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows))) {
-                rrow.push_back((int32_t)acc);
-                rchunk.push_back((int32_t)(c + 1));
-            }
+    for (int64_t c = 0; c < nch; c++) {
+        acc += cr[c];
+        // a table-mapped bin keeps <= kSlotOutEntries segments per range (their y offsets sit in LDS)
+        const bool full = split > 1 || (!affine && (int64_t)(c + 2 - rchunk.back()) * RPI > kSlotOutEntries);
+        if (c + 1 < nch && (full || ((int64_t)rrow.size() < nr && acc * nr >= (int64_t)rrow.size() * rows))) {
+            rrow.push_back((int32_t)acc);
+            rchunk.push_back((int32_t)(c + 1));
         }
     }
     rrow.push_back((int32_t)rows);
     nr = (int64_t)rchunk.size();
     if (layout_knob("VBC_VERBOSE"))
         fprintf(stderr, "[vbc] slot bin kind %d w %d planar %d pair %d run %d split %d chunks %lld rows %lld ranges %lld "
-                "(target share %.0f) interleaved %d\n", kind, w, (int)planar, (int)pair, run, split, (long long)nch,
-                (long long)rows, (long long)nr, share, (int)ilv);
+                "(target share %.0f)\n", kind, w, (int)planar, (int)pair, run, split, (long long)nch, (long long)rows,
+                (long long)nr, share);
     ps = PendingSlot{};
     SlotBin &b = ps.b;
     b.kind = kind;
@@ -588,7 +565,6 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
     b.split = split;
     b.pair = pair ? 1 : 0;
     b.mask = (mask && planar && split == 1 && (!pair || h->planar_mask_pair)) ? 1 : 0;
-    b.ilv = ilv ? (int32_t)nr : 0;
     b.holes = holes ? 1 : 0;
     if (holes && (split == 1 || pair)) return fail(VBC_INVALID_ARG, "internal: runs with holes need the split product");
     if (planar && split > 1) {
@@ -676,8 +652,7 @@ static int build_slots(vbc_handle *h, int kind, int w, int wsrc, const std::vect
             }
         }
     }
-    for (int64_t lc = 0; lc < (pair ? 0 : nch); lc++) {
-        const int64_t c = ilv ? lorder[lc] : lc;  // the bin chunk stored at layout position lc
+    for (int64_t c = 0; c < (pair ? 0 : nch); c++) {
         for (int32_t qr = 0; qr < cr[c]; qr++, row++) {
             const uint32_t last = qr + run == cr[c] ? kLast : 0u;  // on the last run's first row
             if (b.mask) {  // live lanes of this chunk row: a prefix in chunk-local length order
@@ -2840,7 +2815,6 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
     if (const char *e = layout_knob("VBC_XCD_P")) h->xcd_p = atoi(e) != 0;
     if (const char *e = layout_knob("VBC_SLOT_KEYS16")) h->slot_keys16 = atoi(e);  // 0 off, 1 auto, 2 always
     if (const char *e = layout_knob("VBC_SLOT_DEDUP")) h->slot_dedup = atoi(e) != 0;
-    if (const char *e = layout_knob("VBC_SLOT_ILV")) h->slot_ilv = atoi(e) != 0;
     if (const char *e = layout_knob("VBC_SWEEP")) h->sweep_mode = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     h->sweep_tile = (h->esz == 8 ? 4 : 2) * kSweepTileBytes;  // measured on NS: fp64 32 KB 473 us (16 KB 508), fp32 16 KB 313 us (32 KB 353)
     // packed swept keys: NS fp64 464.5 -> 456.2 us, mixed widths 553 -> 539 us; fp32 311 -> 316 us, so

@@ -149,7 +149,6 @@ struct vbc_handle {
     int64_t slot_rows_padded_last = 0;
     int slot_u = 0;                   // rows per step of the slotted kernel (VBC_SLOT_U)
     bool slot_dedup = true;           // VBC_SLOT_DEDUP=0: one stored delta pattern per compressed row
-    int slot_ilv = 0;                 // VBC_SLOT_ILV=1: slotted B'x chunks interleaved over the ranges (SlotBin::ilv)
     int slot_keys16 = 1;              // VBC_SLOT_KEYS16: 0 keep 32-bit keys, 1 auto, 2 compress whenever possible
     int fork = 1;                     // VBC_FORK=0: B'x launch groups queue on the caller's stream (Launch::fork_*)
     int slot_stage = -1;              // VBC_SLOT_STAGE = 0 / 4 / 8: chunks staged in LDS per y write (-1 auto)

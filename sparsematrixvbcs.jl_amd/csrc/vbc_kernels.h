@@ -135,8 +135,7 @@ struct SlotBin {
     const int16_t *lseg;   // ntiles * 64: lane's first segment inside its tile (== stripes of the tile: none)
     int32_t dot;           // pair layout of a forward product (vbc_planar.h run_pair DOT): per block, each output
                            // row's dot product with the x slice is added to its sum (the reference's forward order)
-    int32_t ilv;           // slotted B'x: > 0 = the bin's chunks interleaved over its ranges -- range r holds chunks
-                           // r, r + ilv, r + 2 ilv, ... (ilv = nranges), stored range-major (vbc_device.hip build_slots)
+    int32_t pad_dot;
 };
 
 // Runs with holes (SlotBin::holes): the run's stored-row mask above the gather index of its first key.

@@ -108,23 +108,7 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
 
     // Staged chunks [cfirst, cfirst + nbuf) -> y: one contiguous run (kind 0: RPI * w values per
     // chunk, kind 1: RPI), valid segments only.
-    // the bin chunk (y position) of layout chunk cc: interleaved bins store range r's chunks r, r + ilv, ...
-    auto bin_chunk = [&](int cc) { return b.ilv > 0 ? r + (cc - c0) * b.ilv : cc; };
     auto write_out = [&]() {
-        if constexpr (KIND == 0 && NB > 0) {
-            if (b.ilv > 0) {  // interleaved (contig) bins: each staged chunk's RPI x w outputs to its own place
-                typedef T vt __attribute__((ext_vector_type(V)));
-#pragma nounroll
-                for (int i = 0; i < nbuf; i++) {
-                    const int seg = bin_chunk(cfirst + i) * RPI + slot;
-                    if (active && seg < b.nseg)
-                        *(gptr<vt>)(G(y) + b.out_base + (int64_t)seg * b.out_stride + sub * V) =
-                            *reinterpret_cast<const vt *>(lds_wave + ((size_t)i * 64 + lane) * V * sizeof(T));
-                }
-                nbuf = 0;
-                return;
-            }
-        }
         const int64_t segs = min((int64_t)nbuf * RPI, (int64_t)b.nseg - (int64_t)cfirst * RPI);
         const int64_t bytes = segs * (KIND == 0 ? w : 1) * (int64_t)sizeof(T);
         char *dst = reinterpret_cast<char *>(y + b.out_base + (int64_t)cfirst * RPI * b.out_stride);
@@ -144,8 +128,9 @@ __device__ __forceinline__ void run_slots(const SlotBin &b, int r, int lane, con
         }
         nbuf = 0;
     };
+
     auto flush = [&]() {
-        const int seg = bin_chunk(c) * RPI + slot;
+        const int seg = c * RPI + slot;
         const bool ok = active && seg < b.nseg;
         if constexpr (NB > 0) {
             if constexpr (KIND == 0) {
