@@ -182,10 +182,21 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
     // lane j of the row holds the key of step t0 + j, j < 2 NBT (the bin carries padding past its end)
     static_assert(2 * NBT <= 16 && D >= 2, "one key load covers two batches of a 16-lane row");
     auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < 2 * NBT ? j : 2 * NBT - 1)]; };
+    // The batch's NBT * TV values of the row: the lanes of the last load past them (fp32 3 x 3, NBT = 8: 14 of
+    // its 16) read lane 0's address instead of the next batch's values -- a segment the load touches anyway
+    // -- so the load touches 1 segment instead of 4 (the kernel is bound by the 64-B segments its loads touch,
+    // 4.9 -> 4.5 per tile); their registers are never read (the fold's source lanes are < NBT TV)
     auto load_vals = [&](int t0, tv (&V)[NV]) {
-        const gptr<const T> p = val + (kb + t0) * TV + j * EPL;
+        const gptr<const T> p = val + (kb + t0) * TV;
 #pragma unroll
-        for (int v = 0; v < NV; v++) V[v] = __builtin_nontemporal_load((gptr<const tv>)(p + v * PER));
+        for (int v = 0; v < NV; v++) {
+#ifdef VBC_TILE_VALS_ALL  // (A/B build, tools/exp/build_variant.sh: every lane loads its own 16 B)
+            const int jj = j;
+#else
+            const int jj = v * PER + j * EPL < NBT * TV ? j : 0;
+#endif
+            V[v] = __builtin_nontemporal_load((gptr<const tv>)(p + v * PER + jj * EPL));
+        }
     };
     auto load_x = [&](uint32_t K, int k0, T (&xs)[NBT][UB]) {
 #pragma unroll
