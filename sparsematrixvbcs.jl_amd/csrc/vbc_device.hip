@@ -2011,6 +2011,58 @@ struct PendingPanel {
 // padded to the longest with invalid tiles.  Returns false (nothing built) when the bucket does not fit:
 // a tile taller than 4 rows, too much padding, too few rows per tile (auto), rows >= 2^26.
 constexpr double kTilePad = 1.25;
+
+// Launch order of the tile ranges (round 6): BFS balls of K ranges over the graph "two ranges store a tile of
+// the same X row group", ball after ball.  Each XCD takes a contiguous run of the launch's ranges and keeps
+// about K of them resident (K = one XCD's share of the wave slots), so at any moment it folds one ball: a
+// compact region of the operator whose X rows -- its groups plus one layer -- fit the XCD's 4 MB L2, where
+// the natural order's resident ranges form a slab of consecutive stripes whose X window (a 3D mesh's +-g^2
+// rows) does not.  Only the order changes: every range keeps its stripes, streams and data.
+// rg_off / rg_grp: the distinct row groups of each range (CSR, ranges in natural order).
+static std::vector<int64_t> cluster_ranges(int64_t nrg, const std::vector<int64_t> &rg_off,
+                                           const std::vector<int32_t> &rg_grp, int64_t ngroups, int64_t K)
+{
+    std::vector<int64_t> gcnt(ngroups + 1, 0);  // row group -> ranges (CSR)
+    for (int32_t g : rg_grp) gcnt[g + 1]++;
+    for (int64_t g = 0; g < ngroups; g++) gcnt[g + 1] += gcnt[g];
+    std::vector<int32_t> grg(rg_grp.size());
+    {
+        std::vector<int64_t> pos(gcnt.begin(), gcnt.end() - 1);
+        for (int64_t r = 0; r < nrg; r++)
+            for (int64_t q = rg_off[r]; q < rg_off[r + 1]; q++) grg[pos[rg_grp[q]]++] = (int32_t)r;
+    }
+    std::vector<int64_t> order;
+    order.reserve(nrg);
+    std::vector<char> done(nrg, 0), gseen(ngroups, 0);
+    std::vector<int64_t> touched;  // groups expanded by the current ball (reset after it)
+    int64_t seed = 0;
+    while ((int64_t)order.size() < nrg) {
+        while (done[seed]) seed++;
+        const size_t b0 = order.size();
+        order.push_back(seed);
+        done[seed] = 1;
+        for (size_t h = b0; h < order.size() && (int64_t)(order.size() - b0) < K; h++) {
+            const int64_t r = order[h];
+            for (int64_t q = rg_off[r]; q < rg_off[r + 1] && (int64_t)(order.size() - b0) < K; q++) {
+                const int32_t g = rg_grp[q];
+                if (gseen[g]) continue;
+                gseen[g] = 1;
+                touched.push_back(g);
+                for (int64_t t = gcnt[g]; t < gcnt[g + 1] && (int64_t)(order.size() - b0) < K; t++) {
+                    const int32_t r2 = grg[t];
+                    if (!done[r2]) {
+                        done[r2] = 1;
+                        order.push_back(r2);
+                    }
+                }
+            }
+        }
+        for (int64_t g : touched) gseen[g] = 0;
+        touched.clear();
+    }
+    return order;
+}
+
 static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64_t> &stripes_in, int w,
                         const std::vector<int64_t> *tgrp, const char *val, Arena &ar, PendingPanel &pp)
 {
@@ -2207,6 +2259,13 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
     std::fill(key, key + slot_total + kpad, kTileRow);  // padding: invalid tiles (row field all ones)
     std::memset(vv, 0, (size_t)(slot_total * TV + vpad) * esz);
     bool masku = false;
+    // the distinct X row groups of each range (cluster_ranges): group = block row (tgrp) or row / R
+    const int64_t K = std::max<int64_t>(1, slots / 8);
+    const bool cluster = h->tile_cluster && nrg >= 4 * K;
+    const int64_t ngroups = R == 0 ? (int64_t)tgrp->size() : s.m / R + 1;
+    std::vector<int64_t> rg_off{0};
+    std::vector<int32_t> rg_grp, last;
+    if (cluster) last.assign((size_t)ngroups, -1);
     for (int64_t r = 0; r < nrg; r++) {
         const int32_t *ri = &rinfo[(size_t)r * 8];
         const int64_t len = ri[1];
@@ -2227,6 +2286,13 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
                     const int rr = (int)(s.rows[q] - base);
                     const unsigned bit = 1u << rr;
                     if (base != cb || (seen & bit)) {
+                        if (cluster) {
+                            const int64_t gi = R == 0 ? gk[base] : base / R;
+                            if (last[gi] != r) {
+                                last[gi] = (int32_t)r;
+                                rg_grp.push_back((int32_t)gi);
+                            }
+                        }
                         if (cb >= 0) {
                             key[slot] = (uint32_t)kbase | kTileValid | (seen << kTileMaskShift);
                             masku = masku || seen != (1u << ub) - 1;
@@ -2245,13 +2311,19 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
                 slot++;
             }
         }
+        if (cluster) rg_off.push_back((int64_t)rg_grp.size());
+    }
+    if (cluster) {  // launch the ranges ball by ball (the arena's rinfo rows permuted; the data stays put)
+        const std::vector<int64_t> ord = cluster_ranges(nrg, rg_off, rg_grp, ngroups, K);
+        int32_t *dst = ar.at<int32_t>(pp.o_rgrp);
+        for (int64_t q = 0; q < nrg; q++) std::memcpy(dst + q * 8, &rinfo[(size_t)ord[q] * 8], 8 * sizeof(int32_t));
     }
     tb.masku = masku ? 1 : 0;
     h->bytes_m += slot_total * (4 + (int64_t)TV * esz) + nrg * 32;
     if (layout_knob("VBC_VERBOSE"))
-        fprintf(stderr, "[vbc] tiles: w %d, %lld stripes, %lld rows -> %lld tiles of <= %d rows (%s), %lld ranges, %lld slots%s\n",
+        fprintf(stderr, "[vbc] tiles: w %d, %lld stripes, %lld rows -> %lld tiles of <= %d rows (%s), %lld ranges, %lld slots%s%s\n",
                 w, (long long)n, (long long)rows, (long long)total, ub, R == 0 ? "block rows" : "row runs", (long long)nrg,
-                (long long)slot_total, masku ? ", masked rows" : "");
+                (long long)slot_total, masku ? ", masked rows" : "", cluster ? ", clustered launch order" : "");
     return true;
 }
 
@@ -2884,6 +2956,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = layout_knob("VBC_PANEL_TILES")) h->panel_tiles = atoi(e) < 0 ? -1 : atoi(e) != 0;
         if (const char *e = tuning_knob("VBC_TILE_NBT")) h->tile_nbt = atoi(e) >= 8 ? 8 : 4;
         if (const char *e = tuning_knob("VBC_TILE_SPR")) h->tile_spr = std::max(1, atoi(e));
+        if (const char *e = layout_knob("VBC_TILE_CLUSTER")) h->tile_cluster = atoi(e) != 0;
         if (const char *e = tuning_knob("VBC_TILE_DEPTH")) h->tile_depth = atoi(e) == 3 ? 3 : 2;
         h->occ_tiles = occupancy_tiles(h->esz);
     }
