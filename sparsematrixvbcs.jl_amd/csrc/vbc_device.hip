@@ -2260,8 +2260,9 @@ static bool build_tiles(vbc_handle *h, const Stripes &s, const std::vector<int64
     std::memset(vv, 0, (size_t)(slot_total * TV + vpad) * esz);
     bool masku = false;
     // the distinct X row groups of each range (cluster_ranges): group = block row (tgrp) or row / R
-    const int64_t K = std::max<int64_t>(1, slots / 8);
-    const bool cluster = h->tile_cluster && nrg >= 4 * K;
+    // (VBC_TILE_CLUSTER=2: any range count, balls of an eighth of the ranges -- small-scale tests)
+    const int64_t K = h->tile_cluster == 2 ? std::max<int64_t>(1, nrg / 8) : std::max<int64_t>(1, slots / 8);
+    const bool cluster = h->tile_cluster == 2 ? nrg >= 2 : h->tile_cluster && nrg >= 4 * K;
     const int64_t ngroups = R == 0 ? (int64_t)tgrp->size() : s.m / R + 1;
     std::vector<int64_t> rg_off{0};
     std::vector<int32_t> rg_grp, last;
@@ -2956,7 +2957,7 @@ static int create_common(vbc_handle **out, Stripes &s, const void *val, int dtyp
         if (const char *e = layout_knob("VBC_PANEL_TILES")) h->panel_tiles = atoi(e) < 0 ? -1 : atoi(e) != 0;
         if (const char *e = tuning_knob("VBC_TILE_NBT")) h->tile_nbt = atoi(e) >= 8 ? 8 : 4;
         if (const char *e = tuning_knob("VBC_TILE_SPR")) h->tile_spr = std::max(1, atoi(e));
-        if (const char *e = layout_knob("VBC_TILE_CLUSTER")) h->tile_cluster = atoi(e) != 0;
+        if (const char *e = layout_knob("VBC_TILE_CLUSTER")) h->tile_cluster = atoi(e) == 2 ? 2 : atoi(e) != 0;
         if (const char *e = tuning_knob("VBC_TILE_DEPTH")) h->tile_depth = atoi(e) == 3 ? 3 : 2;
         h->occ_tiles = occupancy_tiles(h->esz);
     }

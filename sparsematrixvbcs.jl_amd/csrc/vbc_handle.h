@@ -116,7 +116,8 @@ struct vbc_handle {
     int occ_tiles = 24;           // resident waves per CU of the tile kernel (the layout's range count)
     int tile_nbt = vbc::kTileBatch;  // VBC_TILE_NBT: tiles per stream per pipeline stage of the tile kernel (4 / 8)
     int tile_depth = 2;  // VBC_TILE_DEPTH (VBC_ABLATION build): register sets of the tile kernel's pipeline (2 / 3)
-    int tile_cluster = 1;             // VBC_TILE_CLUSTER=0: tile ranges launched in natural stripe order (no X-locality balls)
+    int tile_cluster = 1;             // VBC_TILE_CLUSTER=0: tile ranges launched in natural stripe order (no X-locality balls);
+                                      // 2: balls at any range count (tests)
     int tile_spr = vbc::kTileStripes;  // VBC_TILE_SPR: stripes per range (wave) of the tile layout
     int64_t panel_val_bytes = 0;  // largest bin val array of the panel layout
     vbc::IntLayout li;            // integer eltypes (dtype VBC_I64): exact wrapping products

@@ -318,6 +318,34 @@ def test_tiles_node_runs_with_holes_exact_and_nonfinite(multi_layout):
     assert np.array_equal(got[fin], ref[fin])
 
 
+def test_tiles_clustered_launch_order_bitwise(multi_layout, monkeypatch):
+    """The tile layout's clustered launch order (VBC_TILE_CLUSTER: ranges taken as BFS balls over shared X row
+    groups) changes only which wave folds which range when: at small scale, forced on
+    (2) against off (0), both directions, the products are bit-identical and equal the oracle's on integer data."""
+    import bench
+    B = bench.build_matrix("c5-mesh", np.float32, 0.01)
+    B.val[:] = np.random.default_rng(5).integers(-8, 9, B.val.shape)
+    Rd = ref_2d(B)
+    Rd.val = Rd.val.astype(np.float64)
+    rng = np.random.default_rng(12)
+    for trans in (True, False):
+        nx, ny = (B.m, B.n) if trans else (B.n, B.m)
+        X = rng.integers(-8, 9, (nx, 16)).astype(np.float32)
+        got = {}
+        for mode in ("0", "2"):
+            monkeypatch.setenv("VBC_TILE_CLUSTER", mode)
+            Bm = bench.build_matrix("c5-mesh", np.float32, 0.01)  # a fresh handle per mode (create-time knob)
+            Bm.val[:] = B.val
+            Yd = torch.empty((ny, 16), dtype=torch.float32, device=DEV)
+            V.mul_(Yd, Bm.T if trans else Bm, torch.from_numpy(X).to(DEV), engine="mfma")
+            got[mode] = Yd.cpu().numpy()
+            Bm.release()
+        want = np.stack([O.mul(Rd, np.ascontiguousarray(X[:, j], dtype=np.float64), np.zeros(ny), 1.0, 0.0, trans=trans,
+                               ref_semantics=False) for j in range(16)], axis=1)
+        assert np.array_equal(got["0"], got["2"]), trans
+        assert np.array_equal(got["2"], want.astype(np.float32)), trans
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_c5_mesh_integer_bitwise(dtype, multi_layout):
     """The structured C5 input (3 x 3 node tiles) at small scale, 16 row-major right-hand sides, both directions
