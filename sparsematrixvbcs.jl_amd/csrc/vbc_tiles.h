@@ -183,9 +183,10 @@ __global__ __launch_bounds__(kBlockThreads) void spmm_tiles(const TileBin b, con
     static_assert(2 * NBT <= 16 && D >= 2, "one key load covers two batches of a 16-lane row");
     auto load_keys = [&](int t0) -> uint32_t { return key[kb + t0 + (j < 2 * NBT ? j : 2 * NBT - 1)]; };
     // The batch's NBT * TV values of the row: the lanes of the last load past them (fp32 3 x 3, NBT = 8: 14 of
-    // its 16) read lane 0's address instead of the next batch's values -- a segment the load touches anyway
-    // -- so the load touches 1 segment instead of 4 (the kernel is bound by the 64-B segments its loads touch,
-    // 4.9 -> 4.5 per tile); their registers are never read (the fold's source lanes are < NBT TV)
+    // its 16) read lane 0's address -- a segment the load touches anyway; their registers are never read (the
+    // fold's source lanes are < NBT TV).  They used to fetch the next batch's first values, which the
+    // non-temporal stream had evicted again by the time that batch loaded them: ~40 % of the value bytes came
+    // from HBM twice (c5-mesh FETCH_SIZE 785 -> 639 MB per product, 303 -> 270.5 us)
     auto load_vals = [&](int t0, tv (&V)[NV]) {
         const gptr<const T> p = val + (kb + t0) * TV;
 #pragma unroll
